@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""bench.py — Gram pairs/s of the MI355X string-kernel Gram engine.
+
+Workload (BASELINE.json configs[1]): spectrum k=8 Gram of N=20000 synthetic DNA
+sequences of length L=101 on one MI355X, int32 exact counts, device-resident
+(input codes already in HBM when the timed region starts).  A "step" is one full
+Gram build: k-mer extraction + posting-index build + Gram kernel over the rank's rows.
+
+Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`):
+one process per GPU, rows of K sharded across ranks with no data-path collective;
+weak scaling — N = 20000*sqrt(G) so every rank computes the same 20000^2 Gram pairs
+(rows N/G x N columns).  `value` = N^2 / max-over-ranks time.  `--allgather` adds the
+RCCL all-gather that assembles K on every GPU (reported separately).
+
+Also reported: the mismatch (k=9, m=1) Gram at the same N (BASELINE configs[2],
+float64 normalised, exact), per-stage device times from HIP events, the HBM roofline
+of the dominant kernel and the oracle timed on the host cores (cpu_baseline).
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kernel-methods-for-genomics_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+from kmgram import _lib as L  # noqa: E402
+from kmgram import encode as E  # noqa: E402
+from kmgram import params as P  # noqa: E402
+
+HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
+          "(k=9,m=1), 1/2/4/8 GPUs")
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")  # barrier / max on the host, no device traffic
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def even_splits(n, parts):
+    return [n * r // parts for r in range(parts + 1)]
+
+
+def run_workload(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, allgather):
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    splits = even_splits(n, dist.world)
+    r0, r1 = splits[dist.rank], splits[dist.rank + 1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    d_codes = ctx.dmalloc(codes.nbytes)
+    d_lens = ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    full_rows = n if allgather else (r1 - r0)
+    d_out = ctx.dmalloc(full_rows * n * esz)
+    out_rows = ctypes.c_void_p(d_out.value + (r0 * n * esz if allgather else 0))
+
+    def step():
+        ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, out_rows, n)
+
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    ctx.set_timing(True)
+    ctx.timing_reset()
+    dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    ctx.set_timing(False)
+    wall = dist.max(t1 - t0)
+    stages = {}
+    for st in ("extract", "scan", "scatter", "diag", "gram"):
+        tot, cnt = ctx.stage_stats(st)
+        if cnt:
+            stages[st] = round(tot / cnt, 5)
+    res = {
+        "name": name, "n": n, "rows": r1 - r0, "wall_s": wall, "steps": steps,
+        "ms_per_step": wall / steps * 1e3, "pairs_per_s": n * n / (wall / steps),
+        "stages_ms": stages, "gram_kernel_ms": stages.get("gram"),
+    }
+    if allgather and dist.world > 1:
+        uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
+        ctx.comm_init(uid, dist.world, dist.rank)
+        ctx.allgather_rows(d_out, n, n, out_dtype, splits)  # warm
+        ctx.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+            ctx.allgather_rows(d_out, n, n, out_dtype, splits)
+        ctx.synchronize()
+        dist.barrier()
+        ag = dist.max(time.perf_counter() - t0)
+        res["with_allgather_ms_per_step"] = ag / steps * 1e3
+        res["with_allgather_pairs_per_s"] = n * n / (ag / steps)
+        ctx.comm_destroy()
+    # small parity spot-check of the measured output (first row of this rank vs oracle)
+    res["spot_check"] = spot_check(ctx, name, codes, lens, n, r0, out_rows, out_dtype)
+    ctx.dfree(d_out)
+    ctx.dfree(d_codes)
+    ctx.dfree(d_lens)
+    return res
+
+
+def spot_check(ctx, name, codes, lens, n, r0, d_rows, out_dtype):
+    try:
+        import cref
+    except Exception:
+        return None
+    row = np.empty(n, dtype=L.DTYPES[out_dtype])
+    ctx.d2h(row, d_rows)
+    if name == "spectrum_k8":
+        ref = cref.spectrum(codes, lens, 8, rows=(r0, r0 + 1))[0]
+        return bool(np.array_equal(row.astype(np.int64), ref))
+    ref = cref.mismatch_rows(codes, lens, 9, 1, rows=(r0, r0 + 1))[0]
+    return bool(np.array_equal(row, ref))
+
+
+def cpu_baseline(name, n, budget_s):
+    """The C oracle (oracle/kmg_oracle.c, OpenMP) on a bounded row sample of the same
+    workload, on this box's host cores."""
+    import cref
+    cref.load()
+    cores = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
+    seed = 2 if name == "spectrum_k8" else 3
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    fn = ((lambda r: cref.spectrum(codes, lens, 8, rows=(0, r))) if name == "spectrum_k8"
+          else (lambda r: cref.mismatch_raw(codes, lens, 9, 1, rows=(0, r))))
+    r = 8
+    while True:
+        t0 = time.perf_counter()
+        fn(r)
+        t = time.perf_counter() - t0
+        if t >= budget_s / 4 or r >= n:
+            break
+        r = min(n, max(r * 2, int(r * (budget_s / 4) / max(t, 1e-3))))
+    rows = min(n, max(r, int(r * budget_s / max(t, 1e-6))))
+    t0 = time.perf_counter()
+    fn(rows)
+    t = time.perf_counter() - t0
+    return {"value": rows * n / t, "unit": "Gram pairs/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/kmg_oracle.c {'kmo_spectrum' if name == 'spectrum_k8' else 'kmo_mismatch_raw'}"
+                      f" rows 0..{rows} x {n} columns ({rows * n} pairs) in {t:.2f} s, "
+                      f"{cores} OpenMP threads"}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed PMC pass (profiles/*pmc*.json), if any."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            best = d["hbm_bytes_per_launch"]
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=20000, help="sequences at 1 GPU (weak-scaled)")
+    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-mismatch", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    args = ap.parse_args()
+
+    dist = Dist()
+    if dist.world != args.gpus and dist.rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
+    ctx = L.Context(dist.local)
+    n = int(round(args.n * math.sqrt(dist.world) / 8.0)) * 8 if dist.world > 1 else args.n
+
+    sp = run_workload(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
+                      args.steps, args.warmup, args.allgather)
+    mm = None
+    if not args.no_mismatch:
+        mm = run_workload(ctx, dist, "mismatch_k9_m1",
+                          P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
+                          n, 3, max(3, args.steps // 4), 1, args.allgather)
+    ctx.close()
+
+    rows = sp["rows"]
+    alg_bytes = 4.0 * rows * n + 26.0 * n  # int32 K write + 2-bit packed input
+    kern_s = sp["gram_kernel_ms"] / 1e3
+    achieved = alg_bytes / kern_s
+    traffic = load_traffic("spectrum_k8")
+    roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "kernel": "kmg::gram_sp_kernel<true,1>", "kernel_ms": sp["gram_kernel_ms"],
+            "alg_bytes_per_launch": alg_bytes}
+
+    line = {
+        "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
+        "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": sp["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(2)",
+        "config": {"workload": "spectrum k=8 Gram, N=20000 x L=101 per GPU-share "
+                               "(BASELINE configs[1]); weak-scaled N=20000*sqrt(G)",
+                   "N": n, "L": 101, "k": 8, "rows_per_rank": rows,
+                   "parallelism": f"row-shard x{dist.world}", "out_dtype": "int32",
+                   "full_k_build_ms": sp["ms_per_step"]},
+        "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],
+    }
+    if "with_allgather_ms_per_step" in sp:
+        line["allgather"] = {k: sp[k] for k in ("with_allgather_ms_per_step",
+                                                "with_allgather_pairs_per_s")}
+    if mm:
+        mm_rows = mm["rows"]
+        mm_bytes = 8.0 * mm_rows * n + 26.0 * n
+        line["secondary"] = {
+            "workload": "mismatch (k=9,m=1) Gram, float64 normalised (BASELINE configs[2])",
+            "N": n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
+            "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
+            "hbm_frac_of_gram_kernel": (mm_bytes / (mm["gram_kernel_ms"] / 1e3)) / HBM_PEAK,
+            "spot_check": mm["spot_check"],
+        }
+    if dist.world == 1 and dist.rank == 0 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
+        if mm:
+            line["secondary"]["cpu_baseline"] = cpu_baseline("mismatch_k9_m1", n,
+                                                             args.cpu_budget / 2)
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

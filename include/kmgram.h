@@ -1,0 +1,152 @@
+/*
+ * kmgram.h — C ABI of libkmgram.so, the MI355X (gfx950) string-kernel Gram engine.
+ *
+ * This is the drop-in boundary for the Gram-matrix hot path of
+ * afiliot/Kernel-Methods-For-Genomics `kernels.py`.  The reference boundary is
+ * pure Python (`kernels.select_method(X, method) -> np.ndarray`, kernels.py:461-505);
+ * its Python mirror (`kernel-methods-for-genomics_amd/kernels.py`) calls the
+ * entry points below through ctypes.  Every entry point cites the reference
+ * interface it replaces.
+ *
+ * Conventions
+ *   - Status: every function returns int; 0 (KMG_OK) on success.  No C++ exception
+ *     or abort crosses the ABI.  kmg_last_error() gives a thread-local message.
+ *   - Sequences enter as symbol codes, uint8 [n][ldc] row-major, plus int32 lengths.
+ *     'A','C','G','T' -> 0,1,2,3.  Any other character -> a code >= 4 (distinct
+ *     characters get distinct codes, so WD/WDS/SS character equality is preserved;
+ *     spectrum treats codes >= 4 as "k-mer matches no beta", kernels.py:21-24).
+ *   - Ownership: the caller owns every buffer it passes.  The context owns all
+ *     device workspace and keeps no caller pointer after a call returns.
+ *   - Threading: a context is not re-entrant (internal mutex); one context per
+ *     device; one process per GPU for multi-GPU (RCCL communicator per context).
+ */
+#ifndef KMGRAM_H
+#define KMGRAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMG_ABI_VERSION 1
+
+/* status codes */
+enum {
+  KMG_OK = 0,
+  KMG_EINVAL = 1,       /* bad argument (shape, range, alphabet) */
+  KMG_EUNSUPPORTED = 2, /* parameter combination not implemented on device */
+  KMG_EHIP = 3,         /* HIP runtime error */
+  KMG_ENOMEM = 4,       /* device allocation failed */
+  KMG_ERCCL = 5,        /* RCCL error */
+  KMG_ENODEV = 6        /* no HIP device visible */
+};
+
+/* kernel families (one per reference get_*_K) */
+enum {
+  KMG_SPECTRUM = 1,   /* get_spectrum_K   kernels.py:28-47   */
+  KMG_MISMATCH = 2,   /* get_mismatch_K   kernels.py:196-217 */
+  KMG_WD = 3,         /* get_WD_K         kernels.py:84-101  */
+  KMG_WDS = 4,        /* get_WDShifts_K   kernels.py:138-155 */
+  KMG_SUBSTRING = 5,  /* get_string_K     kernels.py:367-382 */
+  KMG_LOCALALIGN = 6, /* get_LA_K         kernels.py:273-302 */
+  KMG_GAPPY = 7       /* get_gappy_K      kernels.py:436-455 (k=1,g=0 only: every other
+                         (k,g) raises in the reference under numpy 2) */
+};
+
+/* output element types */
+enum { KMG_I32 = 1, KMG_F32 = 2, KMG_F64 = 3 };
+
+/* LA modes */
+enum { KMG_LA_REFERENCE = 0 /* bit-for-bit the reference: all zeros (kernels.py:238,262) */,
+       KMG_LA_INTENDED = 1  /* aliasing fixed, report §3.5 recurrence; parity unpinned */ };
+
+#define KMG_MAX_COEF 64
+
+typedef struct kmg_params {
+  int32_t kind;      /* KMG_* family */
+  int32_t k;         /* SP/MM/GP k-mer length; SS subsequence length */
+  int32_t m;         /* MM maximal mismatches */
+  int32_t d;         /* WD/WDS maximal degree */
+  int32_t S;         /* WDS maximal shift */
+  int32_t g;         /* GP gap */
+  int32_t window;    /* MM/GP: fixed window the reference hard-codes (101, kernels.py:171,430) */
+  int32_t normalize; /* 1: fused normalize_K epilogue (kernels.py:398-415) */
+  int32_t smith;     /* LA: 1 = Smith_Waterman max form */
+  int32_t la_mode;   /* KMG_LA_REFERENCE / KMG_LA_INTENDED */
+  int32_t reserved[6];
+  double lambda;     /* SS lambda */
+  double lambda2;    /* SS lambda**2 exactly as the host language computes it */
+  double la_e, la_d, la_beta; /* LA gap open / extend / beta */
+  double coef_a[KMG_MAX_COEF]; /* WD/WDS: beta_k for k=1..d at [k-1] (kernels.py:53-61) */
+  double coef_b[KMG_MAX_COEF]; /* WDS: delta_s for s=0..S at [s]   (kernels.py:106-112) */
+  double diag_value; /* WD: the closed-form diagonal L-1+(1-d)/3 (kernels.py:96); NaN = per row */
+} kmg_params;
+
+typedef struct kmg_ctx kmg_ctx;
+
+int kmg_version(void);
+const char *kmg_last_error(void);
+int kmg_device_count(int *n);
+
+/* Create a context bound to one HIP device (one stream, workspace arena). */
+int kmg_create(kmg_ctx **ctx, int device_id);
+int kmg_destroy(kmg_ctx *ctx);
+
+/*
+ * Full Gram matrix, host buffers in and out (drop-in path).
+ * Replaces kernels.select_method / get_*_K (kernels.py:461-505 and the functions it
+ * dispatches to).  out: n x n, row stride ld_out elements, dtype out_dtype.
+ */
+int kmg_gram(kmg_ctx *ctx, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+             int64_t n, int64_t ldc, int32_t out_dtype, void *out, int64_t ld_out);
+
+/*
+ * Device-resident Gram rows [row0, row1) x all n columns (bench / multi-GPU path).
+ * d_codes/d_lens/d_out are device pointers (kmg_dmalloc).  d_out points at row row0.
+ * Runs on the context stream; returns without synchronising.
+ */
+int kmg_gram_device(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
+                    const int32_t *d_lens, int64_t n, int64_t ldc, int64_t row0, int64_t row1,
+                    int32_t out_dtype, void *d_out, int64_t ld_out);
+
+/* normalize_K (kernels.py:398-415) in place on a host float64 matrix, including the
+ * "K[0,0]==1 -> unchanged" rule (returns 1 in *skipped then). */
+int kmg_normalize(kmg_ctx *ctx, double *K, int64_t n, int64_t ld, int32_t *skipped);
+
+/* center_K (kernels.py:387-395): out = (I - 11^T/n) K (I - 11^T/n), float64 host buffers. */
+int kmg_center(kmg_ctx *ctx, const double *K, int64_t ldk, double *out, int64_t ld_out, int64_t n);
+
+/* device memory / stream helpers for device-resident callers */
+int kmg_dmalloc(kmg_ctx *ctx, void **ptr, size_t bytes);
+int kmg_dfree(kmg_ctx *ctx, void *ptr);
+int kmg_h2d(kmg_ctx *ctx, void *dst, const void *src, size_t bytes);
+int kmg_d2h(kmg_ctx *ctx, void *dst, const void *src, size_t bytes);
+int kmg_memset(kmg_ctx *ctx, void *dst, int value, size_t bytes);
+int kmg_synchronize(kmg_ctx *ctx);
+int kmg_stream(kmg_ctx *ctx, void **hip_stream);
+
+/* Per-stage device timings from HIP events recorded on the context stream around
+ * every launch while timing is enabled (kmg_set_timing(ctx,1)); nothing is
+ * synchronised until a stage time is read.  Stage names: "extract", "scan",
+ * "scatter", "diag", "gram".
+ *   kmg_stage_ms:    that stage in the last call (-1 if it did not run)
+ *   kmg_stage_stats: sum and count over every call since kmg_timing_reset */
+int kmg_set_timing(kmg_ctx *ctx, int32_t enable);
+int kmg_timing_reset(kmg_ctx *ctx);
+int kmg_stage_ms(kmg_ctx *ctx, const char *stage, double *ms);
+int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *count);
+
+/* RCCL (one rank per process / GPU).  id is an opaque 128-byte ncclUniqueId. */
+int kmg_comm_unique_id(uint8_t id[128]);
+int kmg_comm_init(kmg_ctx *ctx, const uint8_t id[128], int32_t nranks, int32_t rank);
+/* Assemble the full n x n K on every rank: rank r owns rows [splits[r], splits[r+1]). */
+int kmg_allgather_rows(kmg_ctx *ctx, void *d_K, int64_t n, int64_t ld, int32_t dtype,
+                       const int64_t *splits);
+int kmg_comm_destroy(kmg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMGRAM_H */

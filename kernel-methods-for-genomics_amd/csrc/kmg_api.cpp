@@ -1,0 +1,693 @@
+// kmg_api.cpp — C ABI of libkmgram.so (include/kmgram.h): context, device workspace,
+// parameter validation, dispatch to the HIP kernels, and the RCCL row all-gather.
+//
+// Reference entry points replaced (afiliot/Kernel-Methods-For-Genomics kernels.py):
+//   select_method 461-505 dispatches to
+//   get_spectrum_K 28-47, get_mismatch_K 196-217, get_WD_K 84-101,
+//   get_WDShifts_K 138-155, get_string_K 367-382, get_LA_K 273-302, get_gappy_K 436-455,
+//   normalize_K 398-415, center_K 387-395.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kmg_internal.h"
+
+using namespace kmg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define KMG_HIP(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return fail(_e == hipErrorOutOfMemory ? KMG_ENOMEM : KMG_EHIP, "%s failed: %s (%s:%d)", \
+                  #expr, hipGetErrorString(_e), __FILE__, __LINE__);                           \
+  } while (0)
+
+#define KMG_TRY(expr)          \
+  do {                         \
+    int _r = (expr);           \
+    if (_r != KMG_OK) return _r; \
+  } while (0)
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (want <= bytes) return KMG_OK;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      bytes = 0;
+    }
+    size_t alloc = want < 256 ? 256 : want;
+    hipError_t e = hipMalloc(&p, alloc);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(KMG_ENOMEM, "hipMalloc(%zu) failed: %s", alloc, hipGetErrorString(e));
+    }
+    bytes = alloc;
+    return KMG_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
+const char *kStageNames[] = {"extract", "scan", "scatter", "diag", "gram"};
+constexpr int kNumStages = 5;
+
+}  // namespace
+
+struct kmg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf kmers, hist, off, cursor, partials, ent, diagv, dsq, wtab;
+  DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
+  bool timing = false;
+  // per-stage event pairs of every timed call since the last reset (read after a sync)
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_log;
+  size_t ev_used = 0;
+  int last_call_first = 0;
+  int64_t wtab_host[33] = {};
+  bool wtab_valid = false;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+hipEvent_t pool_event(kmg_ctx *c) {
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[c->ev_used++];
+}
+
+struct StageTimer {
+  kmg_ctx *c;
+  hipEvent_t end = nullptr;
+  StageTimer(kmg_ctx *c_, int i) : c(c_) {
+    if (c->timing) {
+      hipEvent_t b = pool_event(c);
+      end = pool_event(c);
+      (void)hipEventRecord(b, c->stream);
+      c->ev_log.push_back({i, {b, end}});
+    }
+  }
+  ~StageTimer() {
+    if (end) (void)hipEventRecord(end, c->stream);
+  }
+};
+
+size_t dtype_size(int32_t dt) { return dt == KMG_F64 ? 8 : 4; }
+
+int64_t pow4(int e) { return (int64_t)1 << (2 * e); }
+
+// w_m(d): number of betas within Hamming distance m of two k-mers at distance d
+// (the closed form of <Phi_x, Phi_y> for get_phi_km, kernels.py:161-175)
+void mismatch_weights(int k, int m, int64_t *w) {
+  auto C = [](int n, int r) -> int64_t {
+    if (r < 0 || r > n) return 0;
+    int64_t v = 1;
+    for (int t = 1; t <= r; ++t) v = v * (n - r + t) / t;
+    return v;
+  };
+  for (int d = 0; d <= 32; ++d) w[d] = 0;
+  for (int d = 0; d <= k; ++d) {
+    int64_t tot = 0;
+    for (int i = 0; i <= k - d; ++i) {
+      int64_t p3 = 1;
+      for (int t = 0; t < i; ++t) p3 *= 3;
+      for (int a = 0; a <= d; ++a)
+        for (int b = 0; a + b <= d; ++b) {
+          const int c = d - a - b;
+          if (i + b + c > m || i + a + c > m) continue;
+          int64_t multi = C(d, a) * C(d - a, b);
+          tot += C(k - d, i) * p3 * multi * ((int64_t)1 << c);
+        }
+    }
+    w[d] = tot;
+  }
+}
+
+int check_params(const kmg_params *p, int64_t n, int64_t ldc, int32_t dt) {
+  if (!p) return fail(KMG_EINVAL, "params is NULL");
+  if (n < 0) return fail(KMG_EINVAL, "n < 0");
+  if (ldc <= 0 && n > 0) return fail(KMG_EINVAL, "ldc must be > 0");
+  if (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64)
+    return fail(KMG_EINVAL, "unknown out dtype %d", dt);
+  return KMG_OK;
+}
+
+// ----------------------------------------------------------------- posting index
+int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
+                int64_t ldc) {
+  const int64_t nb = g.nbins();
+  const int64_t items = g.n * g.pmax;
+  if ((double)items * g.copies >= 4294967295.0)
+    return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
+  KMG_TRY(c->kmers.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
+  KMG_TRY(c->hist.ensure(sizeof(uint32_t) * (size_t)nb));
+  KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
+  KMG_TRY(c->cursor.ensure(sizeof(uint32_t) * (size_t)nb));
+  KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nb)));
+  KMG_TRY(c->ent.ensure(sizeof(uint32_t) * (size_t)(items * g.copies > 0 ? items * g.copies : 1)));
+  {
+    StageTimer t(c, 0);
+    KMG_HIP(hipMemsetAsync(c->hist.p, 0, sizeof(uint32_t) * (size_t)nb, c->stream));
+    KMG_HIP(launch_extract(g, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(),
+                           c->hist.as<uint32_t>(), c->stream));
+  }
+  {
+    StageTimer t(c, 1);
+    KMG_HIP(launch_scan(c->hist.as<uint32_t>(), c->off.as<uint32_t>(), c->cursor.as<uint32_t>(),
+                        nb, c->partials.as<uint32_t>(), c->stream));
+  }
+  {
+    StageTimer t(c, 2);
+    KMG_HIP(launch_scatter(g, c->kmers.as<uint32_t>(), c->cursor.as<uint32_t>(),
+                           c->ent.as<uint32_t>(), c->stream));
+  }
+  return KMG_OK;
+}
+
+int env_or(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+void choose_chunks(IndexGeom &g, int max_chunk) {
+  if (g.n <= 0) {
+    g.chunk = 8;
+    g.nchunks = 1;
+    return;
+  }
+  const int64_t nch = (g.n + max_chunk - 1) / max_chunk;
+  int64_t ch = (g.n + nch - 1) / nch;
+  ch = (ch + 7) & ~7LL;
+  g.chunk = (int)ch;
+  g.nchunks = (int)((g.n + ch - 1) / ch);
+}
+
+int upload_wtab(kmg_ctx *c, const int64_t *w) {
+  if (c->wtab_valid && memcmp(c->wtab_host, w, sizeof(int64_t) * 33) == 0) return KMG_OK;
+  KMG_TRY(c->wtab.ensure(sizeof(int64_t) * 33));
+  memcpy(c->wtab_host, w, sizeof(int64_t) * 33);
+  c->wtab_valid = true;
+  KMG_HIP(hipMemcpyAsync(c->wtab.p, c->wtab_host, sizeof(int64_t) * 33, hipMemcpyHostToDevice,
+                         c->stream));
+  // pageable source: make the copy complete before the table can change
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int diag_hamming(kmg_ctx *c, const IndexGeom &g) {
+  KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
+  KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
+  StageTimer t(c, 3);
+  KMG_HIP(launch_diag_hamming(g, c->kmers.as<uint32_t>(), c->wtab.as<int64_t>(),
+                              c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+  return KMG_OK;
+}
+
+// ----------------------------------------------------------------- dispatch
+int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
+                int maxlen, int64_t n, int64_t ldc, int64_t row0, int64_t row1, int32_t dt,
+                void *d_out, int64_t ld) {
+  c->last_call_first = (int)c->ev_log.size();
+  if (row0 < 0 || row1 > n || row0 > row1) return fail(KMG_EINVAL, "bad row range");
+  if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
+  OutSpec o{d_out, ld, dt, 0, nullptr, nullptr};
+  const int64_t rows = row1 - row0;
+  switch (p->kind) {
+    case KMG_SPECTRUM:
+    case KMG_MISMATCH: {
+      const bool mm = p->kind == KMG_MISMATCH;
+      const int k = p->k;
+      if (k < 1 || k > 16) return fail(KMG_EUNSUPPORTED, "k=%d outside [1,16]", k);
+      if (mm && p->m < 0) return fail(KMG_EINVAL, "m < 0");
+      IndexGeom g{};
+      g.k = k;
+      g.n = n;
+      g.window = mm ? (p->window > 0 ? p->window : 101) : 0;
+      const int L = mm ? g.window : maxlen;
+      g.pmax = L - k + 1 > 0 ? L - k + 1 : 1;
+      if (g.pmax > 4095) return fail(KMG_EUNSUPPORTED, "more than 4095 k-mers per sequence");
+      int64_t w[33];
+      if (mm) {
+        mismatch_weights(k, p->m, w);
+      } else {
+        for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
+      }
+      const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
+      const bool s1 = mm && p->m == 1 && k >= 2 && k <= 12;  // drop-one-letter index
+      const bool use_index = (exact && k <= 12) || s1;
+      if (dt == KMG_I32 && p->normalize)
+        return fail(KMG_EINVAL, "normalised output needs a floating dtype");
+      if (!use_index) {
+        // all-pairs Hamming formulation (any m, k <= 16)
+        if (g.pmax > 256) return fail(KMG_EUNSUPPORTED, "Hamming path needs <= 256 k-mers");
+        g.copies = 1;
+        g.nkeys = 1;
+        g.chunk = (int)(n > 0 ? n : 1);
+        g.nchunks = 1;
+        KMG_TRY(c->kmers.ensure(sizeof(uint32_t) * (size_t)(n * g.pmax > 0 ? n * g.pmax : 1)));
+        KMG_TRY(c->hist.ensure(sizeof(uint32_t)));
+        {
+          StageTimer t(c, 0);
+          IndexGeom g0 = g;
+          g0.copies = 0;  // extract only: no histogram
+          KMG_HIP(launch_extract(g0, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(),
+                                 c->hist.as<uint32_t>(), c->stream));
+        }
+        KMG_TRY(upload_wtab(c, w));
+        if (p->normalize) {
+          KMG_TRY(diag_hamming(c, g));
+          o.normalize = 1;
+          o.diagv = c->diagv.as<double>();
+          o.dsq = c->dsq.as<double>();
+        }
+        StageTimer t(c, 4);
+        KMG_HIP(launch_gram_hamming(g, c->kmers.as<uint32_t>(), row0, row1,
+                                    c->wtab.as<int64_t>(), o, c->stream));
+        return KMG_OK;
+      }
+      if (exact) {
+        g.copies = 1;
+        g.nkeys = (uint32_t)pow4(k);
+        choose_chunks(g, env_or("KMG_SP_CHUNK", 24576));
+      } else {
+        g.copies = k;
+        g.nkeys = (uint32_t)pow4(k - 1);
+        choose_chunks(g, env_or("KMG_MM_CHUNK", 10240));
+      }
+      KMG_TRY(build_index(c, g, d_codes, d_lens, ldc));
+      if (p->normalize) {
+        KMG_TRY(upload_wtab(c, w));
+        KMG_TRY(diag_hamming(c, g));
+        o.normalize = 1;
+        o.diagv = c->diagv.as<double>();
+        o.dsq = c->dsq.as<double>();
+      }
+      StageTimer t(c, 4);
+      if (exact) {
+        KMG_HIP(launch_gram_spectrum(g, c->kmers.as<uint32_t>(), c->off.as<uint32_t>(),
+                                     c->ent.as<uint32_t>(), row0, row1, o, c->stream));
+      } else {
+        KMG_HIP(launch_gram_mismatch1(g, c->kmers.as<uint32_t>(), c->off.as<uint32_t>(),
+                                      c->ent.as<uint32_t>(), row0, row1, (int)w[0], (int)w[1],
+                                      (int)w[2], o, c->stream));
+      }
+      return KMG_OK;
+    }
+    case KMG_WD:
+    case KMG_WDS: {
+      if (p->d < 0 || p->d > KMG_MAX_COEF) return fail(KMG_EUNSUPPORTED, "d outside [0,64]");
+      if (p->kind == KMG_WDS && (p->S < 0 || p->S > 15))
+        return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
+      if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
+      SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+      StageTimer t(c, 4);
+      hipError_t e = p->kind == KMG_WD
+                         ? launch_gram_wd(q, row0, row1, p->d, p->coef_a, o, c->stream)
+                         : launch_gram_wds(q, row0, row1, p->d, p->S, p->coef_a, p->coef_b, o,
+                                           c->stream);
+      if (e == hipErrorNotSupported)
+        return fail(KMG_EUNSUPPORTED, "WD/WDS: sequence length %d / shift %d not supported",
+                    maxlen, p->S);
+      KMG_HIP(e);
+      return KMG_OK;
+    }
+    case KMG_SUBSTRING: {
+      if (p->k < 0) return fail(KMG_EINVAL, "k < 0");
+      if (dt == KMG_I32) return fail(KMG_EINVAL, "SS produces float64 values");
+      if (p->k > 16) return fail(KMG_EUNSUPPORTED, "SS k > 16");
+      SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+      const int mirror = (row0 == 0 && row1 == n) ? 1 : 0;
+      StageTimer t(c, 4);
+      hipError_t e =
+          launch_gram_ss(q, row0, row1, p->k, p->lambda, p->lambda2, mirror, o, c->stream);
+      if (e == hipErrorNotSupported) return fail(KMG_EUNSUPPORTED, "SS parameters");
+      KMG_HIP(e);
+      return KMG_OK;
+    }
+    case KMG_LOCALALIGN: {
+      if (dt == KMG_I32) return fail(KMG_EINVAL, "LA produces float64 values");
+      if (p->la_mode != KMG_LA_REFERENCE)
+        return fail(KMG_EUNSUPPORTED, "LA intended mode not built in this version");
+      // The reference aliases M,X,Y,X2,Y2 to one array and never writes cell
+      // [n_x, n_y] (kernels.py:238-240, 262-264): every entry is log(1+0)/beta = 0.
+      StageTimer t(c, 4);
+      if (rows > 0 && n > 0)
+        KMG_HIP(hipMemset2DAsync(d_out, (size_t)ld * dtype_size(dt), 0,
+                                 (size_t)n * dtype_size(dt), (size_t)rows, c->stream));
+      return KMG_OK;
+    }
+    case KMG_GAPPY: {
+      if (!(p->k == 1 && p->g == 0))
+        return fail(KMG_EUNSUPPORTED, "gappy kernel defined only for k=1, g=0");
+      if (dt == KMG_I32) return fail(KMG_EINVAL, "GP produces float64 values");
+      SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+      KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+      KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+      o.normalize = 1;
+      o.diagv = c->diagv.as<double>();
+      o.dsq = c->dsq.as<double>();
+      StageTimer t(c, 4);
+      KMG_HIP(launch_gram_gappy1(q, row0, row1, p->window > 0 ? p->window : 101, o,
+                                 c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+      return KMG_OK;
+    }
+    default:
+      return fail(KMG_EINVAL, "unknown kernel kind %d", p->kind);
+  }
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+int kmg_version(void) { return KMG_ABI_VERSION; }
+
+const char *kmg_last_error(void) { return g_err.c_str(); }
+
+int kmg_device_count(int *n) {
+  if (!n) return fail(KMG_EINVAL, "n is NULL");
+  int cnt = 0;
+  hipError_t e = hipGetDeviceCount(&cnt);
+  if (e != hipSuccess) cnt = 0;
+  *n = cnt;
+  return KMG_OK;
+}
+
+int kmg_create(kmg_ctx **out, int device_id) {
+  if (!out) return fail(KMG_EINVAL, "ctx is NULL");
+  *out = nullptr;
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0)
+    return fail(KMG_ENODEV, "no HIP device visible");
+  if (device_id < 0 || device_id >= cnt)
+    return fail(KMG_EINVAL, "device %d outside [0,%d)", device_id, cnt);
+  KMG_HIP(hipSetDevice(device_id));
+  kmg_ctx *c = new kmg_ctx();
+  c->device = device_id;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(KMG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return KMG_OK;
+}
+
+int kmg_destroy(kmg_ctx *c) {
+  if (!c) return KMG_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  DevBuf *bufs[] = {&c->kmers, &c->hist, &c->off, &c->cursor, &c->partials, &c->ent,
+                    &c->diagv, &c->dsq, &c->wtab, &c->h_codes, &c->h_lens, &c->h_out};
+  for (DevBuf *b : bufs) b->release();
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return KMG_OK;
+}
+
+int kmg_gram(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+             int64_t n, int64_t ldc, int32_t out_dtype, void *out, int64_t ld_out) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_TRY(check_params(p, n, ldc, out_dtype));
+  if (n > 0 && (!codes || !lens || !out)) return fail(KMG_EINVAL, "NULL buffer");
+  if (n > 0 && ld_out < n) return fail(KMG_EINVAL, "ld_out < n");
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  int maxlen = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (lens[i] < 0 || lens[i] > ldc) return fail(KMG_EINVAL, "lens[%lld] outside [0,ldc]", (long long)i);
+    if (lens[i] > maxlen) maxlen = lens[i];
+  }
+  if (p->kind == KMG_MISMATCH) {
+    const int W = p->window > 0 ? p->window : 101;
+    for (int64_t i = 0; i < n; ++i)
+      if (lens[i] < W) return fail(KMG_EINVAL, "mismatch kernel needs sequences of length >= %d", W);
+  }
+  const size_t esz = dtype_size(out_dtype);
+  const int64_t ldd = (n + 3) & ~3LL;
+  KMG_TRY(c->h_codes.ensure((size_t)n * ldc));
+  KMG_TRY(c->h_lens.ensure(sizeof(int32_t) * (size_t)n));
+  KMG_TRY(c->h_out.ensure(esz * (size_t)n * ldd));
+  KMG_HIP(hipMemcpyAsync(c->h_codes.p, codes, (size_t)n * ldc, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipMemcpyAsync(c->h_lens.p, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  KMG_TRY(gram_device(c, p, c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), maxlen, n, ldc, 0,
+                      n, out_dtype, c->h_out.p, ldd));
+  KMG_HIP(hipMemcpy2DAsync(out, (size_t)ld_out * esz, c->h_out.p, (size_t)ldd * esz,
+                           (size_t)n * esz, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                    const int32_t *d_lens, int64_t n, int64_t ldc, int64_t row0, int64_t row1,
+                    int32_t out_dtype, void *d_out, int64_t ld_out) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_TRY(check_params(p, n, ldc, out_dtype));
+  KMG_HIP(hipSetDevice(c->device));
+  // device-resident path: sequence lengths are device data; the caller promises
+  // max(lens) <= ldc (checked in the host path).  maxlen = ldc bounds every kernel.
+  return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, row0, row1, out_dtype, d_out,
+                     ld_out);
+}
+
+int kmg_normalize(kmg_ctx *c, double *K, int64_t n, int64_t ld, int32_t *skipped) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (skipped) *skipped = 0;
+  if (n <= 0) return KMG_OK;
+  if (!K || ld < n) return fail(KMG_EINVAL, "bad matrix");
+  if (K[0] == 1.0) {  // kernels.py:404-405: already normalised -> unchanged
+    if (skipped) *skipped = 1;
+    return KMG_OK;
+  }
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_TRY(c->h_out.ensure(sizeof(double) * (size_t)n * n));
+  double *d = c->h_out.as<double>();
+  KMG_HIP(hipMemcpy2DAsync(d, n * 8, K, ld * 8, n * 8, n, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(launch_normalize_dense(d, n, n, c->stream));
+  KMG_HIP(hipMemcpy2DAsync(K, ld * 8, d, n * 8, n * 8, n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_center(kmg_ctx *c, const double *K, int64_t ldk, double *out, int64_t ld_out, int64_t n) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n <= 0) return KMG_OK;
+  if (!K || !out || ldk < n || ld_out < n) return fail(KMG_EINVAL, "bad matrix");
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t mat = sizeof(double) * (size_t)n * n;
+  KMG_TRY(c->h_out.ensure(2 * mat + sizeof(double) * (2 * (size_t)n + 1)));
+  double *dK = c->h_out.as<double>();
+  double *dO = dK + (size_t)n * n;
+  double *rm = dO + (size_t)n * n;
+  double *cm = rm + n;
+  double *tot = cm + n;
+  KMG_HIP(hipMemcpy2DAsync(dK, n * 8, K, ldk * 8, n * 8, n, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(launch_center_dense(dK, n, dO, n, n, rm, cm, tot, c->stream));
+  KMG_HIP(hipMemcpy2DAsync(out, ld_out * 8, dO, n * 8, n * 8, n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_dmalloc(kmg_ctx *c, void **ptr, size_t bytes) {
+  if (!c || !ptr) return fail(KMG_EINVAL, "NULL argument");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipMalloc(ptr, bytes ? bytes : 1));
+  return KMG_OK;
+}
+int kmg_dfree(kmg_ctx *c, void *ptr) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  if (ptr) KMG_HIP(hipFree(ptr));
+  return KMG_OK;
+}
+int kmg_h2d(kmg_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+int kmg_d2h(kmg_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+int kmg_memset(kmg_ctx *c, void *dst, int value, size_t bytes) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipMemsetAsync(dst, value, bytes, c->stream));
+  return KMG_OK;
+}
+int kmg_synchronize(kmg_ctx *c) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+int kmg_stream(kmg_ctx *c, void **s) {
+  if (!c || !s) return fail(KMG_EINVAL, "NULL argument");
+  *s = (void *)c->stream;
+  return KMG_OK;
+}
+
+int kmg_set_timing(kmg_ctx *c, int32_t enable) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->timing = enable != 0;
+  return KMG_OK;
+}
+
+int kmg_timing_reset(kmg_ctx *c) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  c->ev_log.clear();
+  c->ev_used = 0;
+  c->last_call_first = 0;
+  return KMG_OK;
+}
+
+static int stage_index(const char *stage) {
+  for (int s = 0; s < kNumStages; ++s)
+    if (strcmp(stage, kStageNames[s]) == 0) return s;
+  return -1;
+}
+
+static int stage_sum(kmg_ctx *c, int idx, size_t first, double *total, int32_t *count) {
+  double t = 0.0;
+  int32_t n = 0;
+  for (size_t q = first; q < c->ev_log.size(); ++q) {
+    if (c->ev_log[q].first != idx) continue;
+    KMG_HIP(hipEventSynchronize(c->ev_log[q].second.second));
+    float f = 0.f;
+    KMG_HIP(hipEventElapsedTime(&f, c->ev_log[q].second.first, c->ev_log[q].second.second));
+    t += f;
+    ++n;
+  }
+  *total = t;
+  *count = n;
+  return KMG_OK;
+}
+
+int kmg_stage_ms(kmg_ctx *c, const char *stage, double *ms) {
+  if (!c || !stage || !ms) return fail(KMG_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  const int idx = stage_index(stage);
+  if (idx < 0) return fail(KMG_EINVAL, "unknown stage '%s'", stage);
+  double t;
+  int32_t n;
+  KMG_TRY(stage_sum(c, idx, (size_t)c->last_call_first, &t, &n));
+  *ms = n ? t : -1.0;
+  return KMG_OK;
+}
+
+int kmg_stage_stats(kmg_ctx *c, const char *stage, double *total_ms, int32_t *count) {
+  if (!c || !stage || !total_ms || !count) return fail(KMG_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  const int idx = stage_index(stage);
+  if (idx < 0) return fail(KMG_EINVAL, "unknown stage '%s'", stage);
+  return stage_sum(c, idx, 0, total_ms, count);
+}
+
+// ------------------------------------------------------------------ RCCL
+int kmg_comm_unique_id(uint8_t id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  memcpy(id, &u, 128);
+  return KMG_OK;
+}
+
+int kmg_comm_init(kmg_ctx *c, const uint8_t id[128], int32_t nranks, int32_t rank) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  c->nranks = nranks;
+  c->rank = rank;
+  return KMG_OK;
+}
+
+int kmg_allgather_rows(kmg_ctx *c, void *d_K, int64_t n, int64_t ld, int32_t dt,
+                       const int64_t *splits) {
+  if (!c || !c->comm) return fail(KMG_EINVAL, "communicator not initialised");
+  if (!splits) return fail(KMG_EINVAL, "splits is NULL");
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t esz = dtype_size(dt);
+  // rows of rank r are contiguous ([splits[r], splits[r+1]) x ld): an all-gather with
+  // per-rank counts = one broadcast per root, issued as one RCCL group.
+  ncclResult_t r = ncclGroupStart();
+  for (int q = 0; q < c->nranks && r == ncclSuccess; ++q) {
+    const int64_t a = splits[q], b = splits[q + 1];
+    if (b <= a) continue;
+    char *base = (char *)d_K + (size_t)a * ld * esz;
+    r = ncclBroadcast(base, base, (size_t)(b - a) * ld * esz, ncclChar, q, c->comm, c->stream);
+  }
+  ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess || r2 != ncclSuccess)
+    return fail(KMG_ERCCL, "ncclBroadcast group: %s",
+                ncclGetErrorString(r != ncclSuccess ? r : r2));
+  (void)n;
+  return KMG_OK;
+}
+
+int kmg_comm_destroy(kmg_ctx *c) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+  return KMG_OK;
+}
+
+}  // extern "C"

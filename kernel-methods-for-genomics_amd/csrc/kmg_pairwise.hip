@@ -1,0 +1,578 @@
+// kmg_pairwise.hip — per-pair Gram kernels (float64) for gfx950.
+//
+// Reference functions restated on the device, with the reference's floating-point
+// operation order kept exactly (the library is built with -ffp-contract=off and the
+// explicit __dmul_rn/__dadd_rn below so no FMA contraction changes a rounding):
+//   get_WD_K / get_WD_d / beta            kernels.py:53-101
+//   get_WDShifts_K / get_WDShifts_d / delta kernels.py:106-155
+//   get_string_K / K_k / B_k              kernels.py:308-382
+//   get_gappy_K (k=1, g=0)                kernels.py:420-455
+// plus the dense host-matrix helpers normalize_K (kernels.py:398-415) and
+// center_K (kernels.py:387-395).
+#include "kmg_internal.h"
+
+namespace kmg {
+
+struct Coef {
+  double a[KMG_MAX_COEF];
+  double b[KMG_MAX_COEF];
+};
+
+// exact per-byte equality flags of two 4-symbol words -> 4 bits (bit q = byte q equal)
+__device__ __forceinline__ uint32_t eq4(uint32_t x, uint32_t y) {
+  const uint32_t v = x ^ y;
+  uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  t = ~(t | v | 0x7F7F7F7Fu);  // high bit of each zero byte
+  return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+}
+
+template <int NW>
+__device__ __forceinline__ void range_mask(uint64_t (&m)[NW], int lo, int hi_excl) {
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int b0 = w * 64;
+    const int a = max(lo - b0, 0), b = min(hi_excl - b0, 64);
+    if (b <= a) {
+      m[w] = 0;
+    } else {
+      const uint64_t hi = (b >= 64) ? ~0ull : ((1ull << b) - 1ull);
+      const uint64_t lom = (a >= 64) ? ~0ull : ((1ull << a) - 1ull);
+      m[w] = hi & ~lom;
+    }
+  }
+}
+
+// r = m >> sh (bit l of r = bit l+sh of m), 0 <= sh < 64*NW
+template <int NW>
+__device__ __forceinline__ void shr_bits(const uint64_t (&m)[NW], int sh, uint64_t (&r)[NW]) {
+  const int ws = sh >> 6, bs = sh & 63;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      if (u == w + ws) lo = m[u];
+      if (u == w + ws + 1) hi = m[u];
+    }
+    r[w] = bs ? ((lo >> bs) | (hi << (64 - bs))) : lo;
+  }
+}
+
+// symbol rows staged in LDS as words of 4 bytes, padded with 0xFF
+template <int NW>
+struct SeqTile {
+  static constexpr int WORDS = 16 * NW + 8;  // + room for shifted reads
+};
+
+template <int NW>
+__device__ __forceinline__ void stage_seq(uint32_t *dst, const SeqSpec &q, int64_t j) {
+  // one wave loads one sequence: lane l writes word l, l+64, ...
+  const int lane = threadIdx.x & 63;
+  const int L = (j < q.n) ? q.lens[j] : 0;
+  const uint8_t *src = q.codes + (j < q.n ? j : 0) * q.ldc;
+  for (int w = lane; w < SeqTile<NW>::WORDS; w += 64) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int pos = 4 * w + b;
+      const uint32_t c = (pos < L) ? src[pos] : 0xFFu;
+      v |= c << (8 * b);
+    }
+    dst[w] = v;
+  }
+}
+
+// match mask M[l] = [x_{l+sx} == y_{l+sy}] for l with l+sx < Lx and l+sy < Ly
+template <int NW>
+__device__ __forceinline__ void match_mask(const uint32_t *xs, int Lx, int sx, const uint32_t *ys,
+                                           int Ly, int sy, uint64_t (&M)[NW]) {
+#pragma unroll
+  for (int w = 0; w < NW; ++w) M[w] = 0;
+  const int qx = sx >> 2, rx = sx & 3, qy = sy >> 2, ry = sy & 3;
+#pragma unroll
+  for (int w = 0; w < 16 * NW; ++w) {
+    const uint32_t xw = __builtin_amdgcn_alignbyte(xs[w + qx + 1], xs[w + qx], rx);
+    const uint32_t yw = __builtin_amdgcn_alignbyte(ys[w + qy + 1], ys[w + qy], ry);
+    M[w >> 4] |= (uint64_t)eq4(xw, yw) << (4 * (w & 15));
+  }
+  uint64_t lim[NW];
+  range_mask<NW>(lim, 0, min(Lx - sx, Ly - sy));
+#pragma unroll
+  for (int w = 0; w < NW; ++w) M[w] &= lim[w];
+}
+
+template <int NW>
+__device__ __forceinline__ int popc_and(const uint64_t (&a)[NW], const uint64_t (&b)[NW]) {
+  int c = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) c += __popcll(a[w] & b[w]);
+  return c;
+}
+
+__device__ __forceinline__ void store_f(const OutSpec &o, int64_t il, int64_t j, double v) {
+  if (o.dtype == KMG_F64)
+    ((double *)o.out)[il * o.ld + j] = v;
+  else if (o.dtype == KMG_F32)
+    ((float *)o.out)[il * o.ld + j] = (float)v;
+  else
+    ((int32_t *)o.out)[il * o.ld + j] = (int32_t)v;
+}
+
+// ------------------------------------------------------------------ WD
+// K[i,j] (i<j) = sum_{k=1..d} beta_k * #{l in [1, L-k] : x[l:l+k] == y[l:l+k]},
+// L = len(x_i) of the smaller index (kernels.py:64-81, 94-100); diagonal =
+// L-1+(1-d)/3 (kernels.py:96).  Tile: 16 rows x 64 columns, 256 threads.
+template <int NW>
+__global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, int64_t row1, int d,
+                                                      Coef cf, OutSpec o) {
+  constexpr int WS = SeqTile<NW>::WORDS;
+  __shared__ uint32_t srow[16][WS];
+  __shared__ uint32_t scol[64][WS];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t rbase = row0 + (int64_t)blockIdx.y * 16;
+  const int64_t cbase = (int64_t)blockIdx.x * 64;
+  for (int r = wave; r < 16; r += 4) stage_seq<NW>(srow[r], q, rbase + r);
+  for (int c = wave; c < 64; c += 4) stage_seq<NW>(scol[c], q, cbase + c);
+  __syncthreads();
+  const int64_t j = cbase + lane;
+  if (j >= q.n) return;
+  for (int r = wave; r < 16; r += 4) {
+    const int64_t i = rbase + r;
+    if (i >= row1) break;
+    double val;
+    if (i == j) {
+      const int L = q.lens[i];
+      val = __dadd_rn((double)(L - 1), (double)(1 - d) / 3.0);
+    } else {
+      const bool rowx = i < j;
+      const uint32_t *xs = rowx ? srow[r] : scol[lane];
+      const uint32_t *ys = rowx ? scol[lane] : srow[r];
+      const int Lx = q.lens[rowx ? i : j], Ly = q.lens[rowx ? j : i];
+      uint64_t M[NW], A[NW], Ms[NW], V[NW];
+      match_mask<NW>(xs, Lx, 0, ys, Ly, 0, M);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { A[w] = M[w]; Ms[w] = M[w]; }
+      val = 0.0;  // c_t = 0 (int); 0 + x is exact
+      for (int k = 1; k <= d; ++k) {
+        if (k > 1) {
+          // Ms = M >> (k-1); A_k = A_{k-1} & Ms
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const uint64_t nxt = (w + 1 < NW) ? Ms[w + 1] : 0ull;
+            Ms[w] = (Ms[w] >> 1) | (nxt << 63);
+            A[w] &= Ms[w];
+          }
+        }
+        range_mask<NW>(V, 1, Lx - k + 1);
+        const int c = popc_and<NW>(A, V);
+        val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], (double)c));
+      }
+    }
+    store_f(o, i - row0, j, val);
+  }
+}
+
+// ------------------------------------------------------------------ WDS
+// c_st = sum_{i=1}^{L-k} sum_{s=0}^{S} [s+i<L] delta_s * ([x[i+s:i+s+k]==y[i:i+k]] +
+// [x[i:i+k]==y[i+s:i+s+k]]), accumulated in exactly that (i, s) order; K += beta_k*c_st
+// (kernels.py:115-135).  Zero terms are skipped: adding +0.0 never changes an fp64 sum.
+template <int NW, int SMAX>
+__global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, int64_t row1, int d,
+                                                       int S, Coef cf, OutSpec o) {
+  constexpr int WS = SeqTile<NW>::WORDS;
+  __shared__ uint32_t srow[16][WS];
+  __shared__ uint32_t scol[64][WS];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t rbase = row0 + (int64_t)blockIdx.y * 16;
+  const int64_t cbase = (int64_t)blockIdx.x * 64;
+  for (int r = wave; r < 16; r += 4) stage_seq<NW>(srow[r], q, rbase + r);
+  for (int c = wave; c < 64; c += 4) stage_seq<NW>(scol[c], q, cbase + c);
+  __syncthreads();
+  const int64_t j = cbase + lane;
+  if (j >= q.n) return;
+  for (int r = wave; r < 16; r += 4) {
+    const int64_t i = rbase + r;
+    if (i >= row1) break;
+    const bool rowx = i <= j;
+    const uint32_t *xs = rowx ? srow[r] : scol[lane];
+    const uint32_t *ys = rowx ? scol[lane] : srow[r];
+    const int Lx = q.lens[rowx ? i : j], Ly = q.lens[rowx ? j : i];
+    uint64_t M1[SMAX + 1][NW], M2[SMAX + 1][NW], W1[SMAX + 1][NW], W2[SMAX + 1][NW];
+#pragma unroll
+    for (int s = 0; s <= SMAX; ++s) {
+      if (s <= S) {
+        match_mask<NW>(xs, Lx, s, ys, Ly, 0, M1[s]);  // x_{i+s} == y_i
+        match_mask<NW>(xs, Lx, 0, ys, Ly, s, M2[s]);  // x_i == y_{i+s}
+      } else {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) { M1[s][w] = 0; M2[s][w] = 0; }
+      }
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { W1[s][w] = M1[s][w]; W2[s][w] = M2[s][w]; }
+    }
+    double val = 0.0;
+    for (int k = 1; k <= d; ++k) {
+      if (k > 1) {
+#pragma unroll
+        for (int s = 0; s <= SMAX; ++s) {
+          uint64_t t1[NW], t2[NW];
+          shr_bits<NW>(M1[s], k - 1, t1);
+          shr_bits<NW>(M2[s], k - 1, t2);
+#pragma unroll
+          for (int w = 0; w < NW; ++w) { W1[s][w] &= t1[w]; W2[s][w] &= t2[w]; }
+        }
+      }
+      uint64_t V[NW];
+      range_mask<NW>(V, 1, Lx - k + 1);
+      uint64_t any[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        uint64_t a = 0;
+#pragma unroll
+        for (int s = 0; s <= SMAX; ++s) a |= W1[s][w] | W2[s][w];
+        any[w] = a & V[w];
+      }
+      double cst = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        uint64_t bits = any[w];
+        while (bits) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const int ii = 64 * w + b;
+#pragma unroll
+          for (int s = 0; s <= SMAX; ++s) {
+            if (s <= S && s + ii < Lx) {
+              const int m = (int)((W1[s][w] >> b) & 1ull) + (int)((W2[s][w] >> b) & 1ull);
+              if (m) cst = __dadd_rn(cst, __dmul_rn(cf.b[s], (double)m));
+            }
+          }
+        }
+      }
+      val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], cst));
+    }
+    store_f(o, i - row0, j, val);
+  }
+}
+
+// ------------------------------------------------------------------ SS (substring)
+// One wave per pair.  Bottom-up B_t(r, j) = B_t(x[:r], y[:j]) for t = 1..k-1 over an
+// anti-diagonal sweep: lane l of a 64-row strip owns row r, at step st it computes
+// column j = st - l.  B_t(r,j) = ((lam*B_t(r-1,j) + lam*B_t(r,j-1)) - lam2*B_t(r-1,j-1))
+// + [x_{r-1}==y_{j-1}] lam2*B_{t-1}(r-1,j-1)   (kernels.py:337-342)
+// K = sum_{i=k..n} lam2 * S_i,  S_i = sum_{j: y_j == x_{i-1}} B_{k-1}(i-1, j)  (kernels.py:359-364)
+template <int KMAX>
+__global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, int64_t row1, int kk,
+                                                      double lam, double lam2, int mirror,
+                                                      OutSpec o) {
+  extern __shared__ __align__(16) double ssm[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = row0 + blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 4 + wave;
+  if (j >= q.n || i >= row1) return;
+  if (mirror && j < i) return;
+  const int ML = q.maxlen;
+  // per-wave LDS: rowbuf[KMAX-1][ML+1], Sbuf[ML+2], ybytes[ML+4]
+  const int per = (KMAX - 1) * (ML + 1) + (ML + 2) + (ML + 4 + 7) / 8;
+  double *rowbuf = ssm + (size_t)wave * per;
+  double *Sbuf = rowbuf + (KMAX - 1) * (ML + 1);
+  uint8_t *yb = (uint8_t *)(Sbuf + ML + 2);
+  const int64_t ia = min(i, j), ib = max(i, j);
+  const uint8_t *xsrc = q.codes + ia * q.ldc;
+  const uint8_t *ysrc = q.codes + ib * q.ldc;
+  const int nx = q.lens[ia], ny = q.lens[ib];
+  double result;
+  if (kk == 0) {
+    result = 1.0;  // K_k(.., 0, ..) returns 1 (kernels.py:354-355)
+  } else if (nx < kk || ny < kk) {
+    result = 0.0;  // kernels.py:357-358
+  } else {
+    for (int c = lane; c < ny; c += 64) yb[c] = ysrc[c];
+    for (int r = lane; r <= nx + 1; r += 64) Sbuf[r] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+    for (int s0 = 0; s0 <= nx; s0 += 64) {
+      const int r = s0 + lane;  // row = number of x symbols consumed
+      const bool live = r <= nx;
+      const uint32_t xprev = (r >= 1 && live) ? xsrc[r - 1] : 0x1FFu;  // x_{r-1}
+      const uint32_t xcur = (r < nx) ? xsrc[r] : 0x1FFu;               // x_r (for S_{r+1})
+      double last[KMAX - 1], diag[KMAX - 1];
+#pragma unroll
+      for (int t = 0; t < KMAX - 1; ++t) { last[t] = 0.0; diag[t] = 0.0; }
+      double sacc = 0.0;
+      const bool store_row = (lane == 63) && (s0 + 64 <= nx);
+      for (int st = 0; st <= ny + 63; ++st) {
+        const int jc = st - lane;
+        const bool act = live && jc >= 0 && jc <= ny;
+        double up[KMAX - 1];
+#pragma unroll
+        for (int t = 0; t < KMAX - 1; ++t) {
+          const double fromleft = __shfl_up(last[t], 1, 64);
+          double u = fromleft;
+          if (lane == 0) u = (s0 == 0 || jc < 0 || jc > ny) ? 0.0 : rowbuf[t * (ML + 1) + jc];
+          up[t] = u;
+        }
+        if (act) {
+          double cur[KMAX - 1];
+          const bool match = (r >= 1 && jc >= 1) && (xprev == yb[jc - 1]);
+#pragma unroll
+          for (int t = 0; t < KMAX - 1; ++t) {
+            const int lvl = t + 1;
+            double v = 0.0;
+            if (lvl < kk && r >= lvl && jc >= lvl && r >= 1 && jc >= 1) {
+              v = __dadd_rn(__dmul_rn(lam, up[t]), __dmul_rn(lam, last[t]));
+              v = __dsub_rn(v, __dmul_rn(lam2, diag[t]));
+              if (match) {
+                const double prevlvl = (t == 0) ? 1.0 : diag[t - 1];
+                v = __dadd_rn(v, __dmul_rn(lam2, prevlvl));
+              }
+            }
+            cur[t] = v;
+          }
+          if (jc < ny && r < nx && yb[jc] == xcur) {
+            double bkm1 = 1.0;  // B_0 == 1
+#pragma unroll
+            for (int t = 0; t < KMAX - 1; ++t)
+              if (t == kk - 2) bkm1 = cur[t];
+            sacc = __dadd_rn(sacc, bkm1);
+          }
+#pragma unroll
+          for (int t = 0; t < KMAX - 1; ++t) {
+            diag[t] = up[t];
+            last[t] = cur[t];
+          }
+          if (store_row) {
+#pragma unroll
+            for (int t = 0; t < KMAX - 1; ++t) rowbuf[t * (ML + 1) + jc] = cur[t];
+          }
+          if (jc == ny && r < nx) Sbuf[r + 1] = sacc;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_wave_barrier();
+    double K = 0.0;
+    if (lane == 0) {
+      for (int ii = kk; ii <= nx; ++ii) K = __dadd_rn(K, __dmul_rn(lam2, Sbuf[ii]));
+    }
+    result = K;
+  }
+  if (lane == 0) {
+    store_f(o, i - row0, j, result);
+    if (mirror && j != i && j >= row0 && j < row1) store_f(o, j - row0, i, result);
+  }
+}
+
+// ------------------------------------------------------------------ GP (k=1, g=0)
+// phi_c(x) = [letter c occurs in x[0:window]] (gappy_k with k=1, g=0, kernels.py:420-433);
+// K_raw = <phi_x, phi_y>, then normalize_K (kernels.py:454).
+__global__ void gappy1_diag_kernel(SeqSpec q, int window, double *diagv, double *dsq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q.n) return;
+  const int L = min(q.lens[i], window);
+  uint32_t m = 0;
+  for (int t = 0; t < L; ++t) m |= 1u << (q.codes[i * q.ldc + t] & 3u);
+  const double v = (double)__popc(m);
+  diagv[i] = v;
+  dsq[i] = __builtin_sqrt(v);
+}
+
+__global__ void gappy1_gram_kernel(SeqSpec q, int64_t row0, int64_t row1, int window, OutSpec o) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = row0 + blockIdx.y;
+  if (j >= q.n || i >= row1) return;
+  auto mask = [&](int64_t s) {
+    const int L = min(q.lens[s], window);
+    uint32_t m = 0;
+    for (int t = 0; t < L; ++t) m |= 1u << (q.codes[s * q.ldc + t] & 3u);
+    return m;
+  };
+  const double raw = (double)__popc(mask(i) & mask(j));
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  double v = raw;
+  if (norm) v = (i == j) ? 1.0 : raw / (o.dsq[i] * o.dsq[j]);
+  store_f(o, i - row0, j, v);
+}
+
+// ------------------------------------------------------------------ dense helpers
+__global__ void dense_diag_sqrt_kernel(const double *K, int64_t n, int64_t ld, double *dsq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dsq[i] = __builtin_sqrt(K[i * ld + i]);
+}
+
+__global__ void dense_normalize_kernel(double *K, int64_t n, int64_t ld, const double *dsq) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= n || j < i) return;
+  if (j == i) {
+    K[i * ld + i] = 1.0;  // np.fill_diagonal(K, np.ones(n))
+  } else {
+    const double v = K[i * ld + j] / (dsq[i] * dsq[j]);  // K[i,j] /= (d * diag[j])
+    K[i * ld + j] = v;
+    K[j * ld + i] = v;  // K[j,i] = K[i,j]
+  }
+}
+
+__global__ void dense_rowmean_kernel(const double *K, int64_t n, int64_t ld, double *rowmean) {
+  __shared__ double red[256];
+  const int64_t i = blockIdx.x;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += blockDim.x) s += K[i * ld + j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rowmean[i] = red[0] / (double)n;
+}
+
+__global__ void dense_colmean_kernel(const double *K, int64_t n, int64_t ld, double *colmean) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += K[i * ld + j];
+  colmean[j] = s / (double)n;
+}
+
+__global__ void dense_total_kernel(const double *rowmean, int64_t n, double *tot) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += rowmean[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[0] = red[0] / (double)n;
+}
+
+__global__ void dense_center_kernel(const double *K, int64_t ldk, double *out, int64_t ldo,
+                                    int64_t n, const double *rowmean, const double *colmean,
+                                    const double *tot) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= n) return;
+  out[i * ldo + j] = ((K[i * ldk + j] - rowmean[i]) - colmean[j]) + tot[0];
+}
+
+// ------------------------------------------------------------------ launchers
+static bool pick_nw(int maxlen, int &nw) {
+  if (maxlen <= 128) { nw = 2; return true; }
+  if (maxlen <= 256) { nw = 4; return true; }
+  return false;
+}
+
+static Coef make_coef(const double *a, const double *b) {
+  Coef c;
+  for (int t = 0; t < KMG_MAX_COEF; ++t) {
+    c.a[t] = a ? a[t] : 0.0;
+    c.b[t] = b ? b[t] : 0.0;
+  }
+  return c;
+}
+
+hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, const double *beta,
+                          const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || q.n == 0) return hipSuccess;
+  int nw;
+  if (!pick_nw(q.maxlen, nw)) return hipErrorNotSupported;
+  const Coef cf = make_coef(beta, nullptr);
+  const dim3 grid((unsigned)((q.n + 63) / 64), (unsigned)((rows + 15) / 16));
+  if (nw == 2)
+    hipLaunchKernelGGL((gram_wd_kernel<2>), grid, dim3(256), 0, s, q, row0, row1, d, cf, o);
+  else
+    hipLaunchKernelGGL((gram_wd_kernel<4>), grid, dim3(256), 0, s, q, row0, row1, d, cf, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S,
+                           const double *beta, const double *delta, const OutSpec &o,
+                           hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || q.n == 0) return hipSuccess;
+  int nw;
+  if (!pick_nw(q.maxlen, nw)) return hipErrorNotSupported;
+  const Coef cf = make_coef(beta, delta);
+  const dim3 grid((unsigned)((q.n + 63) / 64), (unsigned)((rows + 15) / 16));
+#define KMG_WDS(NW_, SM_) \
+  hipLaunchKernelGGL((gram_wds_kernel<NW_, SM_>), grid, dim3(256), 0, s, q, row0, row1, d, S, cf, o)
+  if (nw == 2) {
+    if (S <= 1) KMG_WDS(2, 1);
+    else if (S <= 3) KMG_WDS(2, 3);
+    else if (S <= 7) KMG_WDS(2, 7);
+    else if (S <= 15) KMG_WDS(2, 15);
+    else return hipErrorNotSupported;
+  } else {
+    if (S <= 1) KMG_WDS(4, 1);
+    else if (S <= 3) KMG_WDS(4, 3);
+    else if (S <= 7) KMG_WDS(4, 7);
+    else return hipErrorNotSupported;
+  }
+#undef KMG_WDS
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
+                          double lam2, int mirror, const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || q.n == 0) return hipSuccess;
+  const int ML = q.maxlen;
+  const dim3 grid((unsigned)((q.n + 3) / 4), (unsigned)rows);
+  auto lds_for = [&](int KM) {
+    const int per = (KM - 1) * (ML + 1) + (ML + 2) + (ML + 4 + 7) / 8;
+    return (size_t)per * 8 * 4;
+  };
+#define KMG_SS(KM_)                                                                          \
+  hipLaunchKernelGGL((gram_ss_kernel<KM_>), grid, dim3(256), lds_for(KM_), s, q, row0, row1, kk, \
+                     lam, lam2, mirror, o)
+  if (kk <= 2) KMG_SS(2);
+  else if (kk <= 4) KMG_SS(4);
+  else if (kk <= 8) KMG_SS(8);
+  else if (kk <= 16) KMG_SS(16);
+  else return hipErrorNotSupported;
+#undef KMG_SS
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int window,
+                              const OutSpec &o, double *diagv, double *dsq, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (q.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gappy1_diag_kernel, dim3((unsigned)((q.n + 255) / 256)), dim3(256), 0, s, q,
+                     window, diagv, dsq);
+  if (rows <= 0) return hipGetLastError();
+  hipLaunchKernelGGL(gappy1_gram_kernel, dim3((unsigned)((q.n + 255) / 256), (unsigned)rows),
+                     dim3(256), 0, s, q, row0, row1, window, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize_dense(double *K, int64_t n, int64_t ld, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  double *dsq = nullptr;
+  hipError_t e = hipMallocAsync((void **)&dsq, sizeof(double) * n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(dense_diag_sqrt_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, K,
+                     n, ld, dsq);
+  hipLaunchKernelGGL(dense_normalize_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n),
+                     dim3(256), 0, s, K, n, ld, dsq);
+  e = hipGetLastError();
+  (void)hipFreeAsync(dsq, s);
+  return e;
+}
+
+hipError_t launch_center_dense(const double *K, int64_t ldk, double *out, int64_t ld_out,
+                               int64_t n, double *rowmean, double *colmean, double *tot,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dense_rowmean_kernel, dim3((unsigned)n), dim3(256), 0, s, K, n, ldk, rowmean);
+  hipLaunchKernelGGL(dense_colmean_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, K, n,
+                     ldk, colmean);
+  hipLaunchKernelGGL(dense_total_kernel, dim3(1), dim3(256), 0, s, rowmean, n, tot);
+  hipLaunchKernelGGL(dense_center_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n), dim3(256),
+                     0, s, K, ldk, out, ld_out, n, rowmean, colmean, tot);
+  return hipGetLastError();
+}
+
+}  // namespace kmg

@@ -1,0 +1,243 @@
+"""ctypes binding of libkmgram.so (C ABI: include/kmgram.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+kernel-methods-for-genomics_amd/csrc``).  There is deliberately no fallback: if the
+shared object is missing or no HIP device is visible, every compute call raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libkmgram.so")
+
+KMG_OK, KMG_EINVAL, KMG_EUNSUPPORTED, KMG_EHIP, KMG_ENOMEM, KMG_ERCCL, KMG_ENODEV = range(7)
+KMG_SPECTRUM, KMG_MISMATCH, KMG_WD, KMG_WDS, KMG_SUBSTRING, KMG_LOCALALIGN, KMG_GAPPY = range(1, 8)
+KMG_I32, KMG_F32, KMG_F64 = 1, 2, 3
+KMG_LA_REFERENCE, KMG_LA_INTENDED = 0, 1
+KMG_MAX_COEF = 64
+
+DTYPES = {KMG_I32: np.int32, KMG_F32: np.float32, KMG_F64: np.float64}
+
+# every entry point declared in include/kmgram.h (checked by tests/test_abi.py)
+EXPORTS = (
+    "kmg_version", "kmg_last_error", "kmg_device_count", "kmg_create", "kmg_destroy",
+    "kmg_gram", "kmg_gram_device", "kmg_normalize", "kmg_center", "kmg_dmalloc", "kmg_dfree",
+    "kmg_h2d", "kmg_d2h", "kmg_memset", "kmg_synchronize", "kmg_stream", "kmg_set_timing",
+    "kmg_timing_reset", "kmg_stage_ms", "kmg_stage_stats", "kmg_comm_unique_id", "kmg_comm_init", "kmg_allgather_rows",
+    "kmg_comm_destroy",
+)
+
+
+class KmgParams(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("m", ctypes.c_int32),
+        ("d", ctypes.c_int32), ("S", ctypes.c_int32), ("g", ctypes.c_int32),
+        ("window", ctypes.c_int32), ("normalize", ctypes.c_int32), ("smith", ctypes.c_int32),
+        ("la_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6),
+        ("lambda_", ctypes.c_double), ("lambda2", ctypes.c_double),
+        ("la_e", ctypes.c_double), ("la_d", ctypes.c_double), ("la_beta", ctypes.c_double),
+        ("coef_a", ctypes.c_double * KMG_MAX_COEF), ("coef_b", ctypes.c_double * KMG_MAX_COEF),
+        ("diag_value", ctypes.c_double),
+    ]
+
+
+class KmgError(RuntimeError):
+    """A libkmgram call returned a non-zero status."""
+
+    def __init__(self, status, msg):
+        super().__init__(f"libkmgram error {status}: {msg}")
+        self.status = status
+
+
+class KmgUnsupported(KmgError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libkmgram.so (raises if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libkmgram.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        lib = ctypes.CDLL(LIB_PATH)
+        P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+        sig = {
+            "kmg_version": ([], ctypes.c_int),
+            "kmg_last_error": ([], ctypes.c_char_p),
+            "kmg_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+            "kmg_create": ([ctypes.POINTER(P), ctypes.c_int], ctypes.c_int),
+            "kmg_destroy": ([P], ctypes.c_int),
+            "kmg_gram": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64], ctypes.c_int),
+            "kmg_gram_device": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I64, I64, I32, P,
+                                 I64], ctypes.c_int),
+            "kmg_normalize": ([P, P, I64, I64, ctypes.POINTER(I32)], ctypes.c_int),
+            "kmg_center": ([P, P, I64, P, I64, I64], ctypes.c_int),
+            "kmg_dmalloc": ([P, ctypes.POINTER(P), SZ], ctypes.c_int),
+            "kmg_dfree": ([P, P], ctypes.c_int),
+            "kmg_h2d": ([P, P, P, SZ], ctypes.c_int),
+            "kmg_d2h": ([P, P, P, SZ], ctypes.c_int),
+            "kmg_memset": ([P, P, ctypes.c_int, SZ], ctypes.c_int),
+            "kmg_synchronize": ([P], ctypes.c_int),
+            "kmg_stream": ([P, ctypes.POINTER(P)], ctypes.c_int),
+            "kmg_set_timing": ([P, I32], ctypes.c_int),
+            "kmg_timing_reset": ([P], ctypes.c_int),
+            "kmg_stage_ms": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+            "kmg_stage_stats": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(I32)], ctypes.c_int),
+            "kmg_comm_unique_id": ([P], ctypes.c_int),
+            "kmg_comm_init": ([P, P, I32, I32], ctypes.c_int),
+            "kmg_allgather_rows": ([P, P, I64, I64, I32, P], ctypes.c_int),
+            "kmg_comm_destroy": ([P], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+        return lib
+
+
+def check(status):
+    if status != KMG_OK:
+        msg = load().kmg_last_error().decode(errors="replace")
+        if status == KMG_EUNSUPPORTED:
+            raise KmgUnsupported(status, msg)
+        raise KmgError(status, msg)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load().kmg_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def ptr(a):
+    """Raw pointer of a numpy array (None for empty)."""
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Context:
+    """One libkmgram context (one HIP device, one stream, a device workspace)."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        self._h = ctypes.c_void_p()
+        check(self.lib.kmg_create(ctypes.byref(self._h), int(device)))
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            self.lib.kmg_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- compute
+    def gram(self, params, codes, lens, out_dtype=KMG_F64, out=None):
+        n, ldc = codes.shape
+        if out is None:
+            out = np.empty((n, n), dtype=DTYPES[out_dtype])
+        assert out.flags.c_contiguous and out.shape == (n, n)
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        check(self.lib.kmg_gram(self._h, ctypes.byref(params), ptr(codes), ptr(lens), n, ldc,
+                                out_dtype, ptr(out), n))
+        return out
+
+    def gram_device(self, params, d_codes, d_lens, n, ldc, row0, row1, out_dtype, d_out, ld):
+        check(self.lib.kmg_gram_device(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
+                                       row0, row1, out_dtype, d_out, ld))
+
+    def normalize(self, K):
+        skipped = ctypes.c_int32(0)
+        check(self.lib.kmg_normalize(self._h, ptr(K), K.shape[0], K.strides[0] // 8,
+                                     ctypes.byref(skipped)))
+        return bool(skipped.value)
+
+    def center(self, K):
+        n = K.shape[0]
+        out = np.empty((n, n), dtype=np.float64)
+        check(self.lib.kmg_center(self._h, ptr(K), K.strides[0] // 8, ptr(out), n, n))
+        return out
+
+    # ---------------------------------------------------------------- device memory
+    def dmalloc(self, nbytes):
+        p = ctypes.c_void_p()
+        check(self.lib.kmg_dmalloc(self._h, ctypes.byref(p), int(nbytes)))
+        return p
+
+    def dfree(self, p):
+        check(self.lib.kmg_dfree(self._h, p))
+
+    def h2d(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        check(self.lib.kmg_h2d(self._h, dst, ptr(arr), arr.nbytes))
+
+    def d2h(self, arr, src):
+        check(self.lib.kmg_d2h(self._h, ptr(arr), src, arr.nbytes))
+        return arr
+
+    def memset(self, dst, value, nbytes):
+        check(self.lib.kmg_memset(self._h, dst, int(value), int(nbytes)))
+
+    def synchronize(self):
+        check(self.lib.kmg_synchronize(self._h))
+
+    def set_timing(self, on=True):
+        check(self.lib.kmg_set_timing(self._h, 1 if on else 0))
+
+    def timing_reset(self):
+        check(self.lib.kmg_timing_reset(self._h))
+
+    def stage_stats(self, stage):
+        """(total_ms, count) of a stage over every timed call since timing_reset()."""
+        t, n = ctypes.c_double(0.0), ctypes.c_int32(0)
+        check(self.lib.kmg_stage_stats(self._h, stage.encode(), ctypes.byref(t), ctypes.byref(n)))
+        return t.value, n.value
+
+    def stream_handle(self):
+        s = ctypes.c_void_p()
+        check(self.lib.kmg_stream(self._h, ctypes.byref(s)))
+        return s.value
+
+    def stage_ms(self, stage):
+        v = ctypes.c_double(0.0)
+        check(self.lib.kmg_stage_ms(self._h, stage.encode(), ctypes.byref(v)))
+        return v.value
+
+    # ---------------------------------------------------------------- RCCL
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        check(load().kmg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid, nranks, rank):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self.lib.kmg_comm_init(self._h, buf, int(nranks), int(rank)))
+
+    def allgather_rows(self, d_K, n, ld, dtype, splits):
+        sp = np.ascontiguousarray(np.asarray(splits, dtype=np.int64))
+        check(self.lib.kmg_allgather_rows(self._h, d_K, n, ld, dtype, ptr(sp)))
+
+    def comm_destroy(self):
+        check(self.lib.kmg_comm_destroy(self._h))

@@ -1,0 +1,145 @@
+"""GramEngine: host orchestration of the device Gram kernels (one HIP device).
+
+Each method takes a list of sequences (str) and returns the full symmetric
+``np.ndarray (n, n) float64`` the matching reference function returns
+(kernels.py:28-455).  All arithmetic runs in libkmgram.so on the GPU; the host only
+encodes sequences, validates reference-visible error cases and copies results back.
+"""
+import os
+import threading
+
+import numpy as np
+
+from . import _lib as L
+from . import encode as E
+from . import params as P
+
+
+class GramEngine:
+    def __init__(self, device=None):
+        if device is None:
+            device = int(os.environ.get("KMG_DEVICE", "0"))
+        self.device = device
+        self._ctx = None
+        self._lock = threading.Lock()
+
+    @property
+    def ctx(self):
+        with self._lock:
+            if self._ctx is None:
+                self._ctx = L.Context(self.device)
+            return self._ctx
+
+    def close(self):
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    # ------------------------------------------------------------------ helpers
+    def _run(self, params, seqs, out_dtype=L.KMG_F64):
+        codes, lens = E.encode(seqs)
+        n = len(lens)
+        if n == 0:
+            return np.zeros((0, 0), dtype=L.DTYPES[out_dtype])
+        return self.ctx.gram(params, codes, lens, out_dtype)
+
+    @staticmethod
+    def _require_acgt(seqs):
+        """format() maps A,C,G,T -> 1..4 and int()s every character (kernels.py:184,193):
+        any other character raises ValueError there; so do we."""
+        for s in seqs:
+            bad = set(s) - set(E.ACGT)
+            if bad:
+                ch = sorted(bad)[0]
+                raise ValueError(f"invalid literal for int() with base 10: '{ch}'")
+
+    # ------------------------------------------------------------------ kernels
+    def spectrum(self, seqs, k, out_dtype=L.KMG_F64):
+        """get_spectrum_K (kernels.py:28-47): K_ij = <phi_i, phi_j>, integer counts."""
+        k = int(k)
+        if k < 1:
+            raise ValueError("k must be >= 1")
+        return self._run(P.make(L.KMG_SPECTRUM, k=k), seqs, out_dtype)
+
+    def mismatch(self, seqs, k, m, normalize=True, window=101, out_dtype=L.KMG_F64):
+        """get_mismatch_K (kernels.py:196-217): <Phi_i, Phi_j> then normalize_K."""
+        seqs = list(seqs)
+        self._require_acgt(seqs)
+        short = [len(s) for s in seqs if len(s) < window]
+        if short:
+            # get_phi_km slices windows up to 101 (kernels.py:171): a shorter sequence
+            # yields k-mers of the wrong shape and numpy raises while comparing them.
+            raise ValueError(f"operands could not be broadcast together (sequence of length "
+                             f"{short[0]} < {window})")
+        p = P.make(L.KMG_MISMATCH, k=int(k), m=int(m), window=window,
+                   normalize=1 if normalize else 0)
+        return self._run(p, seqs, out_dtype)
+
+    def wd(self, seqs, d):
+        """get_WD_K (kernels.py:84-101)."""
+        return self._run(P.make(L.KMG_WD, d=int(d)), seqs)
+
+    def wds(self, seqs, d, S):
+        """get_WDShifts_K (kernels.py:138-155)."""
+        seqs = list(seqs)
+        if len({len(s) for s in seqs}) > 1:
+            raise NotImplementedError("WDS on sequences of different lengths is not supported")
+        return self._run(P.make(L.KMG_WDS, d=int(d), S=int(S)), seqs)
+
+    def substring(self, seqs, lbda, k):
+        """get_string_K (kernels.py:367-382)."""
+        return self._run(P.make(L.KMG_SUBSTRING, k=int(k), lbda=lbda), seqs)
+
+    def local_alignment(self, seqs, e=11, d=1, beta=0.5, smith=0, eig=1):
+        """get_LA_K (kernels.py:273-302), reference semantics (the reference
+        always returns an all-zero K, and raises ArpackError for eig=1, n >= 8)."""
+        seqs = list(seqs)
+        self._require_acgt(seqs)
+        n = len(seqs)
+        if eig == 1 and n >= 8:
+            # eigs(K1) on the all-zero K: ARPACK info=-9 (kernels.py:294)
+            from scipy.sparse.linalg import ArpackError
+            raise ArpackError(-9)
+        p = P.make(L.KMG_LOCALALIGN, smith=int(smith), la_mode=L.KMG_LA_REFERENCE,
+                   la_e=e, la_d=d, la_beta=beta)
+        return self._run(p, seqs)
+
+    def gappy(self, seqs, k, g):
+        """get_gappy_K (kernels.py:436-455)."""
+        seqs = list(seqs)
+        self._require_acgt(seqs)
+        k, g = int(k), int(g)
+        if g > k:
+            raise ValueError("r must be non-negative")  # itertools.combinations(..., k-g)
+        if not (k == 1 and g == 0) and any(len(s) > 0 for s in seqs):
+            # `b in gap_set` compares a length-k array with (k-g)-tuples (kernels.py:432):
+            # numpy 2 raises for every (k, g) except k=1, g=0.
+            if k - g == 0:
+                raise ValueError("The truth value of an empty array is ambiguous. Use "
+                                 "`array.size > 0` to check that an array is not empty.")
+            if k - g == k or k - g == 1:
+                raise ValueError("The truth value of an array with more than one element is "
+                                 "ambiguous. Use a.any() or a.all()")
+            raise ValueError(f"operands could not be broadcast together with shapes ({k},) "
+                             f"({k - g},) ")
+        return self._run(P.make(L.KMG_GAPPY, k=k, g=g, window=101), seqs)
+
+    def normalize(self, K):
+        """normalize_K (kernels.py:398-415) in place on a float64 C-contiguous matrix."""
+        return self.ctx.normalize(K)
+
+    def center(self, K):
+        """center_K (kernels.py:387-395)."""
+        return self.ctx.center(np.ascontiguousarray(K, dtype=np.float64))
+
+
+_default = None
+_default_lock = threading.Lock()
+
+
+def default_engine():
+    global _default
+    with _default_lock:
+        if _default is None:
+            _default = GramEngine()
+        return _default

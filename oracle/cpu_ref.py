@@ -1,0 +1,253 @@
+"""ORACLE — CPU restatement of the reference Gram path.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker (never as the thing measured or shipped).
+
+It restates afiliot/Kernel-Methods-For-Genomics kernels.py (v1) function by function,
+keeping the reference's float64 operation order where results are floating point.
+Parity of this oracle is pinned against golden vectors produced by running the
+unmodified reference in the build container (tests/golden/make_golden.py ->
+tests/golden/golden.npz; checked by tests/test_oracle_golden.py).
+
+Symbol codes: A,C,G,T = 0..3, anything else >= 4 (kmgram.encode).
+"""
+import numpy as np
+import scipy.sparse as sp
+
+
+def _codes_list(codes, lens):
+    return [codes[i, : lens[i]].astype(np.int64) for i in range(len(lens))]
+
+
+# --------------------------------------------------------------------- spectrum
+def kmer_codes(seq, k, window=None):
+    """Base-4 codes of the k-mers x[i:i+k], i in range(len(x)-k+1) (kernels.py:21-22),
+    or range(window-k+1) for the mismatch kernel (kernels.py:171).  Windows holding a
+    non-ACGT symbol map to -1 (they match no beta, kernels.py:23-24)."""
+    L = len(seq) if window is None else window
+    P = L - k + 1
+    if P <= 0:
+        return np.zeros(0, dtype=np.int64)
+    out = np.zeros(P, dtype=np.int64)
+    bad = np.zeros(P, dtype=bool)
+    for q in range(k):
+        col = seq[q:q + P]
+        bad |= col >= 4
+        out = out * 4 + (col & 3)
+    out[bad] = -1
+    return out
+
+
+def spectrum(codes, lens, k):
+    """get_spectrum_K (kernels.py:28-47): K = Phi Phi^T with Phi the k-mer count matrix
+    (get_phi_u, kernels.py:12-25).  Exact integers (int64)."""
+    seqs = _codes_list(codes, lens)
+    rows, cols = [], []
+    for i, s in enumerate(seqs):
+        c = kmer_codes(s, k)
+        c = c[c >= 0]
+        rows.append(np.full(len(c), i))
+        cols.append(c)
+    n = len(seqs)
+    r = np.concatenate(rows) if rows else np.zeros(0, dtype=np.int64)
+    c = np.concatenate(cols) if cols else np.zeros(0, dtype=np.int64)
+    Phi = sp.csr_matrix((np.ones(len(r), dtype=np.int64), (r, c)), shape=(n, 4 ** k))
+    return (Phi @ Phi.T).toarray().astype(np.int64)
+
+
+# --------------------------------------------------------------------- mismatch
+def mismatch_weights(k, m):
+    """Closed form of <Phi_x, Phi_y> per k-mer pair at Hamming distance h (see
+    kmgram.params.mismatch_weights; verified here by brute force in tests)."""
+    from math import comb
+    w = []
+    for h in range(k + 1):
+        tot = 0
+        for i in range(k - h + 1):
+            for a in range(h + 1):
+                for b in range(h - a + 1):
+                    c = h - a - b
+                    if i + b + c <= m and i + a + c <= m:
+                        tot += comb(k - h, i) * 3 ** i * comb(h, a) * comb(h - a, b) * 2 ** c
+        w.append(tot)
+    return np.array(w, dtype=np.int64)
+
+
+def _ham_matrix(a, b, k):
+    x = a[:, None] ^ b[None, :]
+    y = (x | (x >> 1)) & int("01" * k, 2)
+    # popcount
+    cnt = np.zeros(y.shape, dtype=np.int64)
+    while np.any(y):
+        cnt += y & 1
+        y >>= 1
+    return cnt
+
+
+def mismatch_raw(codes, lens, k, m, window=101):
+    """Raw <Phi_km(x), Phi_km(y)> (kernels.py:206-215) = sum_{a,b} w_m[ham(x_a, y_b)]."""
+    seqs = _codes_list(codes, lens)
+    km = [kmer_codes(s, k, window) for s in seqs]
+    w = mismatch_weights(k, m)
+    n = len(seqs)
+    K = np.zeros((n, n), dtype=np.int64)
+    for i in range(n):
+        for j in range(i, n):
+            H = _ham_matrix(km[i], km[j], k)
+            K[i, j] = K[j, i] = int(w[H].sum())
+    return K
+
+
+def normalize(K):
+    """normalize_K (kernels.py:398-415) on a copy: K_ij / (d_i * d_j), d = sqrt(diag),
+    upper triangle mirrored, diagonal := 1; unchanged if K[0,0] == 1."""
+    K = np.array(K, dtype=np.float64)
+    if K[0, 0] == 1:
+        return K
+    d = np.sqrt(np.diag(K))
+    iu = np.triu_indices(K.shape[0], 1)
+    vals = K[iu] / (d[iu[0]] * d[iu[1]])
+    K[iu] = vals
+    K[(iu[1], iu[0])] = vals
+    np.fill_diagonal(K, 1.0)
+    return K
+
+
+def mismatch(codes, lens, k, m, window=101):
+    """get_mismatch_K (kernels.py:196-217)."""
+    return normalize(mismatch_raw(codes, lens, k, m, window).astype(np.float64))
+
+
+def mismatch_phi_bruteforce(codes, lens, k, m, window=101):
+    """Literal restatement of get_phi_km + np.dot (kernels.py:161-175, 211-215) over all
+    4^k betas.  Tiny k only (verifies the closed form)."""
+    seqs = _codes_list(codes, lens)
+    betas = np.array([[(b >> (2 * (k - 1 - q))) & 3 for q in range(k)] for b in range(4 ** k)])
+    Phi = np.zeros((len(seqs), 4 ** k), dtype=np.int64)
+    for i, s in enumerate(seqs):
+        for a in range(window - k + 1):
+            kmer = s[a:a + k]
+            Phi[i] += (np.sum(kmer[None, :] != betas, axis=1) <= m)
+    return Phi @ Phi.T
+
+
+# --------------------------------------------------------------------- WD / WDS
+def wd(codes, lens, d):
+    """get_WD_K (kernels.py:84-101) with get_WD_d (kernels.py:64-81), same fp64 order."""
+    seqs = _codes_list(codes, lens)
+    n = len(seqs)
+    K = np.zeros((n, n))
+    bet = [2 * (d - k + 1) / d / (d + 1) for k in range(1, d + 1)]
+    for i in range(n):
+        x = seqs[i]
+        L = len(x)
+        K[i, i] = L - 1 + (1 - d) / 3
+        for j in range(i + 1, n):
+            y = seqs[j]
+            c_t = 0
+            for k in range(1, d + 1):
+                c_st = 0
+                for l in range(1, L - k + 1):
+                    xs, ys = x[l:l + k], y[l:l + k]
+                    c_st += bool(len(xs) == len(ys) and np.array_equal(xs, ys))
+                c_t += bet[k - 1] * c_st
+            K[i, j] = K[j, i] = c_t
+    return K
+
+
+def _eq(a, b):
+    return len(a) == len(b) and np.array_equal(a, b)
+
+
+def wds(codes, lens, d, S):
+    """get_WDShifts_K (kernels.py:138-155) with get_WDShifts_d (kernels.py:115-135)."""
+    seqs = _codes_list(codes, lens)
+    n = len(seqs)
+    K = np.zeros((n, n))
+    bet = [2 * (d - k + 1) / d / (d + 1) for k in range(1, d + 1)]
+    dlt = [1 / 2 / (s + 1) for s in range(S + 1)]
+    for i in range(n):
+        x = seqs[i]
+        L = len(x)
+        for j in range(i, n):
+            y = seqs[j]
+            c_t = 0
+            for k in range(1, d + 1):
+                c_st = 0
+                for ii in range(1, L - k + 1):
+                    for s in range(0, S + 1):
+                        if s + ii < L:
+                            c_st += dlt[s] * (_eq(x[ii + s:ii + s + k], y[ii:ii + k]) +
+                                              _eq(x[ii:ii + k], y[ii + s:ii + s + k]))
+                c_t += bet[k - 1] * c_st
+            K[i, j] = K[j, i] = c_t
+    return K
+
+
+# --------------------------------------------------------------------- substring
+def ss_pair(x, y, lbda, k):
+    """K_k(lbda, k, x, y) (kernels.py:344-364) by bottom-up DP over B_t (kernels.py:322-342)
+    with the reference's expression order."""
+    if k == 0:
+        return 1
+    n, m = len(x), len(y)
+    if n < k or m < k:
+        return 0
+    lam2 = lbda ** 2
+    # B[t][r][c] = B_t(x[:r], y[:c])
+    B = [[[1] * (m + 1) for _ in range(n + 1)]]
+    for t in range(1, k):
+        Bt = [[0] * (m + 1) for _ in range(n + 1)]
+        prev = B[t - 1]
+        for r in range(n + 1):
+            for c in range(m + 1):
+                if r < t or c < t:
+                    Bt[r][c] = 0
+                    continue
+                v = lbda * Bt[r - 1][c] + lbda * Bt[r][c - 1] - lam2 * Bt[r - 1][c - 1]
+                v = v + (lam2 * prev[r - 1][c - 1] if x[r - 1] == y[c - 1] else 0)
+                Bt[r][c] = v
+        B.append(Bt)
+    Bk1 = B[k - 1]
+    K = 0
+    for i in range(k, n + 1):
+        a = x[i - 1]
+        s = sum(Bk1[i - 1][c] for c in range(m) if y[c] == a)
+        K = K + lam2 * s
+    return K
+
+
+def substring(codes, lens, lbda, k):
+    """get_string_K (kernels.py:367-382)."""
+    seqs = [list(map(int, s)) for s in _codes_list(codes, lens)]
+    n = len(seqs)
+    K = np.zeros((n, n))
+    for i in range(n):
+        for j in range(i, n):
+            K[i, j] = K[j, i] = ss_pair(seqs[i], seqs[j], lbda, k)
+    return K
+
+
+# --------------------------------------------------------------------- others
+def local_alignment_reference(n):
+    """get_LA_K as the reference computes it: M,X,Y,X2,Y2 alias one array
+    (kernels.py:238,262) and cell [n_x, n_y] is never written, so every entry is
+    (1/beta)*log(1+0) = 0.0; the function returns K, not K1 (kernels.py:302)."""
+    return np.zeros((n, n))
+
+
+def gappy_k1g0(codes, lens, window=101):
+    """get_gappy_K(X, 1, 0): phi_c = [letter c occurs in x[:window]] (kernels.py:420-433)."""
+    seqs = _codes_list(codes, lens)
+    Phi = np.zeros((len(seqs), 4))
+    for i, s in enumerate(seqs):
+        for c in set(int(v) for v in s[:window]):
+            Phi[i, c] = 1
+    return normalize(Phi @ Phi.T)
+
+
+def center(K):
+    """center_K (kernels.py:387-395)."""
+    n = K.shape[0]
+    B = np.eye(n) - np.ones((n, n)) / n
+    return np.linalg.multi_dot([B, K, B])

@@ -1,0 +1,40 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "kernel-methods-for-genomics_amd")
+ORACLE = os.path.join(ROOT, "oracle")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (PKG, ORACLE, os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and libkmgram.so")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import golden_io
+    return golden_io.Golden()
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    from kmgram import _lib as L
+    c = L.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from kmgram import GramEngine
+    e = GramEngine(0)
+    yield e
+    e.close()

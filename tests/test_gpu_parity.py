@@ -1,0 +1,289 @@
+"""GPU parity: every Gram kernel through the C ABI (and the drop-in kernels.py) against
+the reference goldens and the oracle.  Integer kernels and the float64 kernels are
+bit-exact (tolerance 0: north_star's 1e-6 relative bound is met with equality)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import cpu_ref
+import cref
+from golden_io import load_xtr0, sha256_f64
+from kmgram import _lib as L
+from kmgram import encode as E
+from kmgram import params as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _X(seqs):
+    return pd.DataFrame({"Id": range(len(seqs)), "seq": list(seqs)})
+
+
+# ------------------------------------------------------------------ goldens via kernels.py
+def test_all_goldens_through_dropin(golden):
+    import kernels
+    fn_map = {
+        "get_spectrum_K": kernels.get_spectrum_K, "get_mismatch_K": kernels.get_mismatch_K,
+        "get_WD_K": kernels.get_WD_K, "get_WDShifts_K": kernels.get_WDShifts_K,
+        "get_string_K": kernels.get_string_K, "get_LA_K": kernels.get_LA_K,
+        "get_gappy_K": kernels.get_gappy_K, "select_method": kernels.select_method,
+    }
+    checked = 0
+    for name in golden.names():
+        if name == "SP_k6_xtr0_full":
+            continue
+        e = golden.entry(name)
+        X = _X(golden.seqs(name))
+        fn = fn_map[e["fn"]]
+        if e["error"]:
+            with pytest.raises(Exception) as ei:
+                fn(X, **e["kwargs"])
+            assert type(ei.value).__name__ == e["error"], name
+        else:
+            K = fn(X, **e["kwargs"])
+            ref = golden.K(name)
+            assert K.dtype == np.float64 and K.flags.c_contiguous, name
+            assert np.array_equal(K, ref), name
+            assert sha256_f64(K) == e["sha256_f64"], name
+        checked += 1
+    assert checked >= 50
+
+
+def test_config1_spectrum_k6_xtr0_sha(golden):
+    """BASELINE configs[0]: get_spectrum_K on Data/Xtr0.csv, k=6 — SHA-256 of the reference K."""
+    import kernels
+    codes, lens = load_xtr0()
+    X = _X(E.decode(codes, lens))
+    K = kernels.get_spectrum_K(X, 6)
+    assert sha256_f64(K) == golden.entry("SP_k6_xtr0_full")["sha256_f64"]
+
+
+# ------------------------------------------------------------------ synthetic, config sizes
+def _row_sums_spectrum(codes, lens, k):
+    """sum_j K_ij = sum_u phi_i(u) * T(u), T = total count of u over all sequences."""
+    P_ = codes.shape[1] - k + 1
+    km = np.zeros((codes.shape[0], P_), dtype=np.int64)
+    for q in range(k):
+        km = km * 4 + codes[:, q:q + P_]
+    T = np.bincount(km.ravel(), minlength=4 ** k)
+    return T[km].sum(axis=1)
+
+
+def test_spectrum_k8_n20000(ctx):
+    """BASELINE configs[1] workload: N=20000, L=101, k=8, int32 exact."""
+    codes, lens = E.synthetic(20000, 101, seed=2)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    for r in np.r_[0:8, 9990:10000, 19992:20000]:
+        ref = cref.spectrum(codes, lens, 8, rows=(int(r), int(r) + 1))[0]
+        assert np.array_equal(K[r].astype(np.int64), ref)
+    # size-independent properties over the whole matrix
+    assert np.array_equal(K, K.T)
+    assert np.array_equal(K.sum(axis=1, dtype=np.int64), _row_sums_spectrum(codes, lens, 8))
+    P_ = 101 - 8 + 1
+    km = np.zeros((20000, P_), dtype=np.int64)
+    for q in range(8):
+        km = km * 4 + codes[:, q:q + P_]
+    km.sort(axis=1)
+    diag = [int((np.unique(row, return_counts=True)[1] ** 2).sum()) for row in km]
+    assert np.array_equal(np.diag(K), np.array(diag))
+
+
+def test_spectrum_homopolymer_max(ctx):
+    """Maximum count: a poly-A row against itself = 94^2 = 8836 at k=8."""
+    codes, lens = E.synthetic(64, 101, seed=3)
+    codes[5] = 0
+    codes[9] = 0
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    assert K[5, 5] == 94 * 94 and K[5, 9] == 94 * 94
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 8))
+
+
+@pytest.mark.parametrize("k", [1, 3, 5, 6, 10, 12, 13, 16])
+def test_spectrum_k_range(ctx, k):
+    codes, lens = E.synthetic(300, 101, seed=k)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=k), codes, lens, L.KMG_I32)
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, k))
+
+
+def test_spectrum_ragged_and_chunks(ctx, monkeypatch):
+    rng = np.random.default_rng(5)
+    seqs = ["".join(rng.choice(list("ACGTN"), p=[.24, .24, .24, .24, .04], size=rng.integers(0, 140)))
+            for _ in range(700)]
+    codes, lens = E.encode(seqs)
+    ref = cref.spectrum(codes, lens, 4)
+    for chunk in ("24576", "104", "256"):
+        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
+        K = ctx.gram(P.make(L.KMG_SPECTRUM, k=4), codes, lens, L.KMG_I32)
+        assert np.array_equal(K.astype(np.int64), ref), chunk
+
+
+def test_spectrum_long_sequences_unpacked(ctx):
+    """P > 255: the 32-bit LDS accumulator variant."""
+    codes, lens = E.synthetic(64, 400, seed=9)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=5), codes, lens, L.KMG_I32)
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 5))
+
+
+def test_mismatch_k9_n20000(ctx):
+    """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows."""
+    codes, lens = E.synthetic(20000, 101, seed=3)
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
+                 L.KMG_F64)
+    rows = [0, 1, 7777, 19999]
+    for r in rows:
+        ref = cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0]
+        assert np.array_equal(K[r], ref), r
+    assert np.array_equal(K, K.T)
+    assert np.all(np.diag(K) == 1.0)
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes[:3000],
+                   lens[:3000], L.KMG_I32)
+    assert np.array_equal(raw[:16].astype(np.int64), cref.mismatch_raw(codes[:3000], lens[:3000], 9, 1, rows=(0, 16)))
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (5, 1), (7, 1), (12, 1), (5, 0), (5, 2), (4, 3), (13, 1)])
+def test_mismatch_params(ctx, k, m):
+    codes, lens = E.synthetic(200, 101, seed=k * 10 + m)
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=0), codes, lens, L.KMG_I32)
+    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, m))
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=1), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.mismatch_rows(codes, lens, k, m))
+
+
+def test_mismatch_chunked(ctx, monkeypatch):
+    codes, lens = E.synthetic(900, 101, seed=11)
+    ref = cref.mismatch_raw(codes, lens, 9, 1)
+    for chunk, g in (("64", "1"), ("128", "4"), ("10240", "64")):
+        monkeypatch.setenv("KMG_MM_CHUNK", chunk)
+        monkeypatch.setenv("KMG_MM_G", g)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), ref), (chunk, g)
+
+
+def test_mismatch_stress_repeats(ctx):
+    codes, lens = E.synthetic(40, 101, seed=12)
+    codes[3] = 0
+    codes[4] = np.tile([0, 1], 51)[:101]
+    codes[5] = 3
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
+    ref = cref.mismatch_raw(codes, lens, 9, 1)
+    assert np.array_equal(K.astype(np.int64), ref)
+    assert K[3, 3] == 28 * 93 * 93  # 242,172
+
+
+def test_mismatch_longer_sequences_use_first_window(ctx):
+    codes, lens = E.synthetic(50, 130, seed=13)
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=6, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    ref = cref.mismatch_rows(codes[:, :101].copy(), np.full(50, 101, np.int32), 6, 1)
+    assert np.array_equal(K, ref)
+
+
+# ------------------------------------------------------------------ float kernels
+@pytest.mark.parametrize("d", [1, 3, 4, 10, 20])
+def test_wd_xtr0(ctx, d):
+    codes, lens = load_xtr0()
+    codes, lens = codes[:400], lens[:400]
+    K = ctx.gram(P.make(L.KMG_WD, d=d), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.wd(codes, lens, d))
+
+
+def test_wd_ragged(ctx):
+    rng = np.random.default_rng(3)
+    seqs = ["".join(rng.choice(list("ACGTN"), size=rng.integers(1, 200))) for _ in range(150)]
+    codes, lens = E.encode(seqs)
+    K = ctx.gram(P.make(L.KMG_WD, d=6), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.wd(codes, lens, 6))
+
+
+@pytest.mark.parametrize("d,S", [(1, 0), (3, 1), (5, 3), (10, 5), (8, 7), (4, 12)])
+def test_wds_xtr0(ctx, d, S):
+    codes, lens = load_xtr0()
+    codes, lens = codes[:160], lens[:160]
+    K = ctx.gram(P.make(L.KMG_WDS, d=d, S=S), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.wds(codes, lens, d, S))
+
+
+@pytest.mark.parametrize("lb,k", [(0.5, 3), (1.0, 3), (0.7, 5), (0.3, 2), (0.5, 1), (0.9, 8), (0.6, 11)])
+def test_ss_xtr0(ctx, lb, k):
+    codes, lens = load_xtr0()
+    codes, lens = codes[:48], lens[:48]
+    K = ctx.gram(P.make(L.KMG_SUBSTRING, k=k, lbda=lb), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.ss(codes, lens, lb, k))
+
+
+def test_ss_ragged(ctx):
+    rng = np.random.default_rng(4)
+    seqs = ["".join(rng.choice(list("ACGT"), size=rng.integers(0, 150))) for _ in range(40)]
+    codes, lens = E.encode(seqs)
+    K = ctx.gram(P.make(L.KMG_SUBSTRING, k=3, lbda=0.5), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.ss(codes, lens, 0.5, 3))
+
+
+def test_gappy_k1g0(ctx):
+    import kernels
+    seqs = ["ACGT" * 26, "AAAA" * 26, "ACAC" * 26, "GGTT" * 26, ""]
+    K = kernels.get_gappy_K(_X(seqs), 1, 0)
+    codes, lens = E.encode(seqs)
+    ref = cpu_ref.gappy_k1g0(codes, lens)
+    assert np.array_equal(K, ref, equal_nan=True)
+
+
+# ------------------------------------------------------------------ helpers
+def test_normalize_and_center(engine):
+    import kernels
+    rng = np.random.default_rng(1)
+    A = rng.integers(0, 50, size=(300, 40)).astype(np.float64)
+    K = A @ A.T
+    ref = cpu_ref.normalize(K)
+    K2 = K.copy()
+    out = kernels.normalize_K(K2)
+    assert out is K2 and np.array_equal(K2, ref)
+    # already normalised -> unchanged
+    K3 = ref.copy()
+    kernels.normalize_K(K3)
+    assert np.array_equal(K3, ref)
+    C = kernels.center_K(K)
+    assert np.allclose(C, cpu_ref.center(K), rtol=0, atol=1e-9 * np.abs(K).max())
+
+
+def test_row_slabs_equal_full(ctx):
+    """kmg_gram_device on row slabs (the multi-GPU shard unit) == full matrix."""
+    codes, lens = E.synthetic(1000, 101, seed=21)
+    n, ldc = codes.shape
+    full = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    fullm = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    fullw = ctx.gram(P.make(L.KMG_WD, d=5), codes, lens, L.KMG_F64)
+    d_codes = ctx.dmalloc(codes.nbytes)
+    d_lens = ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    try:
+        for params, dt, ref in ((P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, full),
+                                (P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64, fullm),
+                                (P.make(L.KMG_WD, d=5), L.KMG_F64, fullw)):
+            esz = np.dtype(L.DTYPES[dt]).itemsize
+            out = np.zeros((n, n), dtype=L.DTYPES[dt])
+            d_out = ctx.dmalloc(n * n * esz)
+            splits = [0, 137, 500, 501, 1000]
+            for a, b in zip(splits[:-1], splits[1:]):
+                import ctypes
+                ctx.gram_device(params, d_codes, d_lens, n, ldc, a, b, dt,
+                                ctypes.c_void_p(d_out.value + a * n * esz), n)
+            ctx.synchronize()
+            ctx.d2h(out, d_out)
+            ctx.dfree(d_out)
+            assert np.array_equal(out, ref)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+
+
+def test_device_sqrt_div_bits(ctx):
+    """The fp64 normalise epilogue reproduces numpy's sqrt and division bits."""
+    codes, lens = E.synthetic(500, 101, seed=31)
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=4, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    raw = cref.mismatch_raw(codes, lens, 4, 1).astype(np.float64)
+    d = np.sqrt(np.diag(raw))
+    ref = raw / (d[:, None] * d[None, :])
+    np.fill_diagonal(ref, 1.0)
+    assert np.array_equal(K, ref)
