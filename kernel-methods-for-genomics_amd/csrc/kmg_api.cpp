@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -79,8 +80,9 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"extract", "scan", "scatter", "diag", "gram"};
-constexpr int kNumStages = 5;
+const char *kStageNames[] = {"count", "scan", "place", "fine", "diag", "gram", "extract"};
+constexpr int kNumStages = 7;
+enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT };
 
 }  // namespace
 
@@ -88,7 +90,7 @@ struct kmg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf kmers, hist, off, cursor, partials, ent, diagv, dsq, wtab;
+  DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
   bool timing = false;
   // per-stage event pairs of every timed call since the last reset (read after a sync)
@@ -172,31 +174,42 @@ int check_params(const kmg_params *p, int64_t n, int64_t ldc, int32_t dt) {
 // ----------------------------------------------------------------- posting index
 int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
                 int64_t ldc) {
+  g.fine_bits = 8;
+  while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > 16384) ++g.fine_bits;
   const int64_t nb = g.nbins();
-  const int64_t items = g.n * g.pmax;
-  if ((double)items * g.copies >= 4294967295.0)
+  const int64_t nbk = g.nbuckets();
+  if (nbk > 16384) return fail(KMG_EUNSUPPORTED, "index too large (%lld bins)", (long long)nb);
+  const int rowlen = g.window > 0 ? g.window : (int)ldc;
+  if (rowlen > 4096) return fail(KMG_EUNSUPPORTED, "sequences longer than 4096");
+  const int64_t items = g.n * g.pmax * g.copies;
+  if ((double)items >= 4294967295.0)
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
-  KMG_TRY(c->kmers.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
-  KMG_TRY(c->hist.ensure(sizeof(uint32_t) * (size_t)nb));
+  KMG_TRY(c->bcount.ensure(sizeof(uint32_t) * (size_t)nbk));
+  KMG_TRY(c->boff.ensure(sizeof(uint32_t) * (size_t)(nbk + 1)));
+  KMG_TRY(c->bcursor.ensure(sizeof(uint32_t) * (size_t)nbk));
+  KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nbk)));
+  KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
   KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
-  KMG_TRY(c->cursor.ensure(sizeof(uint32_t) * (size_t)nb));
-  KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nb)));
-  KMG_TRY(c->ent.ensure(sizeof(uint32_t) * (size_t)(items * g.copies > 0 ? items * g.copies : 1)));
+  KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items > 0 ? items : 1)));
   {
-    StageTimer t(c, 0);
-    KMG_HIP(hipMemsetAsync(c->hist.p, 0, sizeof(uint32_t) * (size_t)nb, c->stream));
-    KMG_HIP(launch_extract(g, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(),
-                           c->hist.as<uint32_t>(), c->stream));
+    StageTimer t(c, ST_COUNT);
+    KMG_HIP(hipMemsetAsync(c->bcount.p, 0, sizeof(uint32_t) * (size_t)nbk, c->stream));
+    KMG_HIP(launch_index_count(g, d_codes, d_lens, ldc, c->bcount.as<uint32_t>(), c->stream));
   }
   {
-    StageTimer t(c, 1);
-    KMG_HIP(launch_scan(c->hist.as<uint32_t>(), c->off.as<uint32_t>(), c->cursor.as<uint32_t>(),
-                        nb, c->partials.as<uint32_t>(), c->stream));
+    StageTimer t(c, ST_SCAN);
+    KMG_HIP(launch_scan(c->bcount.as<uint32_t>(), c->boff.as<uint32_t>(),
+                        c->bcursor.as<uint32_t>(), nbk, c->partials.as<uint32_t>(), c->stream));
   }
   {
-    StageTimer t(c, 2);
-    KMG_HIP(launch_scatter(g, c->kmers.as<uint32_t>(), c->cursor.as<uint32_t>(),
-                           c->ent.as<uint32_t>(), c->stream));
+    StageTimer t(c, ST_PLACE);
+    KMG_HIP(launch_index_place(g, d_codes, d_lens, ldc, c->bcursor.as<uint32_t>(),
+                               c->tmp.as<uint32_t>(), c->stream));
+  }
+  {
+    StageTimer t(c, ST_FINE);
+    KMG_HIP(launch_index_fine(g, c->boff.as<uint32_t>(), c->tmp.as<uint32_t>(),
+                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
   }
   return KMG_OK;
 }
@@ -231,11 +244,13 @@ int upload_wtab(kmg_ctx *c, const int64_t *w) {
   return KMG_OK;
 }
 
-int diag_hamming(kmg_ctx *c, const IndexGeom &g) {
+int diag_hamming(kmg_ctx *c, const IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
+                 int64_t ldc) {
   KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
   KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
-  StageTimer t(c, 3);
-  KMG_HIP(launch_diag_hamming(g, c->kmers.as<uint32_t>(), c->wtab.as<int64_t>(),
+  if (g.pmax > 4096) return fail(KMG_EUNSUPPORTED, "more than 4096 k-mers per sequence");
+  StageTimer t(c, ST_DIAG);
+  KMG_HIP(launch_diag_hamming(g, d_codes, d_lens, ldc, c->wtab.as<int64_t>(),
                               c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
   return KMG_OK;
 }
@@ -282,22 +297,18 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.chunk = (int)(n > 0 ? n : 1);
         g.nchunks = 1;
         KMG_TRY(c->kmers.ensure(sizeof(uint32_t) * (size_t)(n * g.pmax > 0 ? n * g.pmax : 1)));
-        KMG_TRY(c->hist.ensure(sizeof(uint32_t)));
         {
-          StageTimer t(c, 0);
-          IndexGeom g0 = g;
-          g0.copies = 0;  // extract only: no histogram
-          KMG_HIP(launch_extract(g0, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(),
-                                 c->hist.as<uint32_t>(), c->stream));
+          StageTimer t(c, ST_EXTRACT);
+          KMG_HIP(launch_extract(g, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(), c->stream));
         }
         KMG_TRY(upload_wtab(c, w));
         if (p->normalize) {
-          KMG_TRY(diag_hamming(c, g));
+          KMG_TRY(diag_hamming(c, g, d_codes, d_lens, ldc));
           o.normalize = 1;
           o.diagv = c->diagv.as<double>();
           o.dsq = c->dsq.as<double>();
         }
-        StageTimer t(c, 4);
+        StageTimer t(c, ST_GRAM);
         KMG_HIP(launch_gram_hamming(g, c->kmers.as<uint32_t>(), row0, row1,
                                     c->wtab.as<int64_t>(), o, c->stream));
         return KMG_OK;
@@ -305,27 +316,27 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (exact) {
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, env_or("KMG_SP_CHUNK", 24576));
+        choose_chunks(g, std::min(65536, env_or("KMG_SP_CHUNK", 24576)));
       } else {
         g.copies = k;
         g.nkeys = (uint32_t)pow4(k - 1);
-        choose_chunks(g, env_or("KMG_MM_CHUNK", 10240));
+        choose_chunks(g, std::min(16384, env_or("KMG_MM_CHUNK", 10240)));
       }
       KMG_TRY(build_index(c, g, d_codes, d_lens, ldc));
       if (p->normalize) {
         KMG_TRY(upload_wtab(c, w));
-        KMG_TRY(diag_hamming(c, g));
+        KMG_TRY(diag_hamming(c, g, d_codes, d_lens, ldc));
         o.normalize = 1;
         o.diagv = c->diagv.as<double>();
         o.dsq = c->dsq.as<double>();
       }
-      StageTimer t(c, 4);
+      StageTimer t(c, ST_GRAM);
       if (exact) {
-        KMG_HIP(launch_gram_spectrum(g, c->kmers.as<uint32_t>(), c->off.as<uint32_t>(),
-                                     c->ent.as<uint32_t>(), row0, row1, o, c->stream));
+        KMG_HIP(launch_gram_spectrum(g, d_codes, d_lens, ldc, c->off.as<uint32_t>(),
+                                     c->ent.as<uint16_t>(), row0, row1, o, c->stream));
       } else {
-        KMG_HIP(launch_gram_mismatch1(g, c->kmers.as<uint32_t>(), c->off.as<uint32_t>(),
-                                      c->ent.as<uint32_t>(), row0, row1, (int)w[0], (int)w[1],
+        KMG_HIP(launch_gram_mismatch1(g, d_codes, ldc, c->off.as<uint32_t>(),
+                                      c->ent.as<uint16_t>(), row0, row1, (int)w[0], (int)w[1],
                                       (int)w[2], o, c->stream));
       }
       return KMG_OK;
@@ -337,7 +348,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
-      StageTimer t(c, 4);
+      StageTimer t(c, ST_GRAM);
       hipError_t e = p->kind == KMG_WD
                          ? launch_gram_wd(q, row0, row1, p->d, p->coef_a, o, c->stream)
                          : launch_gram_wds(q, row0, row1, p->d, p->S, p->coef_a, p->coef_b, o,
@@ -354,7 +365,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (p->k > 16) return fail(KMG_EUNSUPPORTED, "SS k > 16");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
       const int mirror = (row0 == 0 && row1 == n) ? 1 : 0;
-      StageTimer t(c, 4);
+      StageTimer t(c, ST_GRAM);
       hipError_t e =
           launch_gram_ss(q, row0, row1, p->k, p->lambda, p->lambda2, mirror, o, c->stream);
       if (e == hipErrorNotSupported) return fail(KMG_EUNSUPPORTED, "SS parameters");
@@ -367,7 +378,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         return fail(KMG_EUNSUPPORTED, "LA intended mode not built in this version");
       // The reference aliases M,X,Y,X2,Y2 to one array and never writes cell
       // [n_x, n_y] (kernels.py:238-240, 262-264): every entry is log(1+0)/beta = 0.
-      StageTimer t(c, 4);
+      StageTimer t(c, ST_GRAM);
       if (rows > 0 && n > 0)
         KMG_HIP(hipMemset2DAsync(d_out, (size_t)ld * dtype_size(dt), 0,
                                  (size_t)n * dtype_size(dt), (size_t)rows, c->stream));
@@ -383,7 +394,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       o.normalize = 1;
       o.diagv = c->diagv.as<double>();
       o.dsq = c->dsq.as<double>();
-      StageTimer t(c, 4);
+      StageTimer t(c, ST_GRAM);
       KMG_HIP(launch_gram_gappy1(q, row0, row1, p->window > 0 ? p->window : 101, o,
                                  c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
       return KMG_OK;
@@ -436,8 +447,9 @@ int kmg_destroy(kmg_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
-  DevBuf *bufs[] = {&c->kmers, &c->hist, &c->off, &c->cursor, &c->partials, &c->ent,
-                    &c->diagv, &c->dsq, &c->wtab, &c->h_codes, &c->h_lens, &c->h_out};
+  DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
+                    &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
+                    &c->h_lens, &c->h_out};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);

@@ -77,13 +77,25 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
   }
 }
 
+// row k-mer code of window a of a staged row (KMG_INVALID if it holds a non-ACGT symbol)
+__device__ __forceinline__ uint32_t window_code(const uint8_t *rs, int a, int k) {
+  uint32_t c = 0, bad = 0;
+  for (int q = 0; q < k; ++q) {
+    const uint32_t v = rs[a + q];
+    bad |= v & ~3u;
+    c = (c << 2) | (v & 3u);
+  }
+  return bad ? KMG_INVALID : c;
+}
+
 // ------------------------------------------------------------------ spectrum
 // PACK16: two 16-bit counters per LDS word (valid when every K_ij <= 65535, i.e.
 // P_i * P_j <= 65535; the host checks P_max <= 255).
 template <bool PACK16, int DT>
-__global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint32_t *__restrict__ kmers,
+__global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                      const int32_t *__restrict__ lens, int64_t ldc,
                                                       const uint32_t *__restrict__ off,
-                                                      const uint32_t *__restrict__ ent,
+                                                      const uint16_t *__restrict__ ent,
                                                       int64_t row0, OutSpec o) {
   extern __shared__ __align__(16) uint32_t acc[];
   const int64_t il = blockIdx.x / g.nchunks;
@@ -97,24 +109,23 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint32_
   __syncthreads();
 
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
-  const uint32_t *__restrict__ row = kmers + (size_t)i * g.pmax;
-  for (int a = threadIdx.x; a < g.pmax; a += blockDim.x) {
-    const uint32_t u = row[a];
+  const int L = g.window > 0 ? g.window : lens[i];
+  const uint8_t *rs = codes + i * ldc;
+  for (int a = threadIdx.x; a <= L - g.k; a += blockDim.x) {
+    const uint32_t u = window_code(rs, a, g.k);
     if (u == KMG_INVALID) continue;
     const uint32_t beg = o_c[u], end = o_c[u + 1];
     uint32_t e = beg;
-    for (; e + 4 <= end; e += 4) {
-      const uint32_t j0 = ent[e], j1 = ent[e + 1], j2 = ent[e + 2], j3 = ent[e + 3];
-      if (PACK16) {
-        atomicAdd(&acc[j0 >> 1], 1u << ((j0 & 1) << 4));
-        atomicAdd(&acc[j1 >> 1], 1u << ((j1 & 1) << 4));
-        atomicAdd(&acc[j2 >> 1], 1u << ((j2 & 1) << 4));
-        atomicAdd(&acc[j3 >> 1], 1u << ((j3 & 1) << 4));
-      } else {
-        atomicAdd(&acc[j0], 1u);
-        atomicAdd(&acc[j1], 1u);
-        atomicAdd(&acc[j2], 1u);
-        atomicAdd(&acc[j3], 1u);
+    for (; e + 8 <= end; e += 8) {
+      uint32_t j[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) j[q] = ent[e + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (PACK16)
+          atomicAdd(&acc[j[q] >> 1], 1u << ((j[q] & 1) << 4));
+        else
+          atomicAdd(&acc[j[q]], 1u);
       }
     }
     for (; e < end; ++e) {
@@ -142,66 +153,123 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint32_
 }
 
 // ------------------------------------------------------------------ mismatch m=1
-struct MMSub {
-  int8_t p, q, ci, pad;
-};
-__constant__ MMSub c_mmsub[16 + 3 * 120];
+// Sub-list s of a row k-mer u (nsub = k + 3*k*(k-1)/2 of them):
+//   s <  k: list (p=s, key_p(u)): neighbours equal to u outside p -> ham 0 (counted
+//           once, on p=0, weight w0) or ham 1 at p (weight w1)
+//   s >= k: (p, q<p, ci): substitute letter q of u by the ci-th other letter, scan list
+//           (p, key_p) keeping letters != u_p -> ham 2 exactly at {q,p} (weight w2)
+// Every Hamming<=2 neighbour of u is visited exactly once with its weight.
+constexpr int MM_THREADS = 512;
 
-// G lanes cooperate on one posting list.
 template <int G, int DT>
-__global__ __launch_bounds__(256) void gram_mm1_kernel(IndexGeom g, int nsub,
-                                                       const uint32_t *__restrict__ kmers,
-                                                       const uint32_t *__restrict__ off,
-                                                       const uint32_t *__restrict__ ent,
-                                                       int64_t row0, int w0, int w1, int w2,
-                                                       OutSpec o) {
+__global__ __launch_bounds__(MM_THREADS) void gram_mm1_kernel(IndexGeom g, int nsub,
+                                                              const uint8_t *__restrict__ codes,
+                                                              int64_t ldc,
+                                                              const uint32_t *__restrict__ off,
+                                                              const uint16_t *__restrict__ ent,
+                                                              int64_t row0, int w0, int w1, int w2,
+                                                              OutSpec o) {
   extern __shared__ __align__(16) uint32_t smem[];
   const int64_t il = blockIdx.x / g.nchunks;
   const int64_t i = row0 + il;
   const int c = blockIdx.x - (int)il * g.nchunks;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
-  const int words = ((cw + 3) >> 2) << 2;
+  const int accw = ((g.chunk + 3) >> 2) << 2;
   int32_t *acc = (int32_t *)smem;
-  uint32_t *rowk = smem + (((g.chunk + 3) >> 2) << 2);
+  uint32_t *rowk = smem + accw;          // pmax row k-mers
+  uint32_t *sub = rowk + g.pmax;         // nsub descriptors: p | q << 8 | ci << 16
   uint4 *acc4 = (uint4 *)acc;
-  for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
-  for (int a = threadIdx.x; a < g.pmax; a += blockDim.x) rowk[a] = kmers[(size_t)i * g.pmax + a];
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const int k = g.k;
+  const uint8_t *rs = codes + i * ldc;
+  for (int a = threadIdx.x; a < g.pmax; a += blockDim.x) rowk[a] = window_code(rs, a, k);
+  for (int s = threadIdx.x; s < nsub; s += blockDim.x) {
+    uint32_t d;
+    if (s < k) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - k, pi = t / 3, ci = t - 3 * pi;
+      int p = 1;
+      while ((p + 1) * p / 2 <= pi) ++p;  // pi = p(p-1)/2 + q
+      const int q = pi - p * (p - 1) / 2;
+      d = (uint32_t)p | ((uint32_t)q << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
   __syncthreads();
 
-  const int k = g.k;
   const int grp = threadIdx.x / G, gl = threadIdx.x % G, ngrp = blockDim.x / G;
   const int total = g.pmax * nsub;
-  for (int L = grp; L < total; L += ngrp) {
+  // list descriptor: bin, letter u_p, weights for (letter == u_p) / (letter != u_p)
+  auto describe = [&](int L, uint32_t &bin, uint32_t &up, int &wa, int &wb) -> bool {
     const int a = L / nsub;
     const int s = L - a * nsub;
     const uint32_t u = rowk[a];
-    if (u == KMG_INVALID) continue;
-    const MMSub sb = c_mmsub[s];
-    const int p = sb.p;
+    if (u == KMG_INVALID) return false;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF, q = (d >> 8) & 0xFF;
     uint32_t z = u;
-    int wa, wb;
-    if (sb.q < 0) {
-      // neighbours differing from u at most at p: ham 0 (counted once, on p==0) or 1
+    if (q == 0xFF) {
       wa = (p == 0) ? w0 : 0;
       wb = w1;
     } else {
-      // neighbours differing exactly at {q, p}, q < p: substitute letter q, scan list p
-      const int sh = 2 * (k - 1 - sb.q);
+      const int sh = 2 * (k - 1 - q);
       const uint32_t lq = (u >> sh) & 3u;
-      const uint32_t nl = (lq + 1u + (uint32_t)sb.ci) & 3u;
+      const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
       z = (u & ~(3u << sh)) | (nl << sh);
       wa = 0;
       wb = w2;
     }
-    const uint32_t up = letter_at_g(u, p, k);
-    const size_t bin = ((size_t)p * g.nchunks + c) * g.nkeys + drop_letter_g(z, p, k);
-    const uint32_t beg = off[bin], end = off[bin + 1];
-    for (uint32_t e = beg + gl; e < end; e += G) {
-      const uint32_t v = ent[e];
-      const int w = ((v >> KMG_ENTRY_LETTER_SHIFT) == up) ? wa : wb;
-      if (w) atomicAdd(&acc[v & KMG_ENTRY_SEQ_MASK], w);
+    up = letter_at_g(u, p, k);
+    bin = (uint32_t)(((int64_t)p * g.nchunks + c) * g.nkeys + drop_letter_g(z, p, k));
+    return true;
+  };
+
+  int L = grp;
+  uint32_t beg = 0, end = 0, up = 0;
+  int wa = 0, wb = 0;
+  if (L < total) {
+    uint32_t bin;
+    if (describe(L, bin, up, wa, wb)) {
+      beg = off[bin];
+      end = off[bin + 1];
     }
+  }
+  while (L < total) {
+    // software pipeline: fetch the next list's bounds while this list's entries load
+    const int Ln = L + ngrp;
+    uint32_t nbeg = 0, nend = 0, nup = 0;
+    int nwa = 0, nwb = 0;
+    if (Ln < total) {
+      uint32_t bin;
+      if (describe(Ln, bin, nup, nwa, nwb)) {
+        nbeg = off[bin];
+        nend = off[bin + 1];
+      }
+    }
+    const uint32_t e0 = beg + gl;
+    uint32_t v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (e0 + q * G < end) ? (uint32_t)ent[e0 + q * G] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (v[q] != 0xFFFFFFFFu) {
+        const int w = ((v[q] >> 14) == up) ? wa : wb;
+        if (w) atomicAdd(&acc[v[q] & 0x3FFFu], w);
+      }
+    }
+    for (uint32_t e = e0 + 4 * G; e < end; e += G) {
+      const uint32_t x = ent[e];
+      const int w = ((x >> 14) == up) ? wa : wb;
+      if (w) atomicAdd(&acc[x & 0x3FFFu], w);
+    }
+    L = Ln;
+    beg = nbeg;
+    end = nend;
+    up = nup;
+    wa = nwa;
+    wb = nwb;
   }
   __syncthreads();
 
@@ -256,23 +324,28 @@ __global__ __launch_bounds__(256) void gram_ham_kernel(IndexGeom g, const uint32
 }
 
 // raw self-kernel K_ii for every sequence (diagonal used by normalize_K)
-__global__ __launch_bounds__(64) void diag_ham_kernel(IndexGeom g, const uint32_t *__restrict__ kmers,
+__global__ __launch_bounds__(64) void diag_ham_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                      const int32_t *__restrict__ lens, int64_t ldc,
                                                       const int64_t *__restrict__ wtab,
                                                       double *__restrict__ diagv,
                                                       double *__restrict__ dsq) {
   __shared__ int64_t w_s[33];
+  __shared__ uint32_t xk[4096];
   const int lane = threadIdx.x;
   const int64_t i = blockIdx.x;
   if (lane <= g.k) w_s[lane] = wtab[lane];
+  const int L = g.window > 0 ? g.window : lens[i];
+  const int P = min(L - g.k + 1, 4096);
+  const uint8_t *rs = codes + i * ldc;
+  for (int a = lane; a < P; a += 64) xk[a] = window_code(rs, a, g.k);
   __syncthreads();
   const uint32_t mask55 = (g.k >= 16) ? 0x55555555u : (0x55555555u & ((1u << (2 * g.k)) - 1u));
-  const uint32_t *xc = kmers + (size_t)i * g.pmax;
   int64_t s = 0;
-  for (int a = lane; a < g.pmax; a += 64) {
-    const uint32_t xa = xc[a];
+  for (int a = lane; a < P; a += 64) {
+    const uint32_t xa = xk[a];
     if (xa == KMG_INVALID) continue;
-    for (int b = 0; b < g.pmax; ++b) {
-      const uint32_t yb = xc[b];
+    for (int b = 0; b < P; ++b) {
+      const uint32_t yb = xk[b];
       if (yb != KMG_INVALID) s += w_s[ham2bit(xa, yb, mask55)];
     }
   }
@@ -293,9 +366,9 @@ __global__ __launch_bounds__(64) void diag_ham_kernel(IndexGeom g, const uint32_
     default: { constexpr int D = KMG_F64; __VA_ARGS__; } break;      \
   }
 
-hipError_t launch_gram_spectrum(const IndexGeom &g, const uint32_t *kmers, const uint32_t *off,
-                                const uint32_t *ent, int64_t row0, int64_t row1,
-                                const OutSpec &o, hipStream_t s) {
+hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                                int64_t ldc, const uint32_t *off, const uint16_t *ent,
+                                int64_t row0, int64_t row1, const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   const bool pack = g.pmax <= 255;
@@ -304,33 +377,12 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const uint32_t *kmers, const
   const dim3 grid((unsigned)(rows * g.nchunks));
   if (pack) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D>), grid, dim3(256), lds, s,
-                                                g, kmers, off, ent, row0, o));
+                                                g, codes, lens, ldc, off, ent, row0, o));
   } else {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<false, D>), grid, dim3(256), lds, s,
-                                                g, kmers, off, ent, row0, o));
+                                                g, codes, lens, ldc, off, ent, row0, o));
   }
   return hipGetLastError();
-}
-
-static int g_mm_nsub_k = -1;
-static int g_mm_nsub = 0;
-
-static hipError_t upload_mmsub(int k, hipStream_t s) {
-  if (g_mm_nsub_k == k) return hipSuccess;
-  MMSub tab[16 + 3 * 120];
-  int n = 0;
-  for (int p = 0; p < k; ++p) tab[n++] = MMSub{(int8_t)p, (int8_t)-1, 0, 0};
-  for (int p = 1; p < k; ++p)
-    for (int q = 0; q < p; ++q)
-      for (int ci = 0; ci < 3; ++ci) tab[n++] = MMSub{(int8_t)p, (int8_t)q, (int8_t)ci, 0};
-  hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_mmsub), tab, sizeof(MMSub) * n, 0,
-                                        hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return e;
-  g_mm_nsub_k = k;
-  g_mm_nsub = n;
-  return hipSuccess;
 }
 
 static int env_int(const char *name, int dflt) {
@@ -338,25 +390,25 @@ static int env_int(const char *name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint32_t *kmers, const uint32_t *off,
-                                 const uint32_t *ent, int64_t row0, int64_t row1, int w0, int w1,
-                                 int w2, const OutSpec &o, hipStream_t s) {
+hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                 const uint32_t *off, const uint16_t *ent, int64_t row0,
+                                 int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                 hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
-  hipError_t e = upload_mmsub(g.k, s);
-  if (e != hipSuccess) return e;
-  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax) * 4;
+  const int nsub = g.k + 3 * g.k * (g.k - 1) / 2;
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax + nsub) * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
-  // lanes per posting list ~ half the expected list length (chunk * P / 4^(k-1))
+  // lanes per posting list: 4 unrolled loads per lane cover ~ the expected list length
   const double avg = (double)g.chunk * g.pmax / (double)g.nkeys;
   int G = 1;
-  while (G < 64 && G * 2 <= avg / 2) G *= 2;
+  while (G < 64 && G * 4 < avg) G *= 2;
   G = env_int("KMG_MM_G", G);
-  const int nsub = g_mm_nsub;
-#define KMG_MM_CASE(GG)                                                                          \
-  case GG:                                                                                       \
-    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_mm1_kernel<GG, D>), grid, dim3(256), lds, \
-                                                s, g, nsub, kmers, off, ent, row0, w0, w1, w2, o)); \
+#define KMG_MM_CASE(GG)                                                                    \
+  case GG:                                                                                 \
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_mm1_kernel<GG, D>), grid,           \
+                                                dim3(MM_THREADS), lds, s, g, nsub, codes, \
+                                                ldc, off, ent, row0, w0, w1, w2, o));     \
     break;
   switch (G) {
     KMG_MM_CASE(1)
@@ -383,11 +435,12 @@ hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_
   return hipGetLastError();
 }
 
-hipError_t launch_diag_hamming(const IndexGeom &g, const uint32_t *kmers, const int64_t *wtab,
-                               double *diagv, double *dsq, hipStream_t s) {
+hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                               int64_t ldc, const int64_t *wtab, double *diagv, double *dsq,
+                               hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(diag_ham_kernel, dim3((unsigned)g.n), dim3(64), 0, s, g, kmers, wtab, diagv,
-                     dsq);
+  hipLaunchKernelGGL(diag_ham_kernel, dim3((unsigned)g.n), dim3(64), 0, s, g, codes, lens, ldc,
+                     wtab, diagv, dsq);
   return hipGetLastError();
 }
 

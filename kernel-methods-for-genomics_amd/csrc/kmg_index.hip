@@ -1,88 +1,222 @@
-// kmg_index.hip — k-mer extraction and posting-index build on gfx950.
+// kmg_index.hip — k-mer posting index on gfx950.
 //
 // Replaces the dense feature vectors of the reference:
 //   get_phi_u  (kernels.py:12-25):  phi_u[b] = #{i < len(x)-k+1 : x[i:i+k] == b}
 //   get_phi_km (kernels.py:161-175): phi_km[b] = #{i < 101-k+1 : ham(x[i:i+k], b) <= m}
 // Instead of 4^k-wide float64 rows we keep, per k-mer key, the list of columns
-// (sequences) holding it ("postings").  The Gram kernels then accumulate one row
-// of K at a time in LDS (kmg_gram.hip).  All work here is integer: a histogram
-// (global atomics), an exclusive scan and a scatter.
+// (sequences) holding it ("postings").  The Gram kernels then accumulate one row of
+// K at a time in LDS (kmg_gram.hip).
+//
+// Layout: bins = [copy][chunk][key]; off[bin] .. off[bin+1] indexes ent[].
+// ent is uint16: column inside the chunk (SP: 16 bits; MM: low 14 bits) | letter at
+// the dropped position << 14 (MM).  Order inside a bin is unspecified (the Gram is
+// an integer sum, so results do not depend on it).
+//
+// Build = two-pass MSD partition with LDS histograms (no per-occurrence global
+// atomics): (1) count occurrences per coarse bucket (bins >> fine_bits), LDS
+// histogram per block, one global add per (block, bucket); (2) exclusive scan of the
+// bucket counts; (3) per block, reserve a range per bucket (one returning global add
+// per (block, bucket)) and place items in the bucket arrays with LDS cursors;
+// (4) one block per bucket: LDS histogram + scan of its fine bins -> off[], then
+// place the items with LDS cursors into ent[].
 #include "kmg_internal.h"
 
 namespace kmg {
 
-// letter p of a k-mer code: most significant letter first (itertools.product order,
-// kernels.py:37,206 — base-4 with A=0,C=1,G=2,T=3)
 __device__ __forceinline__ uint32_t letter_at(uint32_t code, int p, int k) {
   return (code >> (2 * (k - 1 - p))) & 3u;
 }
-// the (k-1)-letter key obtained by deleting letter p
 __device__ __forceinline__ uint32_t drop_letter(uint32_t code, int p, int k) {
   const uint64_t c = code;
   const int lo_bits = 2 * (k - 1 - p);
-  const uint64_t hi = c >> (lo_bits + 2);
-  const uint64_t lo = c & ((1ull << lo_bits) - 1ull);
-  return (uint32_t)((hi << lo_bits) | lo);
+  return (uint32_t)(((c >> (lo_bits + 2)) << lo_bits) | (c & ((1ull << lo_bits) - 1ull)));
 }
 
+constexpr int IDX_THREADS = 256;
+constexpr int IDX_SEQS = 16;  // sequences per partition block
+
+// stage IDX_SEQS rows of codes in LDS; returns number of staged sequences
+__device__ __forceinline__ int stage_rows(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                          const int32_t *lens, uint8_t *srow, int32_t *slen,
+                                          int rowlen, int64_t j0) {
+  const int ns = (int)min((int64_t)IDX_SEQS, g.n - j0);
+  for (int t = threadIdx.x; t < ns * rowlen; t += blockDim.x) {
+    const int s = t / rowlen, c = t - s * rowlen;
+    srow[t] = codes[(j0 + s) * ldc + c];
+  }
+  if ((int)threadIdx.x < ns) {
+    const int L = g.window > 0 ? g.window : lens[j0 + threadIdx.x];
+    slen[threadIdx.x] = min(L, rowlen);
+  }
+  __syncthreads();
+  return ns;
+}
+
+// visit every (bin, value) item of the staged sequences
+template <typename F>
+__device__ __forceinline__ void for_items(const IndexGeom &g, const uint8_t *srow,
+                                          const int32_t *slen, int rowlen, int ns, int64_t j0,
+                                          F &&f) {
+  const int per = g.pmax;
+  for (int t = threadIdx.x; t < ns * per; t += blockDim.x) {
+    const int s = t / per, a = t - s * per;
+    if (a > slen[s] - g.k) continue;  // windows range(L-k+1)
+    const uint8_t *w = srow + s * rowlen + a;
+    uint32_t c = 0, bad = 0;
+    for (int q = 0; q < g.k; ++q) {
+      const uint32_t v = w[q];
+      bad |= v & ~3u;  // non-ACGT symbol: k-mer equals no beta (kernels.py:23-24)
+      c = (c << 2) | (v & 3u);
+    }
+    if (bad) continue;
+    const int64_t j = j0 + s;
+    const int ch = (int)(j / g.chunk);
+    const uint32_t col = (uint32_t)(j - (int64_t)ch * g.chunk);
+    if (g.copies == 1) {
+      f((uint32_t)(ch * (int64_t)g.nkeys + c), col);
+    } else {
+      for (int p = 0; p < g.copies; ++p) {
+        const uint32_t bin = (uint32_t)(((int64_t)p * g.nchunks + ch) * g.nkeys + drop_letter(c, p, g.k));
+        f(bin, col | (letter_at(c, p, g.k) << 14));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                                   int64_t ldc, const int32_t *__restrict__ lens,
+                                                                   int rowlen, uint32_t *__restrict__ bcount) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  const int nbk = (int)g.nbuckets();
+  uint32_t *hist = sm;
+  int32_t *slen = (int32_t *)(hist + nbk);
+  uint8_t *srow = (uint8_t *)(slen + IDX_SEQS);
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
+  const int64_t j0 = (int64_t)blockIdx.x * IDX_SEQS;
+  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int fb = g.fine_bits;
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x)
+    if (hist[b]) atomicAdd(&bcount[b], hist[b]);
+}
+
+__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                                   int64_t ldc, const int32_t *__restrict__ lens,
+                                                                   int rowlen, uint32_t *__restrict__ bcursor,
+                                                                   uint32_t *__restrict__ tmp) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  const int nbk = (int)g.nbuckets();
+  uint32_t *hist = sm;
+  int32_t *slen = (int32_t *)(hist + nbk);
+  uint8_t *srow = (uint8_t *)(slen + IDX_SEQS);
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
+  const int64_t j0 = (int64_t)blockIdx.x * IDX_SEQS;
+  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int fb = g.fine_bits;
+  const uint32_t fmask = (1u << fb) - 1u;
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
+  __syncthreads();
+  // reserve this block's range inside every bucket it touches
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
+    const uint32_t c = hist[b];
+    if (c) hist[b] = atomicAdd(&bcursor[b], c);
+  }
+  __syncthreads();
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
+    const uint32_t pos = atomicAdd(&hist[bin >> fb], 1u);
+    tmp[pos] = ((bin & fmask) << 16) | val;
+  });
+}
+
+// block-wide exclusive scan over an LDS array of length len (in place); returns total
+__device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
+  const int nt = blockDim.x, t = threadIdx.x;
+  const int per = (len + nt - 1) / nt;
+  const int b0 = t * per, b1 = min(len, b0 + per);
+  uint32_t s = 0;
+  for (int q = b0; q < b1; ++q) s += a[q];
+  // wave scan
+  const int lane = t & 63, wave = t >> 6, nw = nt >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) wtmp[wave] = inc;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (int w = 0; w < nw; ++w) {
+    if (w < wave) base += wtmp[w];
+    total += wtmp[w];
+  }
+  uint32_t run = base + inc - s;
+  for (int q = b0; q < b1; ++q) {
+    const uint32_t v = a[q];
+    a[q] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+// one block per coarse bucket: fine histogram -> off[], then place values into ent[]
+__global__ __launch_bounds__(IDX_THREADS) void bucket_fine_kernel(IndexGeom g, const uint32_t *__restrict__ boff,
+                                                                  const uint32_t *__restrict__ tmp,
+                                                                  uint32_t *__restrict__ off,
+                                                                  uint16_t *__restrict__ ent) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  __shared__ uint32_t wtmp[IDX_THREADS / 64];
+  const int fb = g.fine_bits;
+  const int nf = 1 << fb;
+  uint32_t *fh = sm;
+  const int b = blockIdx.x;
+  const uint32_t s0 = boff[b], s1 = boff[b + 1];
+  for (int f = threadIdx.x; f < nf; f += blockDim.x) fh[f] = 0;
+  __syncthreads();
+  for (uint32_t t = s0 + threadIdx.x; t < s1; t += blockDim.x) atomicAdd(&fh[tmp[t] >> 16], 1u);
+  __syncthreads();
+  lds_excl_scan(fh, nf, wtmp);
+  const int64_t nb = g.nbins();
+  const int64_t bin0 = (int64_t)b << fb;
+  for (int f = threadIdx.x; f < nf; f += blockDim.x) {
+    const int64_t bin = bin0 + f;
+    if (bin < nb) off[bin] = s0 + fh[f];
+  }
+  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) off[nb] = s1;
+  __syncthreads();
+  for (uint32_t t = s0 + threadIdx.x; t < s1; t += blockDim.x) {
+    const uint32_t it = tmp[t];
+    const uint32_t pos = atomicAdd(&fh[it >> 16], 1u);
+    ent[s0 + pos] = (uint16_t)(it & 0xFFFFu);
+  }
+}
+
+// plain k-mer extraction (Hamming formulation and the diagonal kernels)
 __global__ __launch_bounds__(256) void extract_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
                                                       const int32_t *__restrict__ lens, int64_t ldc,
-                                                      uint32_t *__restrict__ kmers,
-                                                      uint32_t *__restrict__ hist) {
+                                                      uint32_t *__restrict__ kmers) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= g.n * g.pmax) return;
   const int64_t j = t / g.pmax;
   const int a = (int)(t - j * g.pmax);
   const int L = g.window > 0 ? g.window : lens[j];
-  const int P = L - g.k + 1;  // number of windows (range(len(x)-k+1), kernels.py:21)
   uint32_t code = KMG_INVALID;
-  if (a < P) {
+  if (a <= L - g.k) {
     const uint8_t *s = codes + j * ldc + a;
     uint32_t c = 0, bad = 0;
     for (int q = 0; q < g.k; ++q) {
       const uint32_t v = s[q];
-      bad |= v & ~3u;  // non-ACGT symbol: k-mer equals no beta (kernels.py:23-24)
+      bad |= v & ~3u;
       c = (c << 2) | (v & 3u);
     }
     if (!bad) code = c;
   }
   kmers[t] = code;
-  if (code == KMG_INVALID) return;
-  const int ch = (int)(j / g.chunk);
-  if (g.copies == 1) {
-    atomicAdd(&hist[(size_t)ch * g.nkeys + code], 1u);
-  } else {
-    for (int p = 0; p < g.copies; ++p) {
-      const size_t bin = ((size_t)p * g.nchunks + ch) * g.nkeys + drop_letter(code, p, g.k);
-      atomicAdd(&hist[bin], 1u);
-    }
-  }
 }
 
-__global__ __launch_bounds__(256) void scatter_kernel(IndexGeom g, const uint32_t *__restrict__ kmers,
-                                                      uint32_t *__restrict__ cursor,
-                                                      uint32_t *__restrict__ ent) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= g.n * g.pmax) return;
-  const uint32_t code = kmers[t];
-  if (code == KMG_INVALID) return;
-  const int64_t j = t / g.pmax;
-  const int ch = (int)(j / g.chunk);
-  const uint32_t jj = (uint32_t)(j - (int64_t)ch * g.chunk);
-  if (g.copies == 1) {
-    const uint32_t pos = atomicAdd(&cursor[(size_t)ch * g.nkeys + code], 1u);
-    ent[pos] = jj;
-  } else {
-    for (int p = 0; p < g.copies; ++p) {
-      const size_t bin = ((size_t)p * g.nchunks + ch) * g.nkeys + drop_letter(code, p, g.k);
-      const uint32_t pos = atomicAdd(&cursor[bin], 1u);
-      ent[pos] = jj | (letter_at(code, p, g.k) << KMG_ENTRY_LETTER_SHIFT);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ scan
-// Three-phase exclusive scan over uint32 (counts < 2^32 checked by the host).
+// ------------------------------------------------------------------ scan (bucket counts)
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
@@ -97,7 +231,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// exclusive scan of one value per thread across the block; returns the block total
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t &excl, uint32_t *tmp) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint32_t inc = wave_incl_scan(v);
@@ -166,33 +299,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_finalize_kernel(
     }
     run += v[q];
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    const int64_t np = gridDim.x;
-    off[nb] = partials[np];
-  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) off[nb] = partials[gridDim.x];
 }
 
 size_t scan_partials_words(int64_t nb) { return (size_t)((nb + SCAN_TILE - 1) / SCAN_TILE) + 1; }
-
-hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                          int64_t ldc, uint32_t *kmers, uint32_t *hist, hipStream_t s) {
-  const int64_t items = g.n * g.pmax;
-  if (items == 0) return hipSuccess;
-  const int64_t blocks = (items + 255) / 256;
-  hipLaunchKernelGGL(extract_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, codes, lens, ldc,
-                     kmers, hist);
-  return hipGetLastError();
-}
-
-hipError_t launch_scatter(const IndexGeom &g, const uint32_t *kmers, uint32_t *cursor,
-                          uint32_t *ent, hipStream_t s) {
-  const int64_t items = g.n * g.pmax;
-  if (items == 0) return hipSuccess;
-  const int64_t blocks = (items + 255) / 256;
-  hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, kmers, cursor,
-                     ent);
-  return hipGetLastError();
-}
 
 hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, int64_t nb,
                        uint32_t *partials, hipStream_t s) {
@@ -203,6 +313,55 @@ hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, in
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, s, partials, tiles);
   hipLaunchKernelGGL(scan_finalize_kernel, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, s, hist,
                      nb, partials, off, cursor);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ launchers
+static int part_rowlen(const IndexGeom &g, int64_t ldc) {
+  return g.window > 0 ? g.window : (int)ldc;
+}
+
+static size_t part_lds(const IndexGeom &g, int rowlen) {
+  return sizeof(uint32_t) * (size_t)g.nbuckets() + sizeof(int32_t) * IDX_SEQS +
+         (size_t)IDX_SEQS * rowlen + 16;
+}
+
+hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, uint32_t *bcount, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  const int rowlen = part_rowlen(g, ldc);
+  const unsigned blocks = (unsigned)((g.n + IDX_SEQS - 1) / IDX_SEQS);
+  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(IDX_THREADS), part_lds(g, rowlen), s,
+                     g, codes, ldc, lens, rowlen, bcount);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, uint32_t *bcursor, uint32_t *tmp, hipStream_t s) {
+  if (g.n == 0) return hipSuccess;
+  const int rowlen = part_rowlen(g, ldc);
+  const unsigned blocks = (unsigned)((g.n + IDX_SEQS - 1) / IDX_SEQS);
+  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(IDX_THREADS), part_lds(g, rowlen), s,
+                     g, codes, ldc, lens, rowlen, bcursor, tmp);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
+                             uint32_t *off, uint16_t *ent, hipStream_t s) {
+  const int64_t nbk = g.nbuckets();
+  const size_t lds = sizeof(uint32_t) * ((size_t)1 << g.fine_bits);
+  hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(IDX_THREADS), lds, s, g, boff,
+                     tmp, off, ent);
+  return hipGetLastError();
+}
+
+hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                          int64_t ldc, uint32_t *kmers, hipStream_t s) {
+  const int64_t items = g.n * g.pmax;
+  if (items == 0) return hipSuccess;
+  const int64_t blocks = (items + 255) / 256;
+  hipLaunchKernelGGL(extract_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, codes, lens, ldc,
+                     kmers);
   return hipGetLastError();
 }
 

@@ -17,9 +17,9 @@ namespace kmg {
 // Posting index of k-mer occurrences, the MI355X replacement of the dense 4^k
 // feature vectors phi of get_phi_u / get_phi_km (kernels.py:12-25, 161-175).
 //   bins  = copies x nchunks x nkeys, laid out [copy][chunk][key]
-//   off   = exclusive scan of the bin counts (nbins + 1 entries)
-//   ent   = one uint32 per occurrence: column index inside its chunk (low 30 bits)
-//           | letter at the dropped position << 30 (mismatch index only)
+//   off   = bin start offsets (nbins + 1 entries)
+//   ent   = uint16 per occurrence: column inside its chunk (SP: 16 bits; MM: 14 bits)
+//           | letter at the dropped position << 14 (mismatch index only)
 struct IndexGeom {
   int k;            // k-mer length
   int window;       // 0: per-sequence length (spectrum); >0: fixed window (mismatch, 101)
@@ -29,17 +29,25 @@ struct IndexGeom {
   int nchunks;
   uint32_t nkeys;   // keys per (copy, chunk): 4^k or 4^(k-1)
   int64_t n;
-  int64_t nbins() const { return (int64_t)copies * nchunks * (int64_t)nkeys; }
+  int fine_bits;    // bins per coarse bucket = 2^fine_bits (partition pass)
+  __host__ __device__ int64_t nbins() const { return (int64_t)copies * nchunks * (int64_t)nkeys; }
+  __host__ __device__ int64_t nbuckets() const {
+    return (nbins() + ((int64_t)1 << fine_bits) - 1) >> fine_bits;
+  }
 };
 
-hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                          int64_t ldc, uint32_t *kmers, uint32_t *hist, hipStream_t s);
+hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, uint32_t *bcount, hipStream_t s);
 // exclusive scan of hist[0..nb) into off[0..nb] (off[nb] = total); cursor = off[0..nb)
 hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, int64_t nb,
                        uint32_t *partials, hipStream_t s);
 size_t scan_partials_words(int64_t nb);
-hipError_t launch_scatter(const IndexGeom &g, const uint32_t *kmers, uint32_t *cursor,
-                          uint32_t *ent, hipStream_t s);
+hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, uint32_t *bcursor, uint32_t *tmp, hipStream_t s);
+hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
+                             uint32_t *off, uint16_t *ent, hipStream_t s);
+hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                          int64_t ldc, uint32_t *kmers, hipStream_t s);
 
 // ---------------------------------------------------------------- Gram kernels
 struct OutSpec {
@@ -51,17 +59,19 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
 };
 
-hipError_t launch_gram_spectrum(const IndexGeom &g, const uint32_t *kmers, const uint32_t *off,
-                                const uint32_t *ent, int64_t row0, int64_t row1,
-                                const OutSpec &o, hipStream_t s);
-hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint32_t *kmers, const uint32_t *off,
-                                 const uint32_t *ent, int64_t row0, int64_t row1, int w0, int w1,
-                                 int w2, const OutSpec &o, hipStream_t s);
+hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                                int64_t ldc, const uint32_t *off, const uint16_t *ent,
+                                int64_t row0, int64_t row1, const OutSpec &o, hipStream_t s);
+hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                 const uint32_t *off, const uint16_t *ent, int64_t row0,
+                                 int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                 hipStream_t s);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
-hipError_t launch_diag_hamming(const IndexGeom &g, const uint32_t *kmers, const int64_t *wtab,
-                               double *diagv, double *dsq, hipStream_t s);
+hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                               int64_t ldc, const int64_t *wtab, double *diagv, double *dsq,
+                               hipStream_t s);
 
 struct SeqSpec {
   const uint8_t *codes;
@@ -78,9 +88,6 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
                           double lam2, int mirror, const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int window,
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
-hipError_t launch_gram_la_intended(const SeqSpec &q, int64_t row0, int64_t row1, int smith,
-                                   double e, double dgap, double beta, const OutSpec &o,
-                                   hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);
 
 // host-matrix helpers (normalize_K / center_K)
