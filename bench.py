@@ -19,7 +19,6 @@ of the dominant kernel and the oracle timed on the host cores (cpu_baseline).
 import argparse
 import ctypes
 import json
-import math
 import os
 import sys
 import time
@@ -33,6 +32,7 @@ import numpy as np  # noqa: E402
 from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
+from kmgram.shard import even_splits, weak_scaled_n  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
@@ -73,10 +73,6 @@ class Dist:
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
-
-
-def even_splits(n, parts):
-    return [n * r // parts for r in range(parts + 1)]
 
 
 def run_workload(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, allgather):
@@ -217,7 +213,7 @@ def main():
     if dist.world != args.gpus and dist.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
     ctx = L.Context(dist.local)
-    n = int(round(args.n * math.sqrt(dist.world) / 8.0)) * 8 if dist.world > 1 else args.n
+    n = weak_scaled_n(args.n, dist.world)
 
     sp = run_workload(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
                       args.steps, args.warmup, args.allgather)

@@ -171,11 +171,20 @@ int check_params(const kmg_params *p, int64_t n, int64_t ldc, int32_t dt) {
   return KMG_OK;
 }
 
+int env_or(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 // ----------------------------------------------------------------- posting index
 int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
                 int64_t ldc) {
+  // ~256-512 coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins
+  const int target_buckets = env_or("KMG_IDX_BUCKETS", 384);
   g.fine_bits = 8;
-  while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > 16384) ++g.fine_bits;
+  while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
+  g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 64));
+  g.part_threads = std::min(1024, std::max(64, env_or("KMG_IDX_THREADS", 1024)));
   const int64_t nb = g.nbins();
   const int64_t nbk = g.nbuckets();
   if (nbk > 16384) return fail(KMG_EUNSUPPORTED, "index too large (%lld bins)", (long long)nb);
@@ -212,11 +221,6 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
                               c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
   }
   return KMG_OK;
-}
-
-int env_or(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
 }
 
 void choose_chunks(IndexGeom &g, int max_chunk) {

@@ -31,7 +31,7 @@ __device__ __forceinline__ uint32_t drop_letter_g(uint32_t code, int p, int k) {
 }
 
 // ------------------------------------------------------------------ epilogue
-template <int DT>
+template <int DT, bool NT = false>
 __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, int64_t col,
                                       int cnt, int64_t v0, int64_t v1, int64_t v2, int64_t v3,
                                       bool norm) {
@@ -39,7 +39,12 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
   if constexpr (DT == KMG_I32) {
     int32_t *p = (int32_t *)o.out + il * o.ld + col;
     if (cnt == 4 && ((uintptr_t)p & 15) == 0) {
-      *(int4 *)p = make_int4((int)v0, (int)v1, (int)v2, (int)v3);
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      const v4i x = {(int)v0, (int)v1, (int)v2, (int)v3};
+      if constexpr (NT)
+        __builtin_nontemporal_store(x, (v4i *)p);
+      else
+        *(v4i *)p = x;
     } else {
       for (int q = 0; q < cnt; ++q) p[q] = (int32_t)v[q];
     }
@@ -91,7 +96,7 @@ __device__ __forceinline__ uint32_t window_code(const uint8_t *rs, int a, int k)
 // ------------------------------------------------------------------ spectrum
 // PACK16: two 16-bit counters per LDS word (valid when every K_ij <= 65535, i.e.
 // P_i * P_j <= 65535; the host checks P_max <= 255).
-template <bool PACK16, int DT>
+template <bool PACK16, int DT, bool NT>
 __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
                                                       const int32_t *__restrict__ lens, int64_t ldc,
                                                       const uint32_t *__restrict__ off,
@@ -148,7 +153,7 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t
       const uint4 w = *(const uint4 *)&acc[q];
       v0 = w.x; v1 = w.y; v2 = w.z; v3 = w.w;
     }
-    emit4<DT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
+    emit4<DT, NT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
   }
 }
 
@@ -280,6 +285,144 @@ __global__ __launch_bounds__(MM_THREADS) void gram_mm1_kernel(IndexGeom g, int n
   }
 }
 
+// ------------------------------------------------------------------ mismatch m=1, v2
+// Same enumeration as gram_mm1_kernel, restructured for the per-list cost:
+//  - K is a compile-time constant (k=4..12), so sub-list decoding is constant division;
+//  - per row, the drop-one-letter base keys key_p(u_a) and letters u_p live in LDS, and a
+//    type-2 list key is base XOR (letter delta << digit(q)) — no 64-bit shifting per list;
+//  - each lane group owns a CONTIGUOUS range of lists (same occurrence, consecutive
+//    sub-lists), decoded incrementally; the next list's bounds are prefetched while this
+//    list's entries load (4 per lane, G lanes per list).
+template <int K, int G>
+__global__ __launch_bounds__(MM_THREADS) void gram_mm1v2_kernel(IndexGeom g,
+                                                                const uint8_t *__restrict__ codes,
+                                                                int64_t ldc,
+                                                                const uint32_t *__restrict__ off,
+                                                                const uint16_t *__restrict__ ent,
+                                                                int64_t row0, int w0, int w1, int w2,
+                                                                OutSpec o) {
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int64_t il = blockIdx.x / g.nchunks;
+  const int64_t i = row0 + il;
+  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *basek = smem + accw;       // [P][K]: key_p(u_a) | u_p << 30
+  uint32_t *rowu = basek + P * K;      // [P]: u_a
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    basek[t] = drop_letter_g(u, p, K) | (letter_at_g(u, p, K) << 30);
+    if (p == 0) rowu[a] = u;
+  }
+  __syncthreads();
+
+  const uint32_t chunk_keys = (uint32_t)c * g.nkeys;          // + p * nchunks * nkeys
+  const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = P * NSUB;
+  const int per = (total + ngrp - 1) / ngrp;
+  int L = grp * per;
+  const int Lend = min(total, L + per);
+
+  // decode (a, s) incrementally; s -> (p, q, ci) via the fixed enumeration
+  int a = L / NSUB, s = L - a * NSUB;
+  int p = 0, q = -1, ci = 0;
+  auto set_sub = [&]() {
+    if (s < K) {
+      p = s; q = -1; ci = 0;
+    } else {
+      const int t = s - K, pi = t / 3;
+      ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      p = pp;
+      q = pi - pp * (pp - 1) / 2;
+    }
+  };
+  auto describe = [&](uint32_t &bin, uint32_t &up, int &wa, int &wb) {
+    const uint32_t bk = basek[a * K + p];
+    up = bk >> 30;
+    uint32_t key = bk & 0x3FFFFFFFu;
+    if (q < 0) {
+      wa = (p == 0) ? w0 : 0;
+      wb = w1;
+    } else {
+      const uint32_t lq = (rowu[a] >> (2 * (K - 1 - q))) & 3u;
+      const uint32_t nl = (lq + 1u + (uint32_t)ci) & 3u;
+      key ^= (lq ^ nl) << (2 * (K - 2 - q));  // q < p: digit of q inside key_p
+      wa = 0;
+      wb = w2;
+    }
+    bin = (uint32_t)p * copy_stride + chunk_keys + key;
+  };
+  auto advance = [&]() {
+    if (++s == NSUB) { s = 0; ++a; }
+    set_sub();
+  };
+  set_sub();
+
+  uint32_t beg = 0, end = 0, up = 0;
+  int wa = 0, wb = 0;
+  if (L < Lend) {
+    uint32_t bin;
+    describe(bin, up, wa, wb);
+    beg = off[bin];
+    end = off[bin + 1];
+  }
+  for (; L < Lend; ++L) {
+    uint32_t nbeg = 0, nend = 0, nup = 0;
+    int nwa = 0, nwb = 0;
+    if (L + 1 < Lend) {
+      advance();
+      uint32_t bin;
+      describe(bin, nup, nwa, nwb);
+      nbeg = off[bin];
+      nend = off[bin + 1];
+    }
+    const uint32_t e0 = beg + gl;
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (e0 + u * G < end) ? (uint32_t)ent[e0 + u * G] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u] != 0xFFFFFFFFu) {
+        const int w = ((v[u] >> 14) == up) ? wa : wb;
+        if (w) atomicAdd(&acc[v[u] & 0x3FFFu], w);
+      }
+    }
+    for (uint32_t e = e0 + 4 * G; e < end; e += G) {
+      const uint32_t x = ent[e];
+      const int w = ((x >> 14) == up) ? wa : wb;
+      if (w) atomicAdd(&acc[x & 0x3FFFu], w);
+    }
+    beg = nbeg;
+    end = nend;
+    up = nup;
+    wa = nwa;
+    wb = nwb;
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
 // ------------------------------------------------------------------ Hamming forms
 __device__ __forceinline__ int ham2bit(uint32_t a, uint32_t b, uint32_t mask55) {
   const uint32_t x = a ^ b;
@@ -359,6 +502,11 @@ __global__ __launch_bounds__(64) void diag_ham_kernel(IndexGeom g, const uint8_t
 }
 
 // ------------------------------------------------------------------ launchers
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 #define KMG_DISPATCH_DT(DT, ...)                       \
   switch (DT) {                                        \
     case KMG_I32: { constexpr int D = KMG_I32; __VA_ARGS__; } break; \
@@ -375,19 +523,18 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const 
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   const size_t lds = (size_t)words * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
-  if (pack) {
-    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D>), grid, dim3(256), lds, s,
-                                                g, codes, lens, ldc, off, ent, row0, o));
+  const bool nt = env_int("KMG_SP_NT", 1) != 0;
+  if (pack && nt) {
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true>), grid, dim3(256),
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+  } else if (pack) {
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, false>), grid, dim3(256),
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
   } else {
-    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<false, D>), grid, dim3(256), lds, s,
-                                                g, codes, lens, ldc, off, ent, row0, o));
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<false, D, false>), grid, dim3(256),
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
   }
   return hipGetLastError();
-}
-
-static int env_int(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
 }
 
 hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
@@ -404,6 +551,20 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
   int G = 1;
   while (G < 64 && G * 4 < avg) G *= 2;
   G = env_int("KMG_MM_G", G);
+  if (g.k >= 4 && g.k <= 12 && env_int("KMG_MM_VARIANT", 2) == 2) {
+    const size_t lds2 = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * (g.k + 1)) * 4;
+    const int G2 = G < 2 ? 2 : (G > 16 ? 16 : G);
+#define KMG_MM2(KK, GG)                                                                        \
+  if (g.k == KK && G2 == GG)                                                                   \
+    hipLaunchKernelGGL((gram_mm1v2_kernel<KK, GG>), grid, dim3(MM_THREADS), lds2, s, g, codes, \
+                       ldc, off, ent, row0, w0, w1, w2, o);
+#define KMG_MM2K(KK) KMG_MM2(KK, 2) KMG_MM2(KK, 4) KMG_MM2(KK, 8) KMG_MM2(KK, 16)
+    KMG_MM2K(4) KMG_MM2K(5) KMG_MM2K(6) KMG_MM2K(7) KMG_MM2K(8) KMG_MM2K(9) KMG_MM2K(10)
+    KMG_MM2K(11) KMG_MM2K(12)
+#undef KMG_MM2K
+#undef KMG_MM2
+    return hipGetLastError();
+  }
 #define KMG_MM_CASE(GG)                                                                    \
   case GG:                                                                                 \
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_mm1_kernel<GG, D>), grid,           \

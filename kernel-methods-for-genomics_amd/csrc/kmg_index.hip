@@ -32,14 +32,14 @@ __device__ __forceinline__ uint32_t drop_letter(uint32_t code, int p, int k) {
   return (uint32_t)(((c >> (lo_bits + 2)) << lo_bits) | (c & ((1ull << lo_bits) - 1ull)));
 }
 
-constexpr int IDX_THREADS = 256;
-constexpr int IDX_SEQS = 16;  // sequences per partition block
+constexpr int IDX_THREADS = 1024;  // upper bound; blocks launch g.part_threads
+constexpr int FINE_THREADS = 1024;
 
 // stage IDX_SEQS rows of codes in LDS; returns number of staged sequences
 __device__ __forceinline__ int stage_rows(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
                                           const int32_t *lens, uint8_t *srow, int32_t *slen,
                                           int rowlen, int64_t j0) {
-  const int ns = (int)min((int64_t)IDX_SEQS, g.n - j0);
+  const int ns = (int)min((int64_t)g.seqs_per_block, g.n - j0);
   for (int t = threadIdx.x; t < ns * rowlen; t += blockDim.x) {
     const int s = t / rowlen, c = t - s * rowlen;
     srow[t] = codes[(j0 + s) * ldc + c];
@@ -90,9 +90,9 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, 
   const int nbk = (int)g.nbuckets();
   uint32_t *hist = sm;
   int32_t *slen = (int32_t *)(hist + nbk);
-  uint8_t *srow = (uint8_t *)(slen + IDX_SEQS);
+  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
-  const int64_t j0 = (int64_t)blockIdx.x * IDX_SEQS;
+  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
   const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
   const int fb = g.fine_bits;
   for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
@@ -109,9 +109,9 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, 
   const int nbk = (int)g.nbuckets();
   uint32_t *hist = sm;
   int32_t *slen = (int32_t *)(hist + nbk);
-  uint8_t *srow = (uint8_t *)(slen + IDX_SEQS);
+  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
-  const int64_t j0 = (int64_t)blockIdx.x * IDX_SEQS;
+  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
   const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
   const int fb = g.fine_bits;
   const uint32_t fmask = (1u << fb) - 1u;
@@ -162,12 +162,12 @@ __device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
 }
 
 // one block per coarse bucket: fine histogram -> off[], then place values into ent[]
-__global__ __launch_bounds__(IDX_THREADS) void bucket_fine_kernel(IndexGeom g, const uint32_t *__restrict__ boff,
+__global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, const uint32_t *__restrict__ boff,
                                                                   const uint32_t *__restrict__ tmp,
                                                                   uint32_t *__restrict__ off,
                                                                   uint16_t *__restrict__ ent) {
   extern __shared__ __align__(16) uint32_t sm[];
-  __shared__ uint32_t wtmp[IDX_THREADS / 64];
+  __shared__ uint32_t wtmp[FINE_THREADS / 64];
   const int fb = g.fine_bits;
   const int nf = 1 << fb;
   uint32_t *fh = sm;
@@ -322,16 +322,16 @@ static int part_rowlen(const IndexGeom &g, int64_t ldc) {
 }
 
 static size_t part_lds(const IndexGeom &g, int rowlen) {
-  return sizeof(uint32_t) * (size_t)g.nbuckets() + sizeof(int32_t) * IDX_SEQS +
-         (size_t)IDX_SEQS * rowlen + 16;
+  return sizeof(uint32_t) * (size_t)g.nbuckets() + sizeof(int32_t) * g.seqs_per_block +
+         (size_t)g.seqs_per_block * rowlen + 16;
 }
 
 hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
                               int64_t ldc, uint32_t *bcount, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int rowlen = part_rowlen(g, ldc);
-  const unsigned blocks = (unsigned)((g.n + IDX_SEQS - 1) / IDX_SEQS);
-  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(IDX_THREADS), part_lds(g, rowlen), s,
+  const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
+  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen), s,
                      g, codes, ldc, lens, rowlen, bcount);
   return hipGetLastError();
 }
@@ -340,8 +340,8 @@ hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const in
                               int64_t ldc, uint32_t *bcursor, uint32_t *tmp, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int rowlen = part_rowlen(g, ldc);
-  const unsigned blocks = (unsigned)((g.n + IDX_SEQS - 1) / IDX_SEQS);
-  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(IDX_THREADS), part_lds(g, rowlen), s,
+  const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
+  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen), s,
                      g, codes, ldc, lens, rowlen, bcursor, tmp);
   return hipGetLastError();
 }
@@ -350,7 +350,7 @@ hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uin
                              uint32_t *off, uint16_t *ent, hipStream_t s) {
   const int64_t nbk = g.nbuckets();
   const size_t lds = sizeof(uint32_t) * ((size_t)1 << g.fine_bits);
-  hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(IDX_THREADS), lds, s, g, boff,
+  hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(FINE_THREADS), lds, s, g, boff,
                      tmp, off, ent);
   return hipGetLastError();
 }

@@ -30,6 +30,8 @@ struct IndexGeom {
   uint32_t nkeys;   // keys per (copy, chunk): 4^k or 4^(k-1)
   int64_t n;
   int fine_bits;    // bins per coarse bucket = 2^fine_bits (partition pass)
+  int seqs_per_block;  // partition pass: sequences per block
+  int part_threads;    // partition pass: threads per block
   __host__ __device__ int64_t nbins() const { return (int64_t)copies * nchunks * (int64_t)nkeys; }
   __host__ __device__ int64_t nbuckets() const {
     return (nbins() + ((int64_t)1 << fine_bits) - 1) >> fine_bits;
