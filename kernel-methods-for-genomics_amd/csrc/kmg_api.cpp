@@ -98,6 +98,7 @@ struct kmg_ctx {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_log;
   size_t ev_used = 0;
   int last_call_first = 0;
+  bool index_dirty = false;
   int64_t wtab_host[33] = {};
   bool wtab_valid = false;
   ncclComm_t comm = nullptr;
@@ -184,6 +185,11 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
   g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 64));
+  {
+    const int rowlen0 = g.window > 0 ? g.window : (int)ldc;
+    const int64_t budget = 150 * 1024 - 8 * (g.nbins() >> g.fine_bits) - 4096;
+    g.seqs_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(g.seqs_per_block, budget / (rowlen0 + 4)));
+  }
   g.part_threads = std::min(1024, std::max(64, env_or("KMG_IDX_THREADS", 1024)));
   const int64_t nb = g.nbins();
   const int64_t nbk = g.nbuckets();
@@ -193,33 +199,38 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   const int64_t items = g.n * g.pmax * g.copies;
   if ((double)items >= 4294967295.0)
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
+  const bool realloc = c->bcount.bytes < sizeof(uint32_t) * (size_t)nbk ||
+                       c->bcursor.bytes < sizeof(uint32_t) * (size_t)nbk;
   KMG_TRY(c->bcount.ensure(sizeof(uint32_t) * (size_t)nbk));
   KMG_TRY(c->boff.ensure(sizeof(uint32_t) * (size_t)(nbk + 1)));
   KMG_TRY(c->bcursor.ensure(sizeof(uint32_t) * (size_t)nbk));
-  KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nbk)));
   KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
   KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
   KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items > 0 ? items : 1)));
+  // bucket counters are zero between calls (the fine pass re-zeroes them); only a fresh
+  // allocation or an interrupted previous build needs an explicit clear
+  if (realloc || c->index_dirty) {
+    KMG_HIP(hipMemsetAsync(c->bcount.p, 0, c->bcount.bytes, c->stream));
+    KMG_HIP(hipMemsetAsync(c->bcursor.p, 0, c->bcursor.bytes, c->stream));
+  }
+  c->index_dirty = true;
   {
     StageTimer t(c, ST_COUNT);
-    KMG_HIP(hipMemsetAsync(c->bcount.p, 0, sizeof(uint32_t) * (size_t)nbk, c->stream));
     KMG_HIP(launch_index_count(g, d_codes, d_lens, ldc, c->bcount.as<uint32_t>(), c->stream));
   }
   {
-    StageTimer t(c, ST_SCAN);
-    KMG_HIP(launch_scan(c->bcount.as<uint32_t>(), c->boff.as<uint32_t>(),
-                        c->bcursor.as<uint32_t>(), nbk, c->partials.as<uint32_t>(), c->stream));
-  }
-  {
     StageTimer t(c, ST_PLACE);
-    KMG_HIP(launch_index_place(g, d_codes, d_lens, ldc, c->bcursor.as<uint32_t>(),
+    KMG_HIP(launch_index_place(g, d_codes, d_lens, ldc, c->bcount.as<uint32_t>(),
+                               c->bcursor.as<uint32_t>(), c->boff.as<uint32_t>(),
                                c->tmp.as<uint32_t>(), c->stream));
   }
   {
     StageTimer t(c, ST_FINE);
     KMG_HIP(launch_index_fine(g, c->boff.as<uint32_t>(), c->tmp.as<uint32_t>(),
-                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
+                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                              c->bcount.as<uint32_t>(), c->bcursor.as<uint32_t>(), c->stream));
   }
+  c->index_dirty = false;
   return KMG_OK;
 }
 
@@ -291,6 +302,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const bool s1 = mm && p->m == 1 && k >= 2 && k <= 12;  // drop-one-letter index
       const bool use_index = (exact && k <= 12) || s1;
+      const bool use_rot = s1 && k >= 4 && env_or("KMG_MM_VARIANT", 3) == 3;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       if (!use_index) {
@@ -321,6 +333,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
         choose_chunks(g, std::min(65536, env_or("KMG_SP_CHUNK", 24576)));
+      } else if (use_rot) {
+        g.copies = k;
+        g.rot = 1;
+        g.nkeys = (uint32_t)pow4(k);
+        choose_chunks(g, std::min(65536, env_or("KMG_MM_CHUNK", 20480)));
       } else {
         g.copies = k;
         g.nkeys = (uint32_t)pow4(k - 1);
@@ -339,9 +356,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_HIP(launch_gram_spectrum(g, d_codes, d_lens, ldc, c->off.as<uint32_t>(),
                                      c->ent.as<uint16_t>(), row0, row1, o, c->stream));
       } else {
-        KMG_HIP(launch_gram_mismatch1(g, d_codes, ldc, c->off.as<uint32_t>(),
-                                      c->ent.as<uint16_t>(), row0, row1, (int)w[0], (int)w[1],
-                                      (int)w[2], o, c->stream));
+        if (use_rot)
+          KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
+                                            c->ent.as<uint16_t>(), row0, row1, (int)w[0],
+                                            (int)w[1], (int)w[2], o, c->stream));
+        else
+          KMG_HIP(launch_gram_mismatch1(g, d_codes, ldc, c->off.as<uint32_t>(),
+                                        c->ent.as<uint16_t>(), row0, row1, (int)w[0], (int)w[1],
+                                        (int)w[2], o, c->stream));
       }
       return KMG_OK;
     }

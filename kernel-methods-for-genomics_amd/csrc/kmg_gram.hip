@@ -423,6 +423,152 @@ __global__ __launch_bounds__(MM_THREADS) void gram_mm1v2_kernel(IndexGeom g,
   }
 }
 
+// ------------------------------------------------------------------ mismatch m=1, v3
+// Rotated layout: copy p lists every occurrence z under rot_p(z) = key_p(z)*4 + z_p, so
+// the drop-one-letter list (p, key) is the 4 adjacent bins key*4 .. key*4+3, one per
+// letter at p.  A list is then 3 segments: letters below u_p (weight wb), letter u_p
+// (weight wa, skipped unloaded when wa == 0) and letters above u_p (weight wb).
+// Entries are plain 16-bit columns (chunks up to 65536 columns).
+template <int K, int G>
+__global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
+                                                                 const uint8_t *__restrict__ codes,
+                                                                 int64_t ldc,
+                                                                 const uint32_t *__restrict__ off,
+                                                                 const uint16_t *__restrict__ ent,
+                                                                 int64_t row0, int w0, int w1, int w2,
+                                                                 OutSpec o) {
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int64_t il = blockIdx.x / g.nchunks;
+  const int64_t i = row0 + il;
+  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accw;  // [P][K]: rot_p(u_a)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  __syncthreads();
+
+  const uint32_t chunk_bins = (uint32_t)c * g.nkeys;
+  const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = P * NSUB;
+  const int per = (total + ngrp - 1) / ngrp;
+  int L = grp * per;
+  const int Lend = min(total, L + per);
+
+  int a = L / NSUB, s = L - a * NSUB;
+  int p = 0, q = -1, ci = 0;
+  auto set_sub = [&]() {
+    if (s < K) {
+      p = s; q = -1; ci = 0;
+    } else {
+      const int t = s - K, pi = t / 3;
+      ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      p = pp;
+      q = pi - pp * (pp - 1) / 2;
+    }
+  };
+  // list -> base bin of its 4 letter sub-lists, u_p, weights
+  auto describe = [&](uint32_t &base, uint32_t &up, int &wa, int &wb) {
+    const uint32_t rk = rotk[a * K + p];
+    up = rk & 3u;
+    uint32_t key = rk >> 2;
+    if (q < 0) {
+      wa = (p == 0) ? w0 : 0;
+      wb = w1;
+    } else {
+      // letter q of u sits at key digit q (q < p); substitute the ci-th other letter
+      const int sh = 2 * (K - 2 - q);
+      const uint32_t lq = (key >> sh) & 3u;
+      const uint32_t nl = (lq + 1u + (uint32_t)ci) & 3u;
+      key ^= (lq ^ nl) << sh;
+      wa = 0;
+      wb = w2;
+    }
+    base = (uint32_t)p * copy_stride + chunk_bins + (key << 2);
+  };
+  auto advance = [&]() {
+    if (++s == NSUB) { s = 0; ++a; }
+    set_sub();
+  };
+  set_sub();
+
+  // segment bounds of the current list: [b0,b1) wb, [b1,b2) wa, [b2,b3) wb
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+  int wa = 0, wb = 0;
+  auto load_bounds = [&](uint32_t base, uint32_t up, uint32_t &x0, uint32_t &x1, uint32_t &x2,
+                         uint32_t &x3) {
+    const uint4 o4 = *(const uint4 *)(off + base);  // base % 4 == 0: 16-byte aligned
+    const uint32_t o5 = off[base + 4];
+    const uint32_t lo = up == 0 ? o4.x : up == 1 ? o4.y : up == 2 ? o4.z : o4.w;
+    const uint32_t hi = up == 0 ? o4.y : up == 1 ? o4.z : up == 2 ? o4.w : o5;
+    x0 = o4.x; x1 = lo; x2 = hi; x3 = o5;
+  };
+  if (L < Lend) {
+    uint32_t base, up;
+    describe(base, up, wa, wb);
+    load_bounds(base, up, b0, b1, b2, b3);
+  }
+  for (; L < Lend; ++L) {
+    uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+    int nwa = 0, nwb = 0;
+    if (L + 1 < Lend) {
+      advance();
+      uint32_t base, up;
+      describe(base, up, nwa, nwb);
+      load_bounds(base, up, n0, n1, n2, n3);
+    }
+    // virtual index t over [b0,b1) ++ ([b1,b2) if wa) ++ [b2,b3)
+    const uint32_t lA = b1 - b0, lB = wa ? (b2 - b1) : 0u, lC = b3 - b2;
+    const uint32_t tot = lA + lB + lC;
+    for (uint32_t t0 = 0; t0 < tot; t0 += 4 * G) {
+      uint32_t col[4];
+      int wt[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t t = t0 + u * G + gl;
+        uint32_t e;
+        int w;
+        if (t < lA) { e = b0 + t; w = wb; }
+        else if (t < lA + lB) { e = b1 + (t - lA); w = wa; }
+        else { e = b2 + (t - lA - lB); w = wb; }
+        wt[u] = (t < tot) ? w : 0;
+        col[u] = (t < tot) ? (uint32_t)ent[e] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (wt[u]) atomicAdd(&acc[col[u]], wt[u]);
+    }
+    b0 = n0; b1 = n1; b2 = n2; b3 = n3;
+    wa = nwa;
+    wb = nwb;
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
 // ------------------------------------------------------------------ Hamming forms
 __device__ __forceinline__ int ham2bit(uint32_t a, uint32_t b, uint32_t mask55) {
   const uint32_t x = a ^ b;
@@ -582,6 +728,33 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
       KMG_MM_CASE(64)
   }
 #undef KMG_MM_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                     const uint32_t *off, const uint16_t *ent, int64_t row0,
+                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                     hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || g.n == 0) return hipSuccess;
+  if (g.k < 4 || g.k > 12) return hipErrorNotSupported;
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k) * 4;
+  const dim3 grid((unsigned)(rows * g.nchunks));
+  const double avg = (double)g.chunk * g.pmax / ((double)g.nkeys / 4.0);  // per 4-bin list
+  int G = 2;
+  while (G < 16 && G * 4 < avg) G *= 2;
+  G = env_int("KMG_MM_G", G);
+  G = G < 2 ? 2 : (G > 16 ? 16 : G);
+  const int threads = env_int("KMG_MM_THREADS", 512) >= 1024 ? 1024 : 512;
+#define KMG_MM3(KK, GG)                                                                         \
+  if (g.k == KK && G == GG)                                                                     \
+    hipLaunchKernelGGL((gram_mm1rot_kernel<KK, GG>), grid, dim3(threads), lds, s, g, codes,     \
+                       ldc, off, ent, row0, w0, w1, w2, o);
+#define KMG_MM3K(KK) KMG_MM3(KK, 2) KMG_MM3(KK, 4) KMG_MM3(KK, 8) KMG_MM3(KK, 16)
+  KMG_MM3K(4) KMG_MM3K(5) KMG_MM3K(6) KMG_MM3K(7) KMG_MM3K(8) KMG_MM3K(9) KMG_MM3K(10)
+  KMG_MM3K(11) KMG_MM3K(12)
+#undef KMG_MM3K
+#undef KMG_MM3
   return hipGetLastError();
 }
 

@@ -74,6 +74,11 @@ __device__ __forceinline__ void for_items(const IndexGeom &g, const uint8_t *sro
     const uint32_t col = (uint32_t)(j - (int64_t)ch * g.chunk);
     if (g.copies == 1) {
       f((uint32_t)(ch * (int64_t)g.nkeys + c), col);
+    } else if (g.rot) {
+      for (int p = 0; p < g.copies; ++p) {
+        const uint32_t rk = (drop_letter(c, p, g.k) << 2) | letter_at(c, p, g.k);
+        f((uint32_t)(((int64_t)p * g.nchunks + ch) * g.nkeys + rk), col);
+      }
     } else {
       for (int p = 0; p < g.copies; ++p) {
         const uint32_t bin = (uint32_t)(((int64_t)p * g.nchunks + ch) * g.nkeys + drop_letter(c, p, g.k));
@@ -99,34 +104,6 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, 
   __syncthreads();
   for (int b = threadIdx.x; b < nbk; b += blockDim.x)
     if (hist[b]) atomicAdd(&bcount[b], hist[b]);
-}
-
-__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
-                                                                   int64_t ldc, const int32_t *__restrict__ lens,
-                                                                   int rowlen, uint32_t *__restrict__ bcursor,
-                                                                   uint32_t *__restrict__ tmp) {
-  extern __shared__ __align__(16) uint32_t sm[];
-  const int nbk = (int)g.nbuckets();
-  uint32_t *hist = sm;
-  int32_t *slen = (int32_t *)(hist + nbk);
-  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
-  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
-  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
-  const int fb = g.fine_bits;
-  const uint32_t fmask = (1u << fb) - 1u;
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
-  __syncthreads();
-  // reserve this block's range inside every bucket it touches
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
-    const uint32_t c = hist[b];
-    if (c) hist[b] = atomicAdd(&bcursor[b], c);
-  }
-  __syncthreads();
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
-    const uint32_t pos = atomicAdd(&hist[bin >> fb], 1u);
-    tmp[pos] = ((bin & fmask) << 16) | val;
-  });
 }
 
 // block-wide exclusive scan over an LDS array of length len (in place); returns total
@@ -161,11 +138,58 @@ __device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
   return total;
 }
 
+// Every block recomputes the exclusive scan of the bucket totals (nbuckets <= 16384,
+// cheap) so no separate scan launch is needed; block 0 publishes it as boff[] for the
+// fine pass.  Positions inside a bucket: base + one returning add per (block, bucket)
+// on the relative cursor bcursor[] (zero on entry; re-zeroed by the fine pass).
+__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                                   int64_t ldc, const int32_t *__restrict__ lens,
+                                                                   int rowlen, const uint32_t *__restrict__ bcount,
+                                                                   uint32_t *__restrict__ bcursor,
+                                                                   uint32_t *__restrict__ boff,
+                                                                   uint32_t *__restrict__ tmp) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  __shared__ uint32_t wtmp[IDX_THREADS / 64];
+  const int nbk = (int)g.nbuckets();
+  uint32_t *hist = sm;
+  uint32_t *base = hist + nbk;
+  int32_t *slen = (int32_t *)(base + nbk);
+  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
+    hist[b] = 0;
+    base[b] = bcount[b];
+  }
+  __syncthreads();
+  const uint32_t total = lds_excl_scan(base, nbk, wtmp);
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < nbk; b += blockDim.x) boff[b] = base[b];
+    if (threadIdx.x == 0) boff[nbk] = total;
+  }
+  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
+  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int fb = g.fine_bits;
+  const uint32_t fmask = (1u << fb) - 1u;
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
+  __syncthreads();
+  // reserve this block's range inside every bucket it touches
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
+    const uint32_t c = hist[b];
+    if (c) hist[b] = base[b] + atomicAdd(&bcursor[b], c);
+  }
+  __syncthreads();
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
+    const uint32_t pos = atomicAdd(&hist[bin >> fb], 1u);
+    tmp[pos] = ((bin & fmask) << 16) | val;
+  });
+}
+
 // one block per coarse bucket: fine histogram -> off[], then place values into ent[]
 __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, const uint32_t *__restrict__ boff,
                                                                   const uint32_t *__restrict__ tmp,
                                                                   uint32_t *__restrict__ off,
-                                                                  uint16_t *__restrict__ ent) {
+                                                                  uint16_t *__restrict__ ent,
+                                                                  uint32_t *__restrict__ bcount,
+                                                                  uint32_t *__restrict__ bcursor) {
   extern __shared__ __align__(16) uint32_t sm[];
   __shared__ uint32_t wtmp[FINE_THREADS / 64];
   const int fb = g.fine_bits;
@@ -173,6 +197,10 @@ __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, 
   uint32_t *fh = sm;
   const int b = blockIdx.x;
   const uint32_t s0 = boff[b], s1 = boff[b + 1];
+  if (threadIdx.x == 0) {  // leave the counters zero for the next call (no memset launch)
+    bcount[b] = 0;
+    bcursor[b] = 0;
+  }
   for (int f = threadIdx.x; f < nf; f += blockDim.x) fh[f] = 0;
   __syncthreads();
   for (uint32_t t = s0 + threadIdx.x; t < s1; t += blockDim.x) atomicAdd(&fh[tmp[t] >> 16], 1u);
@@ -321,8 +349,8 @@ static int part_rowlen(const IndexGeom &g, int64_t ldc) {
   return g.window > 0 ? g.window : (int)ldc;
 }
 
-static size_t part_lds(const IndexGeom &g, int rowlen) {
-  return sizeof(uint32_t) * (size_t)g.nbuckets() + sizeof(int32_t) * g.seqs_per_block +
+static size_t part_lds(const IndexGeom &g, int rowlen, int arrays) {
+  return sizeof(uint32_t) * (size_t)g.nbuckets() * arrays + sizeof(int32_t) * g.seqs_per_block +
          (size_t)g.seqs_per_block * rowlen + 16;
 }
 
@@ -331,27 +359,30 @@ hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const in
   if (g.n == 0) return hipSuccess;
   const int rowlen = part_rowlen(g, ldc);
   const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen), s,
+  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen, 1), s,
                      g, codes, ldc, lens, rowlen, bcount);
   return hipGetLastError();
 }
 
 hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, uint32_t *bcursor, uint32_t *tmp, hipStream_t s) {
+                              int64_t ldc, const uint32_t *bcount, uint32_t *bcursor,
+                              uint32_t *boff, uint32_t *tmp, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
   const int rowlen = part_rowlen(g, ldc);
   const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen), s,
-                     g, codes, ldc, lens, rowlen, bcursor, tmp);
+  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads),
+                     part_lds(g, rowlen, 2), s, g, codes, ldc, lens, rowlen, bcount, bcursor, boff,
+                     tmp);
   return hipGetLastError();
 }
 
 hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
-                             uint32_t *off, uint16_t *ent, hipStream_t s) {
+                             uint32_t *off, uint16_t *ent, uint32_t *bcount, uint32_t *bcursor,
+                             hipStream_t s) {
   const int64_t nbk = g.nbuckets();
   const size_t lds = sizeof(uint32_t) * ((size_t)1 << g.fine_bits);
   hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(FINE_THREADS), lds, s, g, boff,
-                     tmp, off, ent);
+                     tmp, off, ent, bcount, bcursor);
   return hipGetLastError();
 }
 

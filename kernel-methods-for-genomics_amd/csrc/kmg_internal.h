@@ -30,6 +30,8 @@ struct IndexGeom {
   uint32_t nkeys;   // keys per (copy, chunk): 4^k or 4^(k-1)
   int64_t n;
   int fine_bits;    // bins per coarse bucket = 2^fine_bits (partition pass)
+  int rot;             // mismatch layout: copy p keyed by the k-mer with letter p rotated
+                       // to the lowest digit (4 adjacent letter sub-lists); entry = column
   int seqs_per_block;  // partition pass: sequences per block
   int part_threads;    // partition pass: threads per block
   __host__ __device__ int64_t nbins() const { return (int64_t)copies * nchunks * (int64_t)nkeys; }
@@ -44,10 +46,14 @@ hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const in
 hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, int64_t nb,
                        uint32_t *partials, hipStream_t s);
 size_t scan_partials_words(int64_t nb);
+// place: every block scans the bucket totals itself (block 0 publishes boff[])
 hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, uint32_t *bcursor, uint32_t *tmp, hipStream_t s);
+                              int64_t ldc, const uint32_t *bcount, uint32_t *bcursor,
+                              uint32_t *boff, uint32_t *tmp, hipStream_t s);
+// fine: per-bucket fine histogram -> off[], ent[]; re-zeroes bcount[]/bcursor[]
 hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
-                             uint32_t *off, uint16_t *ent, hipStream_t s);
+                             uint32_t *off, uint16_t *ent, uint32_t *bcount, uint32_t *bcursor,
+                             hipStream_t s);
 hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
                           int64_t ldc, uint32_t *kmers, hipStream_t s);
 
@@ -69,6 +75,11 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
                                  int64_t row1, int w0, int w1, int w2, const OutSpec &o,
                                  hipStream_t s);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
+// mismatch (k,1) on the rotated layout (rot=1, nkeys = 4^k)
+hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                     const uint32_t *off, const uint16_t *ent, int64_t row0,
+                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                     hipStream_t s);
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
 hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
