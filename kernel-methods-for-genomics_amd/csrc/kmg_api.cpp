@@ -206,7 +206,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   KMG_TRY(c->bcursor.ensure(sizeof(uint32_t) * (size_t)nbk));
   KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
   KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
-  KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items > 0 ? items : 1)));
+  KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 64)));  // + pad: clamped reads
   // bucket counters are zero between calls (the fine pass re-zeroes them); only a fresh
   // allocation or an interrupted previous build needs an explicit clear
   if (realloc || c->index_dirty) {
@@ -279,6 +279,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
   if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
   OutSpec o{d_out, ld, dt, 0, nullptr, nullptr};
   const int64_t rows = row1 - row0;
+  if (env_or("KMG_POISON", 0) && rows > 0 && n > 0)  // testing: no stale output can pass
+    KMG_HIP(hipMemset2DAsync(d_out, (size_t)ld * dtype_size(dt), 0xA5, (size_t)n * dtype_size(dt),
+                             (size_t)rows, c->stream));
   switch (p->kind) {
     case KMG_SPECTRUM:
     case KMG_MISMATCH: {
@@ -302,7 +305,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const bool s1 = mm && p->m == 1 && k >= 2 && k <= 12;  // drop-one-letter index
       const bool use_index = (exact && k <= 12) || s1;
-      const bool use_rot = s1 && k >= 4 && env_or("KMG_MM_VARIANT", 3) == 3;
+      const bool use_rot = s1 && k >= 4 && env_or("KMG_MM_VARIANT", 6) >= 3;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       if (!use_index) {
@@ -358,8 +361,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       } else {
         if (use_rot)
           KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
-                                            c->ent.as<uint16_t>(), row0, row1, (int)w[0],
-                                            (int)w[1], (int)w[2], o, c->stream));
+                                            c->ent.as<uint16_t>(),
+                                            (uint32_t)(c->ent.bytes / sizeof(uint16_t)), row0,
+                                            row1, (int)w[0], (int)w[1], (int)w[2], o, c->stream));
         else
           KMG_HIP(launch_gram_mismatch1(g, d_codes, ldc, c->off.as<uint32_t>(),
                                         c->ent.as<uint16_t>(), row0, row1, (int)w[0], (int)w[1],

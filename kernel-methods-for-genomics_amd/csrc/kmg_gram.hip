@@ -431,12 +431,12 @@ __global__ __launch_bounds__(MM_THREADS) void gram_mm1v2_kernel(IndexGeom g,
 // Entries are plain 16-bit columns (chunks up to 65536 columns).
 template <int K, int G>
 __global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
-                                                                 const uint8_t *__restrict__ codes,
-                                                                 int64_t ldc,
-                                                                 const uint32_t *__restrict__ off,
-                                                                 const uint16_t *__restrict__ ent,
-                                                                 int64_t row0, int w0, int w1, int w2,
-                                                                 OutSpec o) {
+                                                           const uint8_t *__restrict__ codes,
+                                                           int64_t ldc,
+                                                           const uint32_t *__restrict__ off,
+                                                           const uint16_t *__restrict__ ent,
+                                                           int64_t row0, int w0, int w1, int w2,
+                                                           OutSpec o) {
   constexpr int NSUB = K + 3 * K * (K - 1) / 2;
   extern __shared__ __align__(16) uint32_t smem[];
   const int64_t il = blockIdx.x / g.nchunks;
@@ -447,7 +447,8 @@ __global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
   const int accw = ((g.chunk + 3) >> 2) << 2;
   const int P = g.pmax;
   int32_t *acc = (int32_t *)smem;
-  uint32_t *rotk = smem + accw;  // [P][K]: rot_p(u_a)
+  uint32_t *rotk = smem + accw;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
   uint4 *acc4 = (uint4 *)acc;
   for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
   const uint8_t *rs = codes + i * ldc;
@@ -456,54 +457,50 @@ __global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
     const uint32_t u = window_code(rs, a, K);
     rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
   }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
   __syncthreads();
 
   const uint32_t chunk_bins = (uint32_t)c * g.nkeys;
   const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
   const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
   const int total = P * NSUB;
-  const int per = (total + ngrp - 1) / ngrp;
-  int L = grp * per;
-  const int Lend = min(total, L + per);
-
-  int a = L / NSUB, s = L - a * NSUB;
-  int p = 0, q = -1, ci = 0;
-  auto set_sub = [&]() {
-    if (s < K) {
-      p = s; q = -1; ci = 0;
-    } else {
-      const int t = s - K, pi = t / 3;
-      ci = t - 3 * pi;
-      int pp = 1;
-      while ((pp + 1) * pp / 2 <= pi) ++pp;
-      p = pp;
-      q = pi - pp * (pp - 1) / 2;
-    }
-  };
+  // groups of a wave take consecutive sub-lists of the same k-mer (strided over the
+  // row's list space): their bins are close in memory (shared cache lines)
+  int L = grp;
+  const int Lend = total;
   // list -> base bin of its 4 letter sub-lists, u_p, weights
-  auto describe = [&](uint32_t &base, uint32_t &up, int &wa, int &wb) {
+  auto describe = [&](int Lx, uint32_t &base, uint32_t &up, int &wa, int &wb) {
+    const int a = Lx / NSUB, s = Lx - a * NSUB;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF, q = (d >> 8) & 0xFF;
     const uint32_t rk = rotk[a * K + p];
     up = rk & 3u;
     uint32_t key = rk >> 2;
-    if (q < 0) {
+    if (q == 0xFF) {
       wa = (p == 0) ? w0 : 0;
       wb = w1;
     } else {
       // letter q of u sits at key digit q (q < p); substitute the ci-th other letter
       const int sh = 2 * (K - 2 - q);
       const uint32_t lq = (key >> sh) & 3u;
-      const uint32_t nl = (lq + 1u + (uint32_t)ci) & 3u;
+      const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
       key ^= (lq ^ nl) << sh;
       wa = 0;
       wb = w2;
     }
     base = (uint32_t)p * copy_stride + chunk_bins + (key << 2);
   };
-  auto advance = [&]() {
-    if (++s == NSUB) { s = 0; ++a; }
-    set_sub();
-  };
-  set_sub();
 
   // segment bounds of the current list: [b0,b1) wb, [b1,b2) wa, [b2,b3) wb
   uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
@@ -518,16 +515,15 @@ __global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
   };
   if (L < Lend) {
     uint32_t base, up;
-    describe(base, up, wa, wb);
+    describe(L, base, up, wa, wb);
     load_bounds(base, up, b0, b1, b2, b3);
   }
-  for (; L < Lend; ++L) {
+  for (; L < Lend; L += ngrp) {
     uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
     int nwa = 0, nwb = 0;
-    if (L + 1 < Lend) {
-      advance();
+    if (L + ngrp < Lend) {
       uint32_t base, up;
-      describe(base, up, nwa, nwb);
+      describe(L + ngrp, base, up, nwa, nwb);
       load_bounds(base, up, n0, n1, n2, n3);
     }
     // virtual index t over [b0,b1) ++ ([b1,b2) if wa) ++ [b2,b3)
@@ -554,6 +550,464 @@ __global__ __launch_bounds__(1024) void gram_mm1rot_kernel(IndexGeom g,
     b0 = n0; b1 = n1; b2 = n2; b3 = n3;
     wa = nwa;
     wb = nwb;
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
+// ------------------------------------------------------------------ mismatch m=1, v4
+// Rotated layout (as v3) with a 3-stage software pipeline per lane group, lists taken
+// interleaved (groups of a wave work on consecutive sub-lists of one k-mer):
+//   iteration t: (1) decode list t+2, issue its 5 bin offsets;
+//                (2) wait for list t+1's offsets, issue up to U*G of its entries;
+//                (3) wait for list t's entries, LDS atomics.
+// Loads are unconditional (clamped address, masked weight) so hipcc can emit counted
+// vmcnt waits instead of draining; a list longer than U*G entries finishes in a slow
+// synchronous loop (rare: average list length ~ 3/4 * 4 * chunk * P / 4^k).
+template <int K, int G, int U>
+__global__ __launch_bounds__(1024) void gram_mm1p_kernel(IndexGeom g,
+                                                         const uint8_t *__restrict__ codes,
+                                                         int64_t ldc,
+                                                         const uint32_t *__restrict__ off,
+                                                         const uint16_t *__restrict__ ent,
+                                                         int64_t row0, int w0, int w1, int w2,
+                                                         OutSpec o) {
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int64_t il = blockIdx.x / g.nchunks;
+  const int64_t i = row0 + il;
+  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accw;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
+  __syncthreads();
+
+  const uint32_t chunk_bins = (uint32_t)c * g.nkeys;
+  const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = P * NSUB;
+  const uint32_t last_bin = (uint32_t)g.nbins() - 4u;  // clamp for out-of-range lists
+
+  // decode list Lx: base bin (multiple of 4) of its 4 letter sub-lists, and meta =
+  // u_p | wa << 8 | wb << 16 (weights <= 255, checked by the host)
+  auto describe = [&](int Lx, uint32_t &base, uint32_t &meta) {
+    if (Lx >= total) {
+      base = last_bin;
+      meta = 0;  // zero weights: contributes nothing
+      return;
+    }
+    const int a = Lx / NSUB, s = Lx - a * NSUB;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF, q = (d >> 8) & 0xFF;
+    const uint32_t rk = rotk[a * K + p];
+    uint32_t key = rk >> 2;
+    uint32_t wa, wb;
+    if (q == 0xFF) {
+      wa = (p == 0) ? (uint32_t)w0 : 0u;
+      wb = (uint32_t)w1;
+    } else {
+      const int sh = 2 * (K - 2 - q);  // letter q of u sits at key digit q (q < p)
+      const uint32_t lq = (key >> sh) & 3u;
+      const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
+      key ^= (lq ^ nl) << sh;
+      wa = 0u;
+      wb = (uint32_t)w2;
+    }
+    base = (uint32_t)p * copy_stride + chunk_bins + (key << 2);
+    meta = (rk & 3u) | (wa << 8) | (wb << 16);
+  };
+  // segments of a list: [x0,x1) wb, [x1,x2) wa (dropped when wa == 0), [x2,x3) wb
+  struct Seg {
+    uint32_t b0, b1, b2, lA, lB, tot;
+    int wa, wb;
+  };
+  auto segs = [&](const uint4 o4, uint32_t o5, uint32_t meta) {
+    const uint32_t up = meta & 3u;
+    Seg sg;
+    const uint32_t lo = up == 0 ? o4.x : up == 1 ? o4.y : up == 2 ? o4.z : o4.w;
+    const uint32_t hi = up == 0 ? o4.y : up == 1 ? o4.z : up == 2 ? o4.w : o5;
+    sg.wa = (int)((meta >> 8) & 0xFFu);
+    sg.wb = (int)(meta >> 16);
+    sg.b0 = o4.x;
+    sg.b1 = lo;
+    sg.b2 = hi;
+    sg.lA = lo - o4.x;
+    sg.lB = sg.wa ? (hi - lo) : 0u;
+    sg.tot = sg.lA + sg.lB + (o5 - hi);
+    return sg;
+  };
+  auto ent_index = [&](const Seg &sg, uint32_t t, uint32_t &e, int &w) {
+    if (t < sg.lA) { e = sg.b0 + t; w = sg.wb; }
+    else if (t < sg.lA + sg.lB) { e = sg.b1 + (t - sg.lA); w = sg.wa; }
+    else { e = sg.b2 + (t - sg.lA - sg.lB); w = sg.wb; }
+    if (t >= sg.tot) { e = sg.b0; w = 0; }  // clamped, masked
+  };
+
+  int L = grp;
+  // prologue: offsets of lists L and L+ngrp; entries of list L
+  uint32_t baseA, metaA, baseB, metaB;
+  describe(L, baseA, metaA);
+  uint4 oA4 = *(const uint4 *)(off + baseA);
+  uint32_t oA5 = off[baseA + 4];
+  describe(L + ngrp, baseB, metaB);
+  uint4 oB4 = *(const uint4 *)(off + baseB);
+  uint32_t oB5 = off[baseB + 4];
+  Seg cur = segs(oA4, oA5, metaA);
+  uint32_t ecur[U];
+  int wcur[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    uint32_t e;
+    int w;
+    ent_index(cur, (uint32_t)(u * G + gl), e, w);
+    wcur[u] = w;
+    ecur[u] = ent[e];
+  }
+  for (; L < total; L += ngrp) {
+    // (1) offsets of list L + 2*ngrp
+    uint32_t baseC, metaC;
+    describe(L + 2 * ngrp, baseC, metaC);
+    const uint4 oC4 = *(const uint4 *)(off + baseC);
+    const uint32_t oC5 = off[baseC + 4];
+    // (2) entries of list L + ngrp
+    const Seg nxt = segs(oB4, oB5, metaB);
+    uint32_t enxt[U];
+    int wnxt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t e;
+      int w;
+      ent_index(nxt, (uint32_t)(u * G + gl), e, w);
+      wnxt[u] = w;
+      enxt[u] = ent[e];
+    }
+    // (3) atomics of list L
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (wcur[u]) atomicAdd(&acc[ecur[u]], wcur[u]);
+    for (uint32_t t = (uint32_t)(U * G + gl); t < cur.tot; t += G) {  // rare long list
+      uint32_t e;
+      int w;
+      ent_index(cur, t, e, w);
+      if (w) atomicAdd(&acc[ent[e]], w);
+    }
+    cur = nxt;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ecur[u] = enxt[u];
+      wcur[u] = wnxt[u];
+    }
+    oB4 = oC4;
+    oB5 = oC5;
+    metaB = metaC;
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
+// ------------------------------------------------------------------ mismatch m=1, v5
+// Rotated layout, branch-free: each lane group (G lanes, G = 1 or 2 by default) owns one
+// list at a time and covers it with U unrolled entry slots per lane; every slot computes
+// its entry index and weight with selects (masked slots add 0), entry and bin-offset
+// reads are raw buffer loads (32-bit offsets, out-of-range reads return 0), and the
+// next list's offsets load while this list's entries are in flight.
+//   list (p, key): bins key*4 .. key*4+3 (letter at p); type 1 p=0 covers all 4 bins
+//   (letter u_p -> w0, others -> w1); otherwise the letter-u_p bin is skipped.
+template <int K, int G, int U>
+__global__ __launch_bounds__(1024) void gram_mm1b_kernel(IndexGeom g,
+                                                         const uint8_t *__restrict__ codes,
+                                                         int64_t ldc,
+                                                         const uint32_t *__restrict__ off,
+                                                         const uint16_t *__restrict__ ent,
+                                                         uint32_t n_ent, int64_t row0, int w0,
+                                                         int w1, int w2, OutSpec o) {
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int64_t il = blockIdx.x / g.nchunks;
+  const int64_t i = row0 + il;
+  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accw;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t roff =
+      __builtin_amdgcn_make_buffer_rsrc((void *)off, (short)0, (int)((g.nbins() + 1) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rent =
+      __builtin_amdgcn_make_buffer_rsrc((void *)ent, (short)0, (int)(n_ent * 2u), 0x00020000);
+  const uint32_t chunk_bins = (uint32_t)c * g.nkeys;
+  const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = P * NSUB;
+
+  // branch-free list decode -> base bin (multiple of 4), letter u_p, weights
+  auto describe = [&](int L, uint32_t &base, uint32_t &up, int &wa, int &wb) {
+    const bool valid = L < total;
+    const int Lc = valid ? L : total - 1;
+    const int a = Lc / NSUB, s = Lc - a * NSUB;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF;
+    const bool t1 = ((d >> 8) & 0xFF) == 0xFF;
+    const int q = t1 ? 0 : (int)((d >> 8) & 0xFF);
+    const uint32_t rk = rotk[a * K + p];
+    const uint32_t key = rk >> 2;
+    const int sh = 2 * (K - 2 - q);
+    const uint32_t lq = (key >> sh) & 3u;
+    const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
+    const uint32_t key2 = key ^ ((lq ^ nl) << sh);
+    base = (uint32_t)p * copy_stride + chunk_bins + ((t1 ? key : key2) << 2);
+    up = rk & 3u;
+    wa = (valid && t1 && p == 0) ? w0 : 0;
+    wb = valid ? (t1 ? w1 : w2) : 0;
+  };
+
+  int L = grp;
+  uint32_t base, up;
+  int wa, wb;
+  describe(L, base, up, wa, wb);
+  uint4 o4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(roff, base * 4u, 0, 0));
+  uint32_t o5 = __builtin_amdgcn_raw_buffer_load_b32(roff, base * 4u + 16u, 0, 0);
+  for (; L < total; L += ngrp) {
+    // segments of this list
+    const uint32_t lo = up == 0 ? o4.x : up == 1 ? o4.y : up == 2 ? o4.z : o4.w;
+    const uint32_t hi = up == 0 ? o4.y : up == 1 ? o4.z : up == 2 ? o4.w : o5;
+    const bool full = wa != 0;
+    const uint32_t b0 = o4.x;
+    const uint32_t lR1 = full ? (o5 - o4.x) : (lo - o4.x);
+    const uint32_t b2p = hi;
+    const uint32_t tot = full ? (o5 - o4.x) : (lo - o4.x) + (o5 - hi);
+    const uint32_t lenB = full ? (hi - lo) : 0u;
+    const int cwa = wa, cwb = wb;
+    // issue this list's entries
+    uint32_t col[U];
+    int wt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = (uint32_t)(u * G + gl);
+      const uint32_t e = t < lR1 ? b0 + t : b2p + (t - lR1);
+      col[u] = __builtin_amdgcn_raw_buffer_load_b16(rent, e * 2u, 0, 0);
+      wt[u] = t < tot ? ((e - lo) < lenB ? cwa : cwb) : 0;
+    }
+    // next list's offsets in flight with them
+    describe(L + ngrp, base, up, wa, wb);
+    o4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(roff, base * 4u, 0, 0));
+    o5 = __builtin_amdgcn_raw_buffer_load_b32(roff, base * 4u + 16u, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) atomicAdd(&acc[col[u]], wt[u]);
+    for (uint32_t t = (uint32_t)(U * G + gl); t < tot; t += G) {  // rare long list
+      const uint32_t e = t < lR1 ? b0 + t : b2p + (t - lR1);
+      const uint32_t cc = __builtin_amdgcn_raw_buffer_load_b16(rent, e * 2u, 0, 0);
+      atomicAdd(&acc[cc], (e - lo) < lenB ? cwa : cwb);
+    }
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
+// ------------------------------------------------------------------ mismatch m=1, v6
+// Rotated layout; the texture-address unit, not the VALU, bounds a 2-byte gather (one
+// wave-wide load with 64 scattered lines costs ~38 TA cycles), so every lane group (G
+// lanes) reads its list's whole 4-bin range [b0, b4) with aligned V-entry vector loads
+// (V=4: 8 B, V=8: 16 B per lane; U loads per lane), and each entry is masked by range
+// and weighted by whether it lies in the letter-u_p bin [lo, hi):
+//   type 1, p=0: u_p bin -> w0, other letters -> w1;  type 1, p>0: u_p bin -> 0, others w1;
+//   type 2: u_p bin -> 0, others -> w2.
+template <int K, int G, int V, int U>
+__global__ __launch_bounds__(1024) void gram_mm1v_kernel(IndexGeom g,
+                                                         const uint8_t *__restrict__ codes,
+                                                         int64_t ldc,
+                                                         const uint32_t *__restrict__ off,
+                                                         const uint16_t *__restrict__ ent,
+                                                         uint32_t n_ent, int64_t row0, int w0,
+                                                         int w1, int w2, OutSpec o) {
+  static_assert(V == 4 || V == 8, "vector width");
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int64_t il = blockIdx.x / g.nchunks;
+  const int64_t i = row0 + il;
+  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accw;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t roff =
+      __builtin_amdgcn_make_buffer_rsrc((void *)off, (short)0, (int)((g.nbins() + 1) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rent =
+      __builtin_amdgcn_make_buffer_rsrc((void *)ent, (short)0, (int)(n_ent * 2u), 0x00020000);
+  const uint32_t chunk_bins = (uint32_t)c * g.nkeys;
+  const uint32_t copy_stride = (uint32_t)g.nchunks * g.nkeys;
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = P * NSUB;
+
+  auto describe = [&](int L, uint32_t &base, uint32_t &up, int &wa, int &wb) {
+    const bool valid = L < total;
+    const int Lc = valid ? L : total - 1;
+    const int a = Lc / NSUB, s = Lc - a * NSUB;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF;
+    const bool t1 = ((d >> 8) & 0xFF) == 0xFF;
+    const int q = t1 ? 0 : (int)((d >> 8) & 0xFF);
+    const uint32_t rk = rotk[a * K + p];
+    const uint32_t key = rk >> 2;
+    const int sh = 2 * (K - 2 - q);
+    const uint32_t lq = (key >> sh) & 3u;
+    const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
+    const uint32_t key2 = key ^ ((lq ^ nl) << sh);
+    base = (uint32_t)p * copy_stride + chunk_bins + ((t1 ? key : key2) << 2);
+    up = rk & 3u;
+    wa = (valid && t1 && p == 0) ? w0 : 0;
+    wb = valid ? (t1 ? w1 : w2) : 0;
+  };
+
+  int L = grp;
+  uint32_t base, up;
+  int wa, wb;
+  describe(L, base, up, wa, wb);
+  uint4 o4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(roff, base * 4u, 0, 0));
+  uint32_t o5 = __builtin_amdgcn_raw_buffer_load_b32(roff, base * 4u + 16u, 0, 0);
+  for (; L < total; L += ngrp) {
+    const uint32_t lo = up == 0 ? o4.x : up == 1 ? o4.y : up == 2 ? o4.z : o4.w;
+    const uint32_t hi = up == 0 ? o4.y : up == 1 ? o4.z : up == 2 ? o4.w : o5;
+    const uint32_t b0 = o4.x, b4 = o5;
+    const uint32_t a0 = b0 & ~(uint32_t)(V - 1);  // aligned window start
+    const int cwa = wa, cwb = wb;
+    // this list's entries: U aligned vectors of V entries per lane
+    uint32_t vec[U][V / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e0 = a0 + (uint32_t)((u * G + gl) * V);
+      if constexpr (V == 8) {
+        const uint4 x = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rent, e0 * 2u, 0, 0));
+        vec[u][0] = x.x; vec[u][1] = x.y; vec[u][2] = x.z; vec[u][3] = x.w;
+      } else {
+        const uint2 x = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rent, e0 * 2u, 0, 0));
+        vec[u][0] = x.x; vec[u][1] = x.y;
+      }
+    }
+    const uint32_t span = (uint32_t)(U * G * V);
+    // next list's offsets in flight with them
+    describe(L + ngrp, base, up, wa, wb);
+    o4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(roff, base * 4u, 0, 0));
+    o5 = __builtin_amdgcn_raw_buffer_load_b32(roff, base * 4u + 16u, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e0 = a0 + (uint32_t)((u * G + gl) * V);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const uint32_t e = e0 + v;
+        const uint32_t col = (vec[u][v >> 1] >> ((v & 1) * 16)) & 0xFFFFu;
+        const int w = (e - b0 < b4 - b0) ? ((e - lo < hi - lo) ? cwa : cwb) : 0;
+        atomicAdd(&acc[col], w);
+      }
+    }
+    // rare: list longer than one window
+    for (uint32_t e = a0 + span + (uint32_t)gl; e < b4; e += G) {
+      const uint32_t cc = __builtin_amdgcn_raw_buffer_load_b16(rent, e * 2u, 0, 0);
+      atomicAdd(&acc[cc], (e - lo < hi - lo) ? cwa : cwb);
+    }
   }
   __syncthreads();
 
@@ -732,20 +1186,73 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
 }
 
 hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                     const uint32_t *off, const uint16_t *ent, int64_t row0,
-                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                     hipStream_t s) {
+                                     const uint32_t *off, const uint16_t *ent, uint32_t n_ent,
+                                     int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                     const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (g.k < 4 || g.k > 12) return hipErrorNotSupported;
-  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k) * 4;
+  const int nsub = g.k + 3 * g.k * (g.k - 1) / 2;
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k + nsub) * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
   const double avg = (double)g.chunk * g.pmax / ((double)g.nkeys / 4.0);  // per 4-bin list
   int G = 2;
   while (G < 16 && G * 4 < avg) G *= 2;
   G = env_int("KMG_MM_G", G);
   G = G < 2 ? 2 : (G > 16 ? 16 : G);
-  const int threads = env_int("KMG_MM_THREADS", 512) >= 1024 ? 1024 : 512;
+  const int threads = env_int("KMG_MM_THREADS", 1024) >= 1024 ? 1024 : 512;
+  const int variant = env_int("KMG_MM_VARIANT", 6);
+  if (variant == 6) {
+    const int G6 = env_int("KMG_MM_G", 4);
+    const int V6 = env_int("KMG_MM_V", 4);
+    const int U6 = env_int("KMG_MM_U", 2);
+    bool launched = false;
+#define KMG_MM6(KK, GG, VV, UU)                                                                    \
+  if (g.k == KK && G6 == GG && V6 == VV && U6 == UU) {                                             \
+    hipLaunchKernelGGL((gram_mm1v_kernel<KK, GG, VV, UU>), grid, dim3(threads), lds, s, g, codes,  \
+                       ldc, off, ent, n_ent, row0, w0, w1, w2, o);                                 \
+    launched = true;                                                                               \
+  }
+#define KMG_MM6K(KK)                                                                               \
+  KMG_MM6(KK, 4, 4, 2) KMG_MM6(KK, 2, 4, 4) KMG_MM6(KK, 2, 8, 2) KMG_MM6(KK, 1, 8, 4)              \
+  KMG_MM6(KK, 4, 8, 1) KMG_MM6(KK, 8, 4, 1) KMG_MM6(KK, 4, 4, 1) KMG_MM6(KK, 2, 8, 1)
+    KMG_MM6K(4) KMG_MM6K(5) KMG_MM6K(6) KMG_MM6K(7) KMG_MM6K(8) KMG_MM6K(9) KMG_MM6K(10)
+    KMG_MM6K(11) KMG_MM6K(12)
+#undef KMG_MM6K
+#undef KMG_MM6
+    return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
+  }
+  if (variant == 5) {
+    const int G5 = env_int("KMG_MM_G", 1);
+    const int U5 = env_int("KMG_MM_U", 24);
+#define KMG_MM5(KK, GG, UU)                                                                     \
+  if (g.k == KK && G5 == GG && U5 == UU)                                                        \
+    hipLaunchKernelGGL((gram_mm1b_kernel<KK, GG, UU>), grid, dim3(threads), lds, s, g, codes,   \
+                       ldc, off, ent, n_ent, row0, w0, w1, w2, o);
+#define KMG_MM5K(KK)                                                                            \
+  KMG_MM5(KK, 1, 16) KMG_MM5(KK, 1, 24) KMG_MM5(KK, 1, 32) KMG_MM5(KK, 2, 8) KMG_MM5(KK, 2, 12)   \
+  KMG_MM5(KK, 2, 16) KMG_MM5(KK, 4, 8)
+    KMG_MM5K(4) KMG_MM5K(5) KMG_MM5K(6) KMG_MM5K(7) KMG_MM5K(8) KMG_MM5K(9) KMG_MM5K(10)
+    KMG_MM5K(11) KMG_MM5K(12)
+#undef KMG_MM5K
+#undef KMG_MM5
+    return hipPeekAtLastError();
+  }
+  if (variant == 4) {
+    const int U = env_int("KMG_MM_U", 8) >= 8 ? 8 : 4;
+#define KMG_MM4(KK, GG, UU)                                                                     \
+  if (g.k == KK && G == GG && U == UU)                                                          \
+    hipLaunchKernelGGL((gram_mm1p_kernel<KK, GG, UU>), grid, dim3(threads), lds, s, g, codes,   \
+                       ldc, off, ent, row0, w0, w1, w2, o);
+#define KMG_MM4K(KK)                                                                            \
+  KMG_MM4(KK, 2, 4) KMG_MM4(KK, 4, 4) KMG_MM4(KK, 8, 4) KMG_MM4(KK, 16, 4) KMG_MM4(KK, 2, 8)    \
+  KMG_MM4(KK, 4, 8) KMG_MM4(KK, 8, 8) KMG_MM4(KK, 16, 8)
+    KMG_MM4K(4) KMG_MM4K(5) KMG_MM4K(6) KMG_MM4K(7) KMG_MM4K(8) KMG_MM4K(9) KMG_MM4K(10)
+    KMG_MM4K(11) KMG_MM4K(12)
+#undef KMG_MM4K
+#undef KMG_MM4
+    return hipGetLastError();
+  }
 #define KMG_MM3(KK, GG)                                                                         \
   if (g.k == KK && G == GG)                                                                     \
     hipLaunchKernelGGL((gram_mm1rot_kernel<KK, GG>), grid, dim3(threads), lds, s, g, codes,     \

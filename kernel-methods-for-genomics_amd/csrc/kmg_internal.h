@@ -77,9 +77,9 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 // mismatch (k,1) on the rotated layout (rot=1, nkeys = 4^k)
 hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                     const uint32_t *off, const uint16_t *ent, int64_t row0,
-                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                     hipStream_t s);
+                                     const uint32_t *off, const uint16_t *ent, uint32_t n_ent,
+                                     int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                     const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
 hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,

@@ -8,6 +8,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "kernel-methods-for-genomics_amd")
 ORACLE = os.path.join(ROOT, "oracle")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# every Gram output is pre-filled with garbage, so a kernel that silently does not run
+# cannot pass by leaving a previous (correct) result in a reused device buffer
+os.environ.setdefault("KMG_POISON", "1")
 for p in (PKG, ORACLE, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

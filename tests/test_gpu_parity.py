@@ -287,3 +287,29 @@ def test_device_sqrt_div_bits(ctx):
     ref = raw / (d[:, None] * d[None, :])
     np.fill_diagonal(ref, 1.0)
     assert np.array_equal(K, ref)
+
+
+def test_rccl_allgather_single_rank(ctx):
+    """kmg_comm_init / kmg_allgather_rows on a 1-rank communicator (the multi-GPU
+    assembly code path; >1 rank needs >1 GPU and is exercised by bench.py --allgather)."""
+    codes, lens = E.synthetic(300, 101, seed=41)
+    n, ldc = codes.shape
+    full = ctx.gram(P.make(L.KMG_SPECTRUM, k=6), codes, lens, L.KMG_I32)
+    uid = L.Context.unique_id()
+    ctx.comm_init(uid, 1, 0)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(n * n * 4)
+    try:
+        ctx.gram_device(P.make(L.KMG_SPECTRUM, k=6), d_codes, d_lens, n, ldc, 0, n, L.KMG_I32,
+                        d_out, n)
+        ctx.allgather_rows(d_out, n, n, L.KMG_I32, [0, n])
+        ctx.synchronize()
+        out = np.empty((n, n), dtype=np.int32)
+        ctx.d2h(out, d_out)
+        assert np.array_equal(out, full)
+    finally:
+        ctx.comm_destroy()
+        for p_ in (d_out, d_codes, d_lens):
+            ctx.dfree(p_)

@@ -15,6 +15,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kernel-methods-for-genomics_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import numpy as np  # noqa: E402
 
@@ -29,8 +30,8 @@ DEFAULT = {
     "mm": [{}, {"KMG_MM_G": "2"}, {"KMG_MM_G": "8"}, {"KMG_MM_CHUNK": "16384"},
            {"KMG_MM_CHUNK": "5120"}, {"KMG_MM_CHUNK": "16384", "KMG_MM_G": "8"}],
 }
-KNOBS = ("KMG_SP_NT", "KMG_SP_CHUNK", "KMG_MM_G", "KMG_MM_CHUNK", "KMG_IDX_SEQS",
-         "KMG_IDX_THREADS", "KMG_IDX_BUCKETS", "KMG_MM_VARIANT")
+KNOBS = ("KMG_SP_NT", "KMG_SP_CHUNK", "KMG_MM_G", "KMG_MM_U", "KMG_MM_V", "KMG_MM_THREADS",
+         "KMG_MM_CHUNK", "KMG_IDX_SEQS", "KMG_IDX_THREADS", "KMG_IDX_BUCKETS", "KMG_MM_VARIANT")
 
 
 def main():
@@ -54,6 +55,11 @@ def main():
     ctx.h2d(d_lens, lens)
     d_out = ctx.dmalloc(n * n * esz)
     probe_rows = [0, n // 3, n - 1]
+    import cref
+    if args.workload == "sp":
+        oracle = {r: cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0] for r in probe_rows}
+    else:
+        oracle = {r: cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0] for r in probe_rows}
     ref = None
     for st in sets:
         for kn in KNOBS:
@@ -75,18 +81,22 @@ def main():
             tot, cnt = ctx.stage_stats(s)
             if cnt:
                 stages[s] = round(tot / cnt * 1e3, 1)
-        rows = []
+        ctx.memset(d_out, 0xA5, n * n * esz)  # poison, then one checked run
+        ctx.gram_device(params, d_codes, d_lens, n, 101, 0, n, dt, d_out, n)
+        ctx.synchronize()
+        rows, ok = [], True
         for r in probe_rows:
             row = np.empty(n, dtype=L.DTYPES[dt])
             ctx.d2h(row, ctypes.c_void_p(d_out.value + r * n * esz))
             rows.append(row)
+            ok &= bool(np.array_equal(row.astype(oracle[r].dtype), oracle[r]))
         same = None
         if ref is None:
             ref = rows
         else:
             same = all(np.array_equal(a, b) for a, b in zip(rows, ref))
         print(json.dumps({"set": st, "wall_ms": round(wall, 4), "stages_us": stages,
-                          "same_as_first": same}), flush=True)
+                          "same_as_first": same, "oracle_ok": ok}), flush=True)
     ctx.close()
 
 
