@@ -1154,16 +1154,19 @@ hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64
   if (g.k >= 4 && g.k <= 12 && env_int("KMG_MM_VARIANT", 2) == 2) {
     const size_t lds2 = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * (g.k + 1)) * 4;
     const int G2 = G < 2 ? 2 : (G > 16 ? 16 : G);
+    bool launched = false;
 #define KMG_MM2(KK, GG)                                                                        \
-  if (g.k == KK && G2 == GG)                                                                   \
+  if (g.k == KK && G2 == GG) {                                                                 \
     hipLaunchKernelGGL((gram_mm1v2_kernel<KK, GG>), grid, dim3(MM_THREADS), lds2, s, g, codes, \
-                       ldc, off, ent, row0, w0, w1, w2, o);
+                       ldc, off, ent, row0, w0, w1, w2, o);                                    \
+    launched = true;                                                                           \
+  }
 #define KMG_MM2K(KK) KMG_MM2(KK, 2) KMG_MM2(KK, 4) KMG_MM2(KK, 8) KMG_MM2(KK, 16)
     KMG_MM2K(4) KMG_MM2K(5) KMG_MM2K(6) KMG_MM2K(7) KMG_MM2K(8) KMG_MM2K(9) KMG_MM2K(10)
     KMG_MM2K(11) KMG_MM2K(12)
 #undef KMG_MM2K
 #undef KMG_MM2
-    return hipGetLastError();
+    return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
   }
 #define KMG_MM_CASE(GG)                                                                    \
   case GG:                                                                                 \
@@ -1225,10 +1228,13 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
   if (variant == 5) {
     const int G5 = env_int("KMG_MM_G", 1);
     const int U5 = env_int("KMG_MM_U", 24);
+    bool launched = false;
 #define KMG_MM5(KK, GG, UU)                                                                     \
-  if (g.k == KK && G5 == GG && U5 == UU)                                                        \
+  if (g.k == KK && G5 == GG && U5 == UU) {                                                      \
     hipLaunchKernelGGL((gram_mm1b_kernel<KK, GG, UU>), grid, dim3(threads), lds, s, g, codes,   \
-                       ldc, off, ent, n_ent, row0, w0, w1, w2, o);
+                       ldc, off, ent, n_ent, row0, w0, w1, w2, o);                              \
+    launched = true;                                                                            \
+  }
 #define KMG_MM5K(KK)                                                                            \
   KMG_MM5(KK, 1, 16) KMG_MM5(KK, 1, 24) KMG_MM5(KK, 1, 32) KMG_MM5(KK, 2, 8) KMG_MM5(KK, 2, 12)   \
   KMG_MM5(KK, 2, 16) KMG_MM5(KK, 4, 8)
@@ -1236,14 +1242,17 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
     KMG_MM5K(11) KMG_MM5K(12)
 #undef KMG_MM5K
 #undef KMG_MM5
-    return hipPeekAtLastError();
+    return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
   }
   if (variant == 4) {
     const int U = env_int("KMG_MM_U", 8) >= 8 ? 8 : 4;
+    bool launched = false;
 #define KMG_MM4(KK, GG, UU)                                                                     \
-  if (g.k == KK && G == GG && U == UU)                                                          \
+  if (g.k == KK && G == GG && U == UU) {                                                        \
     hipLaunchKernelGGL((gram_mm1p_kernel<KK, GG, UU>), grid, dim3(threads), lds, s, g, codes,   \
-                       ldc, off, ent, row0, w0, w1, w2, o);
+                       ldc, off, ent, row0, w0, w1, w2, o);                                     \
+    launched = true;                                                                            \
+  }
 #define KMG_MM4K(KK)                                                                            \
   KMG_MM4(KK, 2, 4) KMG_MM4(KK, 4, 4) KMG_MM4(KK, 8, 4) KMG_MM4(KK, 16, 4) KMG_MM4(KK, 2, 8)    \
   KMG_MM4(KK, 4, 8) KMG_MM4(KK, 8, 8) KMG_MM4(KK, 16, 8)
@@ -1251,18 +1260,21 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
     KMG_MM4K(11) KMG_MM4K(12)
 #undef KMG_MM4K
 #undef KMG_MM4
-    return hipGetLastError();
+    return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
   }
+  bool launched = false;
 #define KMG_MM3(KK, GG)                                                                         \
-  if (g.k == KK && G == GG)                                                                     \
+  if (g.k == KK && G == GG) {                                                                   \
     hipLaunchKernelGGL((gram_mm1rot_kernel<KK, GG>), grid, dim3(threads), lds, s, g, codes,     \
-                       ldc, off, ent, row0, w0, w1, w2, o);
+                       ldc, off, ent, row0, w0, w1, w2, o);                                     \
+    launched = true;                                                                            \
+  }
 #define KMG_MM3K(KK) KMG_MM3(KK, 2) KMG_MM3(KK, 4) KMG_MM3(KK, 8) KMG_MM3(KK, 16)
   KMG_MM3K(4) KMG_MM3K(5) KMG_MM3K(6) KMG_MM3K(7) KMG_MM3K(8) KMG_MM3K(9) KMG_MM3K(10)
   KMG_MM3K(11) KMG_MM3K(12)
 #undef KMG_MM3K
 #undef KMG_MM3
-  return hipGetLastError();
+  return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
 }
 
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,

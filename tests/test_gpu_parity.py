@@ -149,15 +149,38 @@ def test_mismatch_params(ctx, k, m):
     assert np.array_equal(K, cref.mismatch_rows(codes, lens, k, m))
 
 
-def test_mismatch_chunked(ctx, monkeypatch):
+MM_LAUNCH_CONFIGS = [
+    # (KMG_MM_VARIANT, KMG_MM_G, KMG_MM_V, KMG_MM_U): every compiled instance family
+    ("6", "4", "4", "2"), ("6", "2", "8", "2"), ("6", "1", "8", "4"), ("6", "8", "4", "1"),
+    ("5", "1", None, "24"), ("5", "2", None, "8"), ("4", "4", None, "8"), ("3", "4", None, None),
+    ("2", "8", None, None),
+]
+
+
+@pytest.mark.parametrize("variant,g,v,u", MM_LAUNCH_CONFIGS)
+def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u):
     codes, lens = E.synthetic(900, 101, seed=11)
     ref = cref.mismatch_raw(codes, lens, 9, 1)
-    for chunk, g in (("64", "1"), ("128", "4"), ("10240", "64")):
+    monkeypatch.setenv("KMG_MM_VARIANT", variant)
+    for name, val in (("KMG_MM_G", g), ("KMG_MM_V", v), ("KMG_MM_U", u)):
+        if val is None:
+            monkeypatch.delenv(name, raising=False)
+        else:
+            monkeypatch.setenv(name, val)
+    for chunk in ("64", "128", "10240"):
         monkeypatch.setenv("KMG_MM_CHUNK", chunk)
-        monkeypatch.setenv("KMG_MM_G", g)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
                        L.KMG_I32)
-        assert np.array_equal(raw.astype(np.int64), ref), (chunk, g)
+        assert np.array_equal(raw.astype(np.int64), ref), (variant, g, v, u, chunk)
+
+
+def test_mismatch_unmatched_launch_config_fails_loudly(ctx, monkeypatch):
+    codes, lens = E.synthetic(64, 101, seed=11)
+    monkeypatch.setenv("KMG_MM_VARIANT", "6")
+    monkeypatch.setenv("KMG_MM_G", "3")
+    with pytest.raises(L.KmgError):
+        ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
+                 L.KMG_I32)
 
 
 def test_mismatch_stress_repeats(ctx):
