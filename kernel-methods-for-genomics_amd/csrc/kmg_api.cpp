@@ -80,9 +80,9 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"count", "scan", "place", "fine", "diag", "gram", "extract"};
-constexpr int kNumStages = 7;
-enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT };
+const char *kStageNames[] = {"count", "scan", "place", "fine", "diag", "gram", "extract", "features"};
+constexpr int kNumStages = 8;
+enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES };
 
 }  // namespace
 
@@ -91,6 +91,8 @@ struct kmg_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
+  DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
+  int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
   bool timing = false;
   // per-stage event pairs of every timed call since the last reset (read after a sync)
@@ -270,6 +272,75 @@ int diag_hamming(kmg_ctx *c, const IndexGeom &g, const uint8_t *d_codes, const i
   return KMG_OK;
 }
 
+// ----------------------------------------------------------------- dense formulation
+// xor masks of every k-mer within Hamming distance m of a k-mer (2-bit letters; a
+// non-zero xor of a letter is one of the 3 other letters): sum_{t<=m} C(k,t) 3^t masks.
+int64_t dense_mask_count(int k, int m) {
+  int64_t tot = 0, c = 1, p3 = 1;
+  for (int t = 0; t <= std::min(m, k); ++t) {
+    tot += c * p3;
+    c = c * (k - t) / (t + 1);
+    p3 *= 3;
+  }
+  return tot;
+}
+
+int upload_masks(kmg_ctx *c, int k, int m) {
+  if (c->masks_k == k && c->masks_m == m) return KMG_OK;
+  std::vector<uint32_t> masks;
+  masks.push_back(0);
+  // breadth-first over Hamming weight: extend every mask of weight t by one more
+  // position above its highest set position
+  std::vector<std::pair<uint32_t, int>> cur = {{0u, -1}};
+  for (int t = 1; t <= std::min(m, k); ++t) {
+    std::vector<std::pair<uint32_t, int>> nxt;
+    for (auto &e : cur)
+      for (int pos = e.second + 1; pos < k; ++pos)
+        for (uint32_t x = 1; x <= 3; ++x) {
+          const uint32_t mk = e.first | (x << (2 * pos));
+          nxt.push_back({mk, pos});
+          masks.push_back(mk);
+        }
+    cur.swap(nxt);
+  }
+  KMG_TRY(c->masks.ensure(sizeof(uint32_t) * masks.size()));
+  KMG_HIP(hipMemcpyAsync(c->masks.p, masks.data(), sizeof(uint32_t) * masks.size(),
+                         hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));  // pageable source
+  c->masks_k = k;
+  c->masks_m = m;
+  c->nmask = (int)masks.size();
+  return KMG_OK;
+}
+
+// F = int8 count / neighbour-count rows, diagonal ||F_i||^2, then K = F F^T (MFMA)
+int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
+               const int32_t *d_lens, int64_t n, int64_t ldc, int64_t row0, int64_t row1,
+               OutSpec o, bool normalize) {
+  const int dp = (int)std::max<int64_t>(128, pow4(k));
+  KMG_TRY(upload_masks(c, k, m));
+  const int64_t rows_alloc = ((n + 127) & ~127LL) + 128;
+  KMG_TRY(c->feat.ensure((size_t)rows_alloc * dp));
+  KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+  KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+  {
+    StageTimer t(c, ST_FEATURES);
+    KMG_HIP(hipMemsetAsync(c->feat.as<int8_t>() + n * (int64_t)dp, 0,
+                           (size_t)(rows_alloc - n) * dp, c->stream));
+    KMG_HIP(launch_dense_features(d_codes, d_lens, ldc, n, k, window, dp,
+                                  c->masks.as<uint32_t>(), c->nmask, c->feat.as<int8_t>(),
+                                  c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+  }
+  if (normalize) {
+    o.normalize = 1;
+    o.diagv = c->diagv.as<double>();
+    o.dsq = c->dsq.as<double>();
+  }
+  StageTimer t(c, ST_GRAM);
+  KMG_HIP(launch_gram_dense(c->feat.as<int8_t>(), dp, n, row0, row1, o, c->stream));
+  return KMG_OK;
+}
+
 // ----------------------------------------------------------------- dispatch
 int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
                 int maxlen, int64_t n, int64_t ldc, int64_t row0, int64_t row1, int32_t dt,
@@ -308,6 +379,23 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const bool use_rot = s1 && k >= 4 && env_or("KMG_MM_VARIANT", 6) >= 3;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
+      // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
+      // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
+      // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
+      const int mm_eff = mm ? std::min(p->m, k) : 0;
+      const bool dense_ok = k <= 8 && g.pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096;
+      const int algo = env_or("KMG_ALGO", 0);
+      bool dense = false;
+      if (algo == 1) {
+        if (!dense_ok)
+          return fail(KMG_EUNSUPPORTED, "dense formulation needs k <= 8 and <= 127 windows");
+        dense = true;
+      } else if (algo == 0 && dense_ok) {
+        dense = mm ? (k <= env_or("KMG_DENSE_KMAX_MM", 7)) : (k <= env_or("KMG_DENSE_KMAX_SP", 5));
+      }
+      if (dense)
+        return gram_dense(c, k, mm_eff, mm ? g.window : 0, d_codes, d_lens, n, ldc, row0, row1,
+                          o, mm && p->normalize);
       if (!use_index) {
         // all-pairs Hamming formulation (any m, k <= 16)
         if (g.pmax > 256) return fail(KMG_EUNSUPPORTED, "Hamming path needs <= 256 k-mers");
@@ -479,7 +567,7 @@ int kmg_destroy(kmg_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
-                    &c->h_lens, &c->h_out};
+                    &c->h_lens, &c->h_out, &c->feat,    &c->masks};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);

@@ -103,6 +103,13 @@ hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int 
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);
 
+// dense count-vector formulation (kmg_dense.hip): int8 F [rows >= n + 128][dp], K = F F^T
+hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t n,
+                                 int k, int window, int dp, const uint32_t *masks, int nmask,
+                                 int8_t *F, double *diagv, double *dsq, hipStream_t s);
+hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
+                             const OutSpec &o, hipStream_t s);
+
 // host-matrix helpers (normalize_K / center_K)
 hipError_t launch_normalize_dense(double *K, int64_t n, int64_t ld, hipStream_t s);
 hipError_t launch_center_dense(const double *K, int64_t ldk, double *out, int64_t ld_out,

@@ -30,7 +30,7 @@ DEFAULT = {
     "mm": [{}, {"KMG_MM_G": "2"}, {"KMG_MM_G": "8"}, {"KMG_MM_CHUNK": "16384"},
            {"KMG_MM_CHUNK": "5120"}, {"KMG_MM_CHUNK": "16384", "KMG_MM_G": "8"}],
 }
-KNOBS = ("KMG_SP_NT", "KMG_SP_CHUNK", "KMG_MM_G", "KMG_MM_U", "KMG_MM_V", "KMG_MM_THREADS",
+KNOBS = ("KMG_ALGO", "KMG_SP_NT", "KMG_SP_CHUNK", "KMG_MM_G", "KMG_MM_U", "KMG_MM_V", "KMG_MM_THREADS",
          "KMG_MM_CHUNK", "KMG_IDX_SEQS", "KMG_IDX_THREADS", "KMG_IDX_BUCKETS", "KMG_MM_VARIANT")
 
 
@@ -40,15 +40,18 @@ def main():
     ap.add_argument("--n", type=int, default=20000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--sets", type=str, default=None)
+    ap.add_argument("--k", type=int, default=None, help="k-mer length (default 8 sp / 9 mm)")
+    ap.add_argument("--m", type=int, default=1)
     args = ap.parse_args()
     sets = json.loads(args.sets) if args.sets else DEFAULT[args.workload]
     n = args.n
     codes, lens = E.synthetic(n, 101, seed=2 if args.workload == "sp" else 3)
     ctx = L.Context(0)
+    k = args.k or (8 if args.workload == "sp" else 9)
     if args.workload == "sp":
-        params, dt = P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32
+        params, dt = P.make(L.KMG_SPECTRUM, k=k), L.KMG_I32
     else:
-        params, dt = P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64
+        params, dt = P.make(L.KMG_MISMATCH, k=k, m=args.m, window=101, normalize=1), L.KMG_F64
     esz = np.dtype(L.DTYPES[dt]).itemsize
     d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
     ctx.h2d(d_codes, codes)
@@ -57,9 +60,10 @@ def main():
     probe_rows = [0, n // 3, n - 1]
     import cref
     if args.workload == "sp":
-        oracle = {r: cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0] for r in probe_rows}
+        oracle = {r: cref.spectrum(codes, lens, k, rows=(r, r + 1))[0] for r in probe_rows}
     else:
-        oracle = {r: cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0] for r in probe_rows}
+        oracle = {r: cref.mismatch_rows(codes, lens, k, args.m, rows=(r, r + 1))[0]
+                  for r in probe_rows}
     ref = None
     for st in sets:
         for kn in KNOBS:
@@ -77,7 +81,7 @@ def main():
         wall = (time.perf_counter() - t0) / args.reps * 1e3
         ctx.set_timing(False)
         stages = {}
-        for s in ("count", "scan", "place", "fine", "extract", "diag", "gram"):
+        for s in ("count", "scan", "place", "fine", "extract", "features", "diag", "gram"):
             tot, cnt = ctx.stage_stats(s)
             if cnt:
                 stages[s] = round(tot / cnt * 1e3, 1)
@@ -95,7 +99,7 @@ def main():
             ref = rows
         else:
             same = all(np.array_equal(a, b) for a, b in zip(rows, ref))
-        print(json.dumps({"set": st, "wall_ms": round(wall, 4), "stages_us": stages,
+        print(json.dumps({"k": k, "set": st, "wall_ms": round(wall, 4), "stages_us": stages,
                           "same_as_first": same, "oracle_ok": ok}), flush=True)
     ctx.close()
 
