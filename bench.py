@@ -108,7 +108,7 @@ def run_workload(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, all
     ctx.set_timing(False)
     wall = dist.max(t1 - t0)
     stages = {}
-    for st in ("count", "scan", "place", "fine", "extract", "features", "diag", "gram"):
+    for st in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram"):
         tot, cnt = ctx.stage_stats(st)
         if cnt:
             stages[st] = round(tot / cnt, 5)

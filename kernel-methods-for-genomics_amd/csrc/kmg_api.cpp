@@ -80,9 +80,10 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"count", "scan", "place", "fine", "diag", "gram", "extract", "features"};
-constexpr int kNumStages = 8;
-enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES };
+const char *kStageNames[] = {"count", "scan",    "place",    "fine", "diag",
+                             "gram",  "extract", "features", "pack"};
+constexpr int kNumStages = 9;
+enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES, ST_PACK };
 
 }  // namespace
 
@@ -92,6 +93,7 @@ struct kmg_ctx {
   std::mutex mu;
   DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
+  DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
   bool timing = false;
@@ -186,7 +188,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   const int target_buckets = env_or("KMG_IDX_BUCKETS", 384);
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
-  g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 64));
+  g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 80));
   {
     const int rowlen0 = g.window > 0 ? g.window : (int)ldc;
     const int64_t budget = 150 * 1024 - 8 * (g.nbins() >> g.fine_bits) - 4096;
@@ -376,7 +378,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const bool s1 = mm && p->m == 1 && k >= 2 && k <= 12;  // drop-one-letter index
       const bool use_index = (exact && k <= 12) || s1;
-      const bool use_rot = s1 && k >= 4 && env_or("KMG_MM_VARIANT", 6) >= 3;
+      // mismatch launch family: 7 = slot layout (k in [8,12]; v6 below that), 3..6 = rotated
+      // CSR variants, 2 = drop-one-letter CSR (see kmg_gram.hip)
+      const int mm_variant = env_or("KMG_MM_VARIANT", 7);
+      const bool use_rot = s1 && k >= 4 && mm_variant >= 3;
+      const bool use_slots = use_rot && mm_variant == 7 && k >= 8 && k <= 12;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
@@ -428,13 +434,24 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = k;
         g.rot = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, std::min(65536, env_or("KMG_MM_CHUNK", 20480)));
+        int max_chunk = std::min(65536, env_or("KMG_MM_CHUNK", 20480));
+        if (use_slots) {  // mean list (4-bin group) length <= 40: inline in one line
+          const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
+          max_chunk = (int)std::max<int64_t>(8, std::min<int64_t>(max_chunk, cap));
+        }
+        choose_chunks(g, max_chunk);
       } else {
         g.copies = k;
         g.nkeys = (uint32_t)pow4(k - 1);
         choose_chunks(g, std::min(16384, env_or("KMG_MM_CHUNK", 10240)));
       }
       KMG_TRY(build_index(c, g, d_codes, d_lens, ldc));
+      if (use_slots) {
+        KMG_TRY(c->slots.ensure((size_t)(g.nbins() >> 2) * KMG_SLOT_BYTES));
+        StageTimer t(c, ST_PACK);
+        KMG_HIP(launch_slot_pack(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                 c->slots.as<uint4>(), c->stream));
+      }
       if (p->normalize) {
         KMG_TRY(upload_wtab(c, w));
         KMG_TRY(diag_hamming(c, g, d_codes, d_lens, ldc));
@@ -447,7 +464,12 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_HIP(launch_gram_spectrum(g, d_codes, d_lens, ldc, c->off.as<uint32_t>(),
                                      c->ent.as<uint16_t>(), row0, row1, o, c->stream));
       } else {
-        if (use_rot)
+        if (use_slots)
+          KMG_HIP(launch_gram_mismatch1_slots(g, d_codes, ldc, c->slots.as<uint4>(),
+                                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), row0,
+                                              row1, (int)w[0], (int)w[1], (int)w[2], o,
+                                              c->stream));
+        else if (use_rot)
           KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
                                             c->ent.as<uint16_t>(),
                                             (uint32_t)(c->ent.bytes / sizeof(uint16_t)), row0,
@@ -567,7 +589,7 @@ int kmg_destroy(kmg_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
-                    &c->h_lens, &c->h_out, &c->feat,    &c->masks};
+                    &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);

@@ -66,8 +66,15 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
     if constexpr (DT == KMG_F64) {
       double *p = (double *)o.out + il * o.ld + col;
       if (cnt == 4 && ((uintptr_t)p & 15) == 0) {
-        *(double2 *)p = make_double2(r[0], r[1]);
-        *(double2 *)(p + 2) = make_double2(r[2], r[3]);
+        if constexpr (NT) {
+          typedef double v2d __attribute__((ext_vector_type(2)));
+          const v2d a = {r[0], r[1]}, b = {r[2], r[3]};
+          __builtin_nontemporal_store(a, (v2d *)p);
+          __builtin_nontemporal_store(b, (v2d *)(p + 2));
+        } else {
+          *(double2 *)p = make_double2(r[0], r[1]);
+          *(double2 *)(p + 2) = make_double2(r[2], r[3]);
+        }
       } else {
         for (int q = 0; q < cnt; ++q) p[q] = r[q];
       }
@@ -1023,6 +1030,166 @@ __global__ __launch_bounds__(1024) void gram_mm1v_kernel(IndexGeom g,
   }
 }
 
+// ------------------------------------------------------------------ mismatch m=1, v7
+// Slot layout (kmg_index.hip slot_pack_kernel): every 4-bin group (p, chunk, key) of the
+// rotated index is also stored as ONE 128-byte line: uint16 e1, e2, e3, tot (ends of the
+// letter-0/1/2 bins relative to the group start, and the group total; tot = 0xFFFF: the
+// group is too large for 16-bit counts and lives in the CSR only) followed by the first
+// KMG_SLOT_INLINE entries.  v6 pays an offsets line plus one or two entry lines per list
+// and is bound by those L2-miss lines (Infinity-Cache traffic); here a list is one line.
+// Entries past the inline ones come from the CSR (off/ent) in a slow path (rare at the
+// chunk the host picks: mean group size <= 40).
+//   G lanes per list, each loads 128/G bytes (CH = 8/G uint4); D lists in flight per
+//   lane group (a ring unrolled at compile time); the grid is chunk-major so only one
+//   chunk's slot table is live at a time (config 5: N = 200000 is 10 chunks).
+template <int K, int G, int D>
+__global__ __launch_bounds__(1024) void gram_mm1s_kernel(IndexGeom g,
+                                                         const uint8_t *__restrict__ codes,
+                                                         int64_t ldc,
+                                                         const uint4 *__restrict__ slots,
+                                                         const uint32_t *__restrict__ off,
+                                                         const uint16_t *__restrict__ ent,
+                                                         int64_t row0, int64_t rows, int w0,
+                                                         int w1, int w2, OutSpec o) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per list");
+  constexpr int CH = 8 / G;
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int c = (int)(blockIdx.x / rows);
+  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  const int64_t i = row0 + il;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accw;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
+  __syncthreads();
+
+  const uint32_t chunk_groups = (uint32_t)c * (g.nkeys >> 2);
+  const uint32_t copy_groups = (uint32_t)g.nchunks * (g.nkeys >> 2);
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int lane = threadIdx.x & 63;
+  const int total = P * NSUB;
+
+  // list -> group index and meta = u_p | wa << 8 | wb << 16 (weights <= 255, host check)
+  auto describe = [&](int L, uint32_t &gidx, uint32_t &meta) {
+    const bool valid = L < total;
+    const int Lc = valid ? L : total - 1;
+    const int a = Lc / NSUB, s = Lc - a * NSUB;
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF;
+    const bool t1 = ((d >> 8) & 0xFF) == 0xFF;
+    const int q = t1 ? 0 : (int)((d >> 8) & 0xFF);
+    const uint32_t rk = rotk[a * K + p];
+    const uint32_t key = rk >> 2;
+    const int sh = 2 * (K - 2 - q);  // letter q of u sits at key digit q (q < p)
+    const uint32_t lq = (key >> sh) & 3u;
+    const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
+    const uint32_t key2 = key ^ ((lq ^ nl) << sh);
+    gidx = (uint32_t)p * copy_groups + chunk_groups + (t1 ? key : key2);
+    const uint32_t wa = (valid && t1 && p == 0) ? (uint32_t)w0 : 0u;
+    const uint32_t wb = valid ? (uint32_t)(t1 ? w1 : w2) : 0u;
+    meta = (rk & 3u) | (wa << 8) | (wb << 16);
+  };
+  auto load = [&](uint32_t gidx, uint4(&b)[CH]) {
+    const uint4 *sp = slots + (size_t)gidx * 8 + gl * CH;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) b[j] = sp[j];
+  };
+  // slow path: entries [t0, tot) of group gidx from the CSR, letter bins from off[]
+  auto csr_tail = [&](uint32_t gidx, uint32_t t0, uint32_t meta) {
+    const uint32_t *ob = off + (size_t)gidx * 4;
+    const uint32_t o0 = ob[0], o4 = ob[4];
+    const uint32_t up = meta & 3u;
+    const uint32_t lo = ob[up], hi = ob[up + 1];
+    const int wa = (int)((meta >> 8) & 0xFFu), wb = (int)(meta >> 16);
+    for (uint32_t e = o0 + t0 + (uint32_t)gl; e < o4; e += G) {
+      const int w = (e - lo < hi - lo) ? wa : wb;
+      if (w) atomicAdd(&acc[ent[e]], w);
+    }
+  };
+  auto process = [&](const uint4(&b)[CH], uint32_t gidx, uint32_t meta) {
+    // group header = the line's first 8 bytes (lane gl == 0, chunk 0)
+    uint32_t h0 = b[0].x, h1 = b[0].y;
+    if constexpr (G > 1) {
+      const int src = lane & ~(G - 1);
+      h0 = (uint32_t)__shfl((int)h0, src, 64);
+      h1 = (uint32_t)__shfl((int)h1, src, 64);
+    }
+    const uint32_t e1 = h0 & 0xFFFFu, e2 = h0 >> 16, e3 = h1 & 0xFFFFu, tot = h1 >> 16;
+    const uint32_t up = meta & 3u;
+    const int wa = (int)((meta >> 8) & 0xFFu), wb = (int)(meta >> 16);
+    const uint32_t lo = up == 0 ? 0u : up == 1 ? e1 : up == 2 ? e2 : e3;
+    const uint32_t hi = up == 0 ? e1 : up == 1 ? e2 : up == 2 ? e3 : tot;
+    const bool big = tot == 0xFFFFu;
+    const uint32_t lim = big ? 0u : min(tot, (uint32_t)KMG_SLOT_INLINE);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const uint32_t wd[4] = {b[j].x, b[j].y, b[j].z, b[j].w};
+      const int tb = (gl * CH + j) * 8 - 4;  // entry index of the chunk's first halfword
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const int t = tb + v;  // t < 0: header halfwords
+        const uint32_t col = (wd[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu;
+        const int w = (t >= 0 && (uint32_t)t < lim) ? (((uint32_t)t - lo < hi - lo) ? wa : wb) : 0;
+        if (w) atomicAdd(&acc[col], w);
+      }
+    }
+    if (big || tot > (uint32_t)KMG_SLOT_INLINE)
+      csr_tail(gidx, big ? 0u : (uint32_t)KMG_SLOT_INLINE, meta);
+  };
+
+  uint4 buf[D][CH];
+  uint32_t gid[D], met[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    describe(grp + r * ngrp, gid[r], met[r]);
+    load(gid[r], buf[r]);
+  }
+  for (int L = grp; L < total; L += D * ngrp) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      if (L + r * ngrp < total) process(buf[r], gid[r], met[r]);
+      describe(L + (r + D) * ngrp, gid[r], met[r]);
+      load(gid[r], buf[r]);
+    }
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
 // ------------------------------------------------------------------ Hamming forms
 __device__ __forceinline__ int ham2bit(uint32_t a, uint32_t b, uint32_t mask55) {
   const uint32_t x = a ^ b;
@@ -1204,7 +1371,8 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
   G = env_int("KMG_MM_G", G);
   G = G < 2 ? 2 : (G > 16 ? 16 : G);
   const int threads = env_int("KMG_MM_THREADS", 1024) >= 1024 ? 1024 : 512;
-  const int variant = env_int("KMG_MM_VARIANT", 6);
+  int variant = env_int("KMG_MM_VARIANT", 6);
+  if (variant == 7) variant = 6;  // slot layout is k >= 8 only: v6 below that
   if (variant == 6) {
     const int G6 = env_int("KMG_MM_G", 4);
     const int V6 = env_int("KMG_MM_V", 4);
@@ -1274,6 +1442,37 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
   KMG_MM3K(11) KMG_MM3K(12)
 #undef KMG_MM3K
 #undef KMG_MM3
+  return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
+}
+
+hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                       const uint4 *slots, const uint32_t *off,
+                                       const uint16_t *ent, int64_t row0, int64_t row1, int w0,
+                                       int w1, int w2, const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || g.n == 0) return hipSuccess;
+  if (g.k < 8 || g.k > 12 || !g.rot) return hipErrorNotSupported;
+  if (w0 > 255 || w1 > 255 || w2 > 255) return hipErrorNotSupported;
+  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  const int nsub = g.k + 3 * g.k * (g.k - 1) / 2;
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k + nsub) * 4;
+  const dim3 grid((unsigned)(rows * g.nchunks));
+  const int threads = env_int("KMG_MM_THREADS", 1024) >= 1024 ? 1024 : 512;
+  const int G7 = env_int("KMG_MM_G", 2);
+  const int D7 = env_int("KMG_MM_D", 2);
+  bool launched = false;
+#define KMG_MM7(KK, GG, DD)                                                                      \
+  if (g.k == KK && G7 == GG && D7 == DD) {                                                       \
+    hipLaunchKernelGGL((gram_mm1s_kernel<KK, GG, DD>), grid, dim3(threads), lds, s, g, codes,    \
+                       ldc, slots, off, ent, row0, rows, w0, w1, w2, o);                         \
+    launched = true;                                                                             \
+  }
+#define KMG_MM7K(KK)                                                                             \
+  KMG_MM7(KK, 2, 2) KMG_MM7(KK, 2, 3) KMG_MM7(KK, 2, 4) KMG_MM7(KK, 1, 2) KMG_MM7(KK, 1, 3)      \
+  KMG_MM7(KK, 4, 2) KMG_MM7(KK, 8, 2) KMG_MM7(KK, 4, 3)
+  KMG_MM7K(8) KMG_MM7K(9) KMG_MM7K(10) KMG_MM7K(11) KMG_MM7K(12)
+#undef KMG_MM7K
+#undef KMG_MM7
   return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
 }
 

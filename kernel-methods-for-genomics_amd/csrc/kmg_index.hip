@@ -221,6 +221,52 @@ __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, 
   }
 }
 
+// Slot layout of the rotated mismatch index (read by gram_mm1s_kernel): one 128-byte line
+// per 4-bin group (copy p, chunk, key): halfwords 0..3 = e1, e2, e3, tot (letter-bin ends
+// relative to the group start, group total), halfwords 4.. = the group's first
+// KMG_SLOT_INLINE entries in CSR order.  A group of >= 0xFFFF entries gets tot = 0xFFFF
+// and no inline entries (the kernel then reads it from the CSR).  8 threads per group,
+// each writes 16 bytes of the line.
+__global__ __launch_bounds__(256) void slot_pack_kernel(int64_t ngroups, const uint32_t *__restrict__ off,
+                                                        const uint16_t *__restrict__ ent,
+                                                        uint4 *__restrict__ slots) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gi = t >> 3;
+  const int q = (int)(t & 7);
+  if (gi >= ngroups) return;
+  const uint32_t *ob = off + gi * 4;
+  const uint32_t o0 = ob[0], o4 = ob[4];
+  const uint32_t tot = o4 - o0;
+  const bool big = tot >= 0xFFFFu;
+  uint32_t hw[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int h = q * 8 + s;
+    uint32_t v = 0;
+    if (h < 4) {
+      v = big ? (h == 3 ? 0xFFFFu : 0u) : (h == 3 ? tot : ob[h + 1] - o0);
+    } else {
+      const uint32_t e = (uint32_t)(h - 4);
+      if (!big && e < tot) v = ent[o0 + e];
+    }
+    hw[s] = v;
+  }
+  slots[t] = make_uint4(hw[0] | (hw[1] << 16), hw[2] | (hw[3] << 16), hw[4] | (hw[5] << 16),
+                        hw[6] | (hw[7] << 16));
+}
+
+hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint16_t *ent,
+                            uint4 *slots, hipStream_t s) {
+  static_assert(KMG_SLOT_BYTES == 128 && KMG_SLOT_INLINE == 60, "slot layout");
+  if (!g.rot) return hipErrorInvalidValue;
+  const int64_t ngroups = g.nbins() >> 2;
+  if (ngroups == 0) return hipSuccess;
+  const int64_t threads = ngroups * 8;
+  hipLaunchKernelGGL(slot_pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     ngroups, off, ent, slots);
+  return hipGetLastError();
+}
+
 // plain k-mer extraction (Hamming formulation and the diagonal kernels)
 __global__ __launch_bounds__(256) void extract_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
                                                       const int32_t *__restrict__ lens, int64_t ldc,

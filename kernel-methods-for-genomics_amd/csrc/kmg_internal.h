@@ -10,6 +10,9 @@
 #define KMG_INVALID 0xFFFFFFFFu
 #define KMG_ENTRY_LETTER_SHIFT 30
 #define KMG_ENTRY_SEQ_MASK 0x3FFFFFFFu
+// slot layout of the rotated mismatch index: 128-byte line = 8-byte header + 60 entries
+#define KMG_SLOT_BYTES 128
+#define KMG_SLOT_INLINE 60
 
 namespace kmg {
 
@@ -56,6 +59,9 @@ hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uin
                              hipStream_t s);
 hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
                           int64_t ldc, uint32_t *kmers, hipStream_t s);
+// rotated mismatch index (rot = 1): one KMG_SLOT_BYTES line per 4-bin group
+hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint16_t *ent,
+                            uint4 *slots, hipStream_t s);
 
 // ---------------------------------------------------------------- Gram kernels
 struct OutSpec {
@@ -80,6 +86,11 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
                                      const uint32_t *off, const uint16_t *ent, uint32_t n_ent,
                                      int64_t row0, int64_t row1, int w0, int w1, int w2,
                                      const OutSpec &o, hipStream_t s);
+// mismatch (k,1), 8 <= k <= 12, on the slot layout (one line per list)
+hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
+                                       const uint4 *slots, const uint32_t *off,
+                                       const uint16_t *ent, int64_t row0, int64_t row1, int w0,
+                                       int w1, int w2, const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
 hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,

@@ -150,19 +150,22 @@ def test_mismatch_params(ctx, k, m):
 
 
 MM_LAUNCH_CONFIGS = [
-    # (KMG_MM_VARIANT, KMG_MM_G, KMG_MM_V, KMG_MM_U): every compiled instance family
-    ("6", "4", "4", "2"), ("6", "2", "8", "2"), ("6", "1", "8", "4"), ("6", "8", "4", "1"),
-    ("5", "1", None, "24"), ("5", "2", None, "8"), ("4", "4", None, "8"), ("3", "4", None, None),
-    ("2", "8", None, None),
+    # (KMG_MM_VARIANT, KMG_MM_G, KMG_MM_V, KMG_MM_U, KMG_MM_D): every compiled instance family
+    ("7", "2", None, None, "2"), ("7", "2", None, None, "3"), ("7", "2", None, None, "4"),
+    ("7", "1", None, None, "2"), ("7", "1", None, None, "3"), ("7", "4", None, None, "2"),
+    ("7", "8", None, None, "2"), ("7", "4", None, None, "3"),
+    ("6", "4", "4", "2", None), ("6", "2", "8", "2", None), ("6", "1", "8", "4", None),
+    ("6", "8", "4", "1", None), ("5", "1", None, "24", None), ("5", "2", None, "8", None),
+    ("4", "4", None, "8", None), ("3", "4", None, None, None), ("2", "8", None, None, None),
 ]
 
 
-@pytest.mark.parametrize("variant,g,v,u", MM_LAUNCH_CONFIGS)
-def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u):
+@pytest.mark.parametrize("variant,g,v,u,d", MM_LAUNCH_CONFIGS)
+def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u, d):
     codes, lens = E.synthetic(900, 101, seed=11)
     ref = cref.mismatch_raw(codes, lens, 9, 1)
     monkeypatch.setenv("KMG_MM_VARIANT", variant)
-    for name, val in (("KMG_MM_G", g), ("KMG_MM_V", v), ("KMG_MM_U", u)):
+    for name, val in (("KMG_MM_G", g), ("KMG_MM_V", v), ("KMG_MM_U", u), ("KMG_MM_D", d)):
         if val is None:
             monkeypatch.delenv(name, raising=False)
         else:
@@ -171,7 +174,35 @@ def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u):
         monkeypatch.setenv("KMG_MM_CHUNK", chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
                        L.KMG_I32)
-        assert np.array_equal(raw.astype(np.int64), ref), (variant, g, v, u, chunk)
+        assert np.array_equal(raw.astype(np.int64), ref), (variant, g, v, u, d, chunk)
+
+
+@pytest.mark.parametrize("k", [8, 10, 11, 12])
+def test_mismatch_slots_k_range(ctx, monkeypatch, k):
+    """Slot layout (v7, the default for 8 <= k <= 12) at every compiled k."""
+    monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
+    codes, lens = E.synthetic(400, 101, seed=50 + k)
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                   L.KMG_I32)
+    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1))
+
+
+def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch):
+    """Slot groups longer than the 60 inline entries (CSR tail) and groups of >= 65535
+    entries (16-bit header overflow, CSR only): 720 poly-A rows put 720 * 93 = 66960
+    occurrences in the AAAAAAAAA groups of every copy."""
+    monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
+    monkeypatch.setenv("KMG_MM_CHUNK", "20480")
+    codes, lens = E.synthetic(760, 101, seed=61)
+    codes[:720] = 0
+    codes[700] = np.tile([0, 1], 51)[:101]
+    codes[701, 50] = 2  # poly-A with one substitution: Hamming-1/2 neighbours of the big group
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
+                   L.KMG_I32)
+    ref = cref.mismatch_raw(codes, lens, 9, 1, rows=(690, 760))
+    assert np.array_equal(raw[690:760].astype(np.int64), ref)
+    assert np.array_equal(raw[:5].astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1, rows=(0, 5)))
+    assert np.array_equal(raw, raw.T)
 
 
 def test_mismatch_unmatched_launch_config_fails_loudly(ctx, monkeypatch):
