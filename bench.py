@@ -231,7 +231,7 @@ def main():
     traffic = load_traffic("spectrum_k8")
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "kmg::gram_sp_kernel<true,1,true>", "kernel_ms": sp["gram_kernel_ms"],
+            "kernel": "kmg::gram_sp_kernel<true,1,true,1>", "kernel_ms": sp["gram_kernel_ms"],
             "alg_bytes_per_launch": alg_bytes}
 
     line = {

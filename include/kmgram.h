@@ -118,6 +118,33 @@ int kmg_normalize(kmg_ctx *ctx, double *K, int64_t n, int64_t ld, int32_t *skipp
 /* center_K (kernels.py:387-395): out = (I - 11^T/n) K (I - 11^T/n), float64 host buffers. */
 int kmg_center(kmg_ctx *ctx, const double *K, int64_t ldk, double *out, int64_t ld_out, int64_t n);
 
+/*
+ * Kernel-combination consumers of the Gram matrices (the callers of the Gram path in
+ * run.py / main.py).  K is an array of p pointers to n x n float64 matrices (row stride
+ * ld), p <= 12.  The plain functions take host buffers (copied in, result copied out);
+ * the _device functions take device pointers for everything (K, u, alpha, y and the
+ * outputs), e.g. Grams produced by kmg_gram_device, and return without synchronising.
+ */
+/* NLCK.svm_step / NLCK.get_K (NLCKernels.py:52, 97): out = (sum_m u[m] K_m) ** degree */
+int kmg_combine(kmg_ctx *ctx, const double *const *K, int32_t p, const double *u, int32_t degree,
+                int64_t n, int64_t ld, double *out, int64_t ld_out);
+int kmg_combine_device(kmg_ctx *ctx, const double *const *d_K, int32_t p, const double *d_u,
+                       int32_t degree, int64_t n, int64_t ld, double *d_out, int64_t ld_out);
+/* NLCK.grad (NLCKernels.py:61-66): grad[m] = -degree * alpha^T (K_t o K_m) alpha,
+ * K_t = (sum_m u[m] K_m) ** (degree - 1) */
+int kmg_nlck_grad(kmg_ctx *ctx, const double *const *K, int32_t p, const double *u,
+                  int32_t degree, const double *alpha, int64_t n, int64_t ld, double *grad);
+int kmg_nlck_grad_device(kmg_ctx *ctx, const double *const *d_K, int32_t p, const double *d_u,
+                         int32_t degree, const double *d_alpha, int64_t n, int64_t ld,
+                         double *d_grad);
+/* ALIGNF.get_a / ALIGNF.get_M (ALIGNF.py:43-58) on Kc_m = center_K(K_m) (kernels.py:387-395):
+ * a[m] = sum(Kc_m * outer(y, y)), M[l][m] = sum(Kc_l * Kc_m) (p x p, symmetric) */
+int kmg_alignf(kmg_ctx *ctx, const double *const *K, int32_t p, const double *y, int64_t n,
+               int64_t ld, double *a, double *M);
+/* device form: out = a[0..p) followed by the upper triangle of M row by row (l <= m) */
+int kmg_alignf_device(kmg_ctx *ctx, const double *const *d_K, int32_t p, const double *d_y,
+                      int64_t n, int64_t ld, double *d_out);
+
 /* device memory / stream helpers for device-resident callers */
 int kmg_dmalloc(kmg_ctx *ctx, void **ptr, size_t bytes);
 int kmg_dfree(kmg_ctx *ctx, void *ptr);

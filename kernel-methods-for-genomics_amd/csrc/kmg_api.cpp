@@ -80,10 +80,13 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"count", "scan",    "place",    "fine", "diag",
-                             "gram",  "extract", "features", "pack"};
-constexpr int kNumStages = 9;
-enum { ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES, ST_PACK };
+const char *kStageNames[] = {"count",   "scan",     "place", "fine",   "diag",
+                             "gram",    "extract",  "features", "pack", "combine"};
+constexpr int kNumStages = 10;
+enum {
+  ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES, ST_PACK,
+  ST_COMBINE
+};
 
 }  // namespace
 
@@ -92,8 +95,10 @@ struct kmg_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
+  DevBuf hcnt, hstart;            // index build v2: per-(bucket, block) counts / local starts
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
+  DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
   bool timing = false;
@@ -184,8 +189,10 @@ int env_or(const char *name, int dflt) {
 // ----------------------------------------------------------------- posting index
 int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
                 int64_t ldc) {
-  // ~256-512 coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins
-  const int target_buckets = env_or("KMG_IDX_BUCKETS", 384);
+  // coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins: ~384 for the
+  // spectrum index, ~1024 for the k-copy mismatch index (16.7M occurrences at N=20000,
+  // where 288 buckets left the fine pass at 240 us and 576 halved it)
+  const int target_buckets = env_or("KMG_IDX_BUCKETS", g.copies > 1 ? 1024 : 384);
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
   g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 80));
@@ -203,6 +210,29 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   const int64_t items = g.n * g.pmax * g.copies;
   if ((double)items >= 4294967295.0)
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
+  const int64_t nblk = (g.n + g.seqs_per_block - 1) / g.seqs_per_block;
+  const int64_t cap = (int64_t)g.seqs_per_block * g.pmax * g.copies;
+  if (env_or("KMG_IDX_V2", 1) && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
+      nblk * cap < ((int64_t)1 << 34)) {
+    KMG_TRY(c->hcnt.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
+    KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
+    KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(nblk * cap)));
+    KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
+    KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 64)));  // + pad: clamped reads
+    {
+      StageTimer t(c, ST_PLACE);
+      KMG_HIP(launch_index_local(g, d_codes, d_lens, ldc, (int)nblk, (uint32_t)cap,
+                                 c->hcnt.as<uint32_t>(), c->hstart.as<uint32_t>(),
+                                 c->tmp.as<uint32_t>(), c->stream));
+    }
+    {
+      StageTimer t(c, ST_FINE);
+      KMG_HIP(launch_index_gather(g, (int)nblk, (uint32_t)cap, c->hcnt.as<uint32_t>(),
+                                  c->hstart.as<uint32_t>(), c->tmp.as<uint32_t>(),
+                                  c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
+    }
+    return KMG_OK;
+  }
   const bool realloc = c->bcount.bytes < sizeof(uint32_t) * (size_t)nbk ||
                        c->bcursor.bytes < sizeof(uint32_t) * (size_t)nbk;
   KMG_TRY(c->bcount.ensure(sizeof(uint32_t) * (size_t)nbk));
@@ -265,11 +295,14 @@ int upload_wtab(kmg_ctx *c, const int64_t *w) {
 
 int diag_hamming(kmg_ctx *c, const IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
                  int64_t ldc) {
+  int max_dist = 0;  // weights are zero past this Hamming distance
+  for (int d = 0; d <= 32; ++d)
+    if (c->wtab_host[d] != 0) max_dist = d;
   KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
   KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
   if (g.pmax > 4096) return fail(KMG_EUNSUPPORTED, "more than 4096 k-mers per sequence");
   StageTimer t(c, ST_DIAG);
-  KMG_HIP(launch_diag_hamming(g, d_codes, d_lens, ldc, c->wtab.as<int64_t>(),
+  KMG_HIP(launch_diag_hamming(g, d_codes, d_lens, ldc, c->wtab.as<int64_t>(), max_dist,
                               c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
   return KMG_OK;
 }
@@ -589,7 +622,9 @@ int kmg_destroy(kmg_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
-                    &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots};
+                    &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots,
+                    &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
+                    &c->cmb_out, &c->cmb_tmp};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -786,6 +821,169 @@ int kmg_stage_stats(kmg_ctx *c, const char *stage, double *total_ms, int32_t *co
   const int idx = stage_index(stage);
   if (idx < 0) return fail(KMG_EINVAL, "unknown stage '%s'", stage);
   return stage_sum(c, idx, 0, total_ms, count);
+}
+
+// ------------------------------------------------------------------ combination consumers
+static int check_combine(kmg_ctx *c, const void *K, int32_t p, int64_t n, int64_t ld) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  if (!K) return fail(KMG_EINVAL, "K is NULL");
+  if (p < 1 || p > KMG_COMBINE_PMAX) return fail(KMG_EUNSUPPORTED, "p=%d outside [1,%d]", p, KMG_COMBINE_PMAX);
+  if (n < 0 || (n > 0 && ld < n)) return fail(KMG_EINVAL, "bad matrix shape");
+  return KMG_OK;
+}
+
+// device array of the p matrix pointers
+static int upload_ptrs(kmg_ctx *c, const double *const *ptrs, int32_t p) {
+  KMG_TRY(c->cmb_ptrs.ensure(sizeof(double *) * (size_t)p));
+  KMG_HIP(hipMemcpyAsync(c->cmb_ptrs.p, ptrs, sizeof(double *) * (size_t)p, hipMemcpyHostToDevice,
+                         c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));  // pageable source
+  return KMG_OK;
+}
+
+// host matrices -> one device slab [p][n][n]; returns the device pointer array
+static int stage_host_kernels(kmg_ctx *c, const double *const *K, int32_t p, int64_t n, int64_t ld,
+                              std::vector<const double *> &dptrs) {
+  const size_t mat = sizeof(double) * (size_t)n * (size_t)n;
+  KMG_TRY(c->cmb_k.ensure(mat * (size_t)p));
+  dptrs.resize(p);
+  for (int m = 0; m < p; ++m) {
+    if (!K[m]) return fail(KMG_EINVAL, "K[%d] is NULL", m);
+    double *dst = c->cmb_k.as<double>() + (size_t)m * n * n;
+    KMG_HIP(hipMemcpy2DAsync(dst, n * 8, K[m], ld * 8, n * 8, n, hipMemcpyHostToDevice, c->stream));
+    dptrs[m] = dst;
+  }
+  return upload_ptrs(c, dptrs.data(), p);
+}
+
+int kmg_combine_device(kmg_ctx *c, const double *const *d_K, int32_t p, const double *d_u,
+                       int32_t degree, int64_t n, int64_t ld, double *d_out, int64_t ld_out) {
+  KMG_TRY(check_combine(c, d_K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (degree < 0) return fail(KMG_EINVAL, "degree < 0");
+  if (n > 0 && ld_out < n) return fail(KMG_EINVAL, "ld_out < n");
+  KMG_HIP(hipSetDevice(c->device));
+  KMG_TRY(upload_ptrs(c, d_K, p));
+  StageTimer t(c, ST_COMBINE);
+  KMG_HIP(launch_combine(c->cmb_ptrs.as<const double *>(), d_u, p, degree, n, ld, d_out, ld_out,
+                         c->stream));
+  return KMG_OK;
+}
+
+int kmg_combine(kmg_ctx *c, const double *const *K, int32_t p, const double *u, int32_t degree,
+                int64_t n, int64_t ld, double *out, int64_t ld_out) {
+  KMG_TRY(check_combine(c, K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (degree < 0) return fail(KMG_EINVAL, "degree < 0");
+  if (!u || !out || (n > 0 && ld_out < n)) return fail(KMG_EINVAL, "bad u / out");
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  std::vector<const double *> dptrs;
+  KMG_TRY(stage_host_kernels(c, K, p, n, ld, dptrs));
+  KMG_TRY(c->cmb_vec.ensure(sizeof(double) * (size_t)p));
+  KMG_TRY(c->cmb_out.ensure(sizeof(double) * (size_t)n * n));
+  KMG_HIP(hipMemcpyAsync(c->cmb_vec.p, u, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+  {
+    StageTimer t(c, ST_COMBINE);
+    KMG_HIP(launch_combine(c->cmb_ptrs.as<const double *>(), c->cmb_vec.as<double>(), p, degree,
+                           n, n, c->cmb_out.as<double>(), n, c->stream));
+  }
+  KMG_HIP(hipMemcpy2DAsync(out, ld_out * 8, c->cmb_out.p, n * 8, n * 8, n, hipMemcpyDeviceToHost,
+                           c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_nlck_grad_device(kmg_ctx *c, const double *const *d_K, int32_t p, const double *d_u,
+                         int32_t degree, const double *d_alpha, int64_t n, int64_t ld,
+                         double *d_grad) {
+  KMG_TRY(check_combine(c, d_K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (degree < 1) return fail(KMG_EINVAL, "degree < 1");
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  KMG_TRY(upload_ptrs(c, d_K, p));
+  KMG_TRY(c->cmb_tmp.ensure(sizeof(double) * (size_t)n * p));
+  StageTimer t(c, ST_COMBINE);
+  KMG_HIP(launch_nlck_grad(c->cmb_ptrs.as<const double *>(), d_u, p, degree, d_alpha, n, ld,
+                           c->cmb_tmp.as<double>(), d_grad, c->stream));
+  return KMG_OK;
+}
+
+int kmg_nlck_grad(kmg_ctx *c, const double *const *K, int32_t p, const double *u,
+                  int32_t degree, const double *alpha, int64_t n, int64_t ld, double *grad) {
+  KMG_TRY(check_combine(c, K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (degree < 1) return fail(KMG_EINVAL, "degree < 1");
+  if (!u || !alpha || !grad) return fail(KMG_EINVAL, "NULL buffer");
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) {
+    for (int m = 0; m < p; ++m) grad[m] = -0.0 * degree;
+    return KMG_OK;
+  }
+  std::vector<const double *> dptrs;
+  KMG_TRY(stage_host_kernels(c, K, p, n, ld, dptrs));
+  KMG_TRY(c->cmb_vec.ensure(sizeof(double) * (size_t)(2 * p + n)));
+  double *du = c->cmb_vec.as<double>(), *dg = du + p, *da = dg + p;
+  KMG_HIP(hipMemcpyAsync(du, u, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipMemcpyAsync(da, alpha, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  KMG_TRY(c->cmb_tmp.ensure(sizeof(double) * (size_t)n * p));
+  {
+    StageTimer t(c, ST_COMBINE);
+    KMG_HIP(launch_nlck_grad(c->cmb_ptrs.as<const double *>(), du, p, degree, da, n, n,
+                             c->cmb_tmp.as<double>(), dg, c->stream));
+  }
+  KMG_HIP(hipMemcpyAsync(grad, dg, sizeof(double) * p, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+static int alignf_run(kmg_ctx *c, const double *const *dptrs_dev, int32_t p, const double *d_y,
+                      int64_t n, int64_t ld, double *d_out) {
+  const size_t stride = (size_t)p + (size_t)p * (p + 1) / 2;
+  KMG_TRY(c->cmb_tmp.ensure(sizeof(double) * ((size_t)n * stride + 2 * (size_t)p * n + p)));
+  double *part = c->cmb_tmp.as<double>();
+  double *rmean = part + (size_t)n * stride, *cmean = rmean + (size_t)p * n;
+  double *tmean = cmean + (size_t)p * n;
+  StageTimer t(c, ST_COMBINE);
+  KMG_HIP(launch_alignf(dptrs_dev, p, d_y, n, ld, rmean, cmean, tmean, part, d_out, c->stream));
+  return KMG_OK;
+}
+
+int kmg_alignf_device(kmg_ctx *c, const double *const *d_K, int32_t p, const double *d_y,
+                      int64_t n, int64_t ld, double *d_out) {
+  KMG_TRY(check_combine(c, d_K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  KMG_TRY(upload_ptrs(c, d_K, p));
+  return alignf_run(c, c->cmb_ptrs.as<const double *>(), p, d_y, n, ld, d_out);
+}
+
+int kmg_alignf(kmg_ctx *c, const double *const *K, int32_t p, const double *y, int64_t n,
+               int64_t ld, double *a, double *M) {
+  KMG_TRY(check_combine(c, K, p, n, ld));
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!y || !a || !M) return fail(KMG_EINVAL, "NULL buffer");
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t stride = (size_t)p + (size_t)p * (p + 1) / 2;
+  std::vector<double> host(stride, 0.0);
+  if (n > 0) {
+    std::vector<const double *> dptrs;
+    KMG_TRY(stage_host_kernels(c, K, p, n, ld, dptrs));
+    KMG_TRY(c->cmb_vec.ensure(sizeof(double) * ((size_t)n + stride)));
+    double *dy = c->cmb_vec.as<double>(), *dout = dy + n;
+    KMG_HIP(hipMemcpyAsync(dy, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    KMG_TRY(alignf_run(c, c->cmb_ptrs.as<const double *>(), p, dy, n, n, dout));
+    KMG_HIP(hipMemcpyAsync(host.data(), dout, sizeof(double) * stride, hipMemcpyDeviceToHost,
+                           c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+  }
+  for (int m = 0; m < p; ++m) a[m] = host[m];
+  size_t q = p;
+  for (int l = 0; l < p; ++l)
+    for (int m = l; m < p; ++m, ++q) M[(size_t)l * p + m] = M[(size_t)m * p + l] = host[q];
+  return KMG_OK;
 }
 
 // ------------------------------------------------------------------ RCCL

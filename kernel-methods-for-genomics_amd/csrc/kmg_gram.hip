@@ -103,7 +103,10 @@ __device__ __forceinline__ uint32_t window_code(const uint8_t *rs, int a, int k)
 // ------------------------------------------------------------------ spectrum
 // PACK16: two 16-bit counters per LDS word (valid when every K_ij <= 65535, i.e.
 // P_i * P_j <= 65535; the host checks P_max <= 255).
-template <bool PACK16, int DT, bool NT>
+// G lanes walk one posting list (G * windows ~ the block): each lane issues U entry
+// loads per round before its atomics, so a list of ~30 entries (k=8, N=20000) costs one
+// memory round trip instead of four.
+template <bool PACK16, int DT, bool NT, int G = 1>
 __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
                                                       const int32_t *__restrict__ lens, int64_t ldc,
                                                       const uint32_t *__restrict__ off,
@@ -123,29 +126,45 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
   const int L = g.window > 0 ? g.window : lens[i];
   const uint8_t *rs = codes + i * ldc;
-  for (int a = threadIdx.x; a <= L - g.k; a += blockDim.x) {
-    const uint32_t u = window_code(rs, a, g.k);
-    if (u == KMG_INVALID) continue;
-    const uint32_t beg = o_c[u], end = o_c[u + 1];
-    uint32_t e = beg;
-    for (; e + 8 <= end; e += 8) {
-      uint32_t j[8];
+  auto add = [&](uint32_t j0) {
+    if (PACK16)
+      atomicAdd(&acc[j0 >> 1], 1u << ((j0 & 1) << 4));
+    else
+      atomicAdd(&acc[j0], 1u);
+  };
+  if constexpr (G == 1) {
+    for (int a = threadIdx.x; a <= L - g.k; a += blockDim.x) {
+      const uint32_t u = window_code(rs, a, g.k);
+      if (u == KMG_INVALID) continue;
+      const uint32_t beg = o_c[u], end = o_c[u + 1];
+      uint32_t e = beg;
+      for (; e + 8 <= end; e += 8) {
+        uint32_t j[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) j[q] = ent[e + q];
+        for (int q = 0; q < 8; ++q) j[q] = ent[e + q];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (PACK16)
-          atomicAdd(&acc[j[q] >> 1], 1u << ((j[q] & 1) << 4));
-        else
-          atomicAdd(&acc[j[q]], 1u);
+        for (int q = 0; q < 8; ++q) add(j[q]);
       }
+      for (; e < end; ++e) add(ent[e]);
     }
-    for (; e < end; ++e) {
-      const uint32_t j0 = ent[e];
-      if (PACK16)
-        atomicAdd(&acc[j0 >> 1], 1u << ((j0 & 1) << 4));
-      else
-        atomicAdd(&acc[j0], 1u);
+  } else {
+    constexpr int U = 16;
+    const int gl = threadIdx.x % G;
+    for (int a = threadIdx.x / G; a <= L - g.k; a += blockDim.x / G) {
+      const uint32_t u = window_code(rs, a, g.k);
+      if (u == KMG_INVALID) continue;
+      const uint32_t beg = o_c[u], end = o_c[u + 1];
+      for (uint32_t e = beg + gl; e < end; e += U * G) {
+        uint32_t j[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          const uint32_t x = e + (uint32_t)(q * G);
+          j[q] = x < end ? (uint32_t)ent[x] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q)
+          if (j[q] != 0xFFFFFFFFu) add(j[q]);
+      }
     }
   }
   __syncthreads();
@@ -1268,6 +1287,57 @@ __global__ __launch_bounds__(64) void diag_ham_kernel(IndexGeom g, const uint8_t
   }
 }
 
+// raw self-kernel K_ii when the weights vanish beyond Hamming distance M2 = min(2m, k)
+// <= 4 (m <= 2: every run.py / BASELINE mismatch kernel): one wave per sequence, four per
+// block, k-mers staged in LDS; per lane only the histogram of distances 0..M2 is kept
+// (int32) and weighted once at the end.  Same integer sum as diag_ham_kernel.
+template <int M2>
+__global__ __launch_bounds__(256) void diag_ham_small_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
+                                                             const int32_t *__restrict__ lens,
+                                                             int64_t ldc,
+                                                             const int64_t *__restrict__ wtab,
+                                                             double *__restrict__ diagv,
+                                                             double *__restrict__ dsq) {
+  extern __shared__ __align__(16) uint32_t xk_all[];  // [4][pmax]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  const bool valid = i < g.n;
+  uint32_t *xk = xk_all + wave * g.pmax;
+  int P = 0;
+  if (valid) {
+    const int L = g.window > 0 ? g.window : lens[i];
+    P = max(0, min(L - g.k + 1, g.pmax));
+    const uint8_t *rs = codes + i * ldc;
+    for (int a = lane; a < P; a += 64) xk[a] = window_code(rs, a, g.k);
+  }
+  __syncthreads();
+  if (!valid) return;
+  const uint32_t mask55 = (g.k >= 16) ? 0x55555555u : (0x55555555u & ((1u << (2 * g.k)) - 1u));
+  int cnt[M2 + 1];
+#pragma unroll
+  for (int d = 0; d <= M2; ++d) cnt[d] = 0;
+  for (int a = lane; a < P; a += 64) {
+    const uint32_t xa = xk[a];
+    if (xa == KMG_INVALID) continue;
+    for (int b = 0; b < P; ++b) {
+      const uint32_t yb = xk[b];  // same address in every lane: LDS broadcast
+      const int h = (yb == KMG_INVALID) ? 64 : ham2bit(xa, yb, mask55);
+#pragma unroll
+      for (int d = 0; d <= M2; ++d) cnt[d] += (h == d) ? 1 : 0;
+    }
+  }
+  int64_t s = 0;
+#pragma unroll
+  for (int d = 0; d <= M2; ++d) s += (int64_t)cnt[d] * wtab[d];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (lane == 0) {
+    const double v = (double)s;
+    diagv[i] = v;
+    dsq[i] = __builtin_sqrt(v);  // np.sqrt(np.diag(K)) (kernels.py:408): IEEE sqrt
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 static int env_int(const char *name, int dflt) {
   const char *v = getenv(name);
@@ -1291,7 +1361,16 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const 
   const size_t lds = (size_t)words * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
   const bool nt = env_int("KMG_SP_NT", 1) != 0;
-  if (pack && nt) {
+  // lanes per posting list (KMG_SP_G; 1, 2 or 4): at k=8, N=20000 the kernel is bound by
+  // its row stores, and G = 1 measured 291.6 us against 298.9 (G = 2) and 303.5 (G = 4)
+  const int G = env_int("KMG_SP_G", 1);
+  if (pack && nt && G == 2) {
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true, 2>), grid, dim3(256),
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+  } else if (pack && nt && G == 4) {
+    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true, 4>), grid, dim3(256),
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+  } else if (pack && nt) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true>), grid, dim3(256),
                                                 lds, s, g, codes, lens, ldc, off, ent, row0, o));
   } else if (pack) {
@@ -1488,9 +1567,28 @@ hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_
 }
 
 hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                               int64_t ldc, const int64_t *wtab, double *diagv, double *dsq,
-                               hipStream_t s) {
+                               int64_t ldc, const int64_t *wtab, int max_dist, double *diagv,
+                               double *dsq, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
+  if (max_dist <= 4 && g.pmax <= 4096 && env_int("KMG_DIAG_SMALL", 1)) {
+    const dim3 grid((unsigned)((g.n + 3) / 4));
+    const size_t lds = (size_t)4 * g.pmax * sizeof(uint32_t);
+#define KMG_DIAG(M2_)                                                                          \
+  case M2_:                                                                                    \
+    hipLaunchKernelGGL((diag_ham_small_kernel<M2_>), grid, dim3(256), lds, s, g, codes, lens,   \
+                       ldc, wtab, diagv, dsq);                                                 \
+    break;
+    switch (max_dist < 0 ? 0 : max_dist) {
+      KMG_DIAG(0)
+      KMG_DIAG(1)
+      KMG_DIAG(2)
+      KMG_DIAG(3)
+      default:
+        KMG_DIAG(4)
+    }
+#undef KMG_DIAG
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(diag_ham_kernel, dim3((unsigned)g.n), dim3(64), 0, s, g, codes, lens, ldc,
                      wtab, diagv, dsq);
   return hipGetLastError();

@@ -221,6 +221,112 @@ __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, 
   }
 }
 
+// ------------------------------------------------------------------ index build, v2
+// Two launches, no device-scope atomics and no communication between the workgroups of
+// a launch (v1's count/place passes each pay one device-scope atomic per (block, coarse
+// bucket) on a few hundred hot words, serialised at the memory-side atomic unit):
+//  (1) part_local_kernel: block q stages its sequences, builds the LDS histogram over the
+//      coarse buckets, scans it, and writes its items bucket-sorted into its own region
+//      of tmp (cap items).  Counts and local starts are published bucket-major:
+//      hcnt[b * nblk + q], hstart[b * nblk + q].
+//  (2) part_gather_kernel: one block per coarse bucket b.  The bucket's global start is
+//      sum_q hstart[b][q] (every block's items of the buckets before b) and its size is
+//      sum_q hcnt[b][q]; LDS fine histogram + scan -> off[], then the items are gathered
+//      from every block's segment into ent[].  Results do not depend on dispatch order.
+__global__ __launch_bounds__(IDX_THREADS) void part_local_kernel(
+    IndexGeom g, const uint8_t *__restrict__ codes, int64_t ldc, const int32_t *__restrict__ lens,
+    int rowlen, int nblk, uint32_t cap, uint32_t *__restrict__ hcnt, uint32_t *__restrict__ hstart,
+    uint32_t *__restrict__ tmp) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  __shared__ uint32_t wtmp[IDX_THREADS / 64];
+  const int nbk = (int)g.nbuckets();
+  uint32_t *h = sm;
+  int32_t *slen = (int32_t *)(h + nbk);
+  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) h[b] = 0;
+  const int q = blockIdx.x;
+  const int64_t j0 = (int64_t)q * g.seqs_per_block;
+  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int fb = g.fine_bits;
+  const uint32_t fmask = (1u << fb) - 1u;
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&h[bin >> fb], 1u); });
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hcnt[(size_t)b * nblk + q] = h[b];
+  __syncthreads();
+  lds_excl_scan(h, nbk, wtmp);
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hstart[(size_t)b * nblk + q] = h[b];
+  __syncthreads();
+  uint32_t *out = tmp + (size_t)q * cap;
+  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
+    const uint32_t pos = atomicAdd(&h[bin >> fb], 1u);
+    out[pos] = ((bin & fmask) << 16) | val;
+  });
+}
+
+__global__ __launch_bounds__(FINE_THREADS) void part_gather_kernel(
+    IndexGeom g, int nblk, uint32_t cap, const uint32_t *__restrict__ hcnt,
+    const uint32_t *__restrict__ hstart, const uint32_t *__restrict__ tmp,
+    uint32_t *__restrict__ off, uint16_t *__restrict__ ent) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  __shared__ uint32_t wtmp[FINE_THREADS / 64];
+  __shared__ uint32_t red[2][FINE_THREADS / 64];
+  const int fb = g.fine_bits, nf = 1 << fb;
+  const int b = blockIdx.x;
+  uint32_t *fh = sm;           // nf fine counters
+  uint32_t *cnt = fh + nf;     // nblk: items of block q in bucket b
+  uint32_t *src = cnt + nblk;  // nblk: where they start inside block q's region
+  for (int f = threadIdx.x; f < nf; f += blockDim.x) fh[f] = 0;
+  uint32_t s_cnt = 0, s_start = 0;
+  const uint32_t *cb = hcnt + (size_t)b * nblk, *sb = hstart + (size_t)b * nblk;
+  for (int q = threadIdx.x; q < nblk; q += blockDim.x) {
+    const uint32_t c = cb[q], st = sb[q];
+    cnt[q] = c;
+    src[q] = st;
+    s_cnt += c;
+    s_start += st;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    s_cnt += __shfl_xor(s_cnt, d, 64);
+    s_start += __shfl_xor(s_start, d, 64);
+  }
+  if (lane == 0) {
+    red[0][wave] = s_cnt;
+    red[1][wave] = s_start;
+  }
+  __syncthreads();
+  uint32_t total = 0, base = 0;  // items of bucket b; items of all buckets before b
+  for (int w = 0; w < nw; ++w) {
+    total += red[0][w];
+    base += red[1][w];
+  }
+  for (int q = wave; q < nblk; q += nw) {
+    const uint32_t c = cnt[q];
+    const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+    for (uint32_t x = lane; x < c; x += 64) atomicAdd(&fh[sp[x] >> 16], 1u);
+  }
+  __syncthreads();
+  lds_excl_scan(fh, nf, wtmp);
+  const int64_t nb = g.nbins();
+  const int64_t bin0 = (int64_t)b << fb;
+  for (int f = threadIdx.x; f < nf; f += blockDim.x) {
+    const int64_t bin = bin0 + f;
+    if (bin < nb) off[bin] = base + fh[f];
+  }
+  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) off[nb] = base + total;
+  __syncthreads();
+  for (int q = wave; q < nblk; q += nw) {
+    const uint32_t c = cnt[q];
+    const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+    for (uint32_t x = lane; x < c; x += 64) {
+      const uint32_t it = sp[x];
+      const uint32_t pos = atomicAdd(&fh[it >> 16], 1u);
+      ent[base + pos] = (uint16_t)(it & 0xFFFFu);
+    }
+  }
+}
+
 // Slot layout of the rotated mismatch index (read by gram_mm1s_kernel): one 128-byte line
 // per 4-bin group (copy p, chunk, key): halfwords 0..3 = e1, e2, e3, tot (letter-bin ends
 // relative to the group start, group total), halfwords 4.. = the group's first
@@ -429,6 +535,32 @@ hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uin
   const size_t lds = sizeof(uint32_t) * ((size_t)1 << g.fine_bits);
   hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(FINE_THREADS), lds, s, g, boff,
                      tmp, off, ent, bcount, bcursor);
+  return hipGetLastError();
+}
+
+size_t index_gather_lds(const IndexGeom &g, int64_t nblk) {
+  return sizeof(uint32_t) * (((size_t)1 << g.fine_bits) + 2 * (size_t)nblk);
+}
+
+hipError_t launch_index_local(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, int nblk, uint32_t cap, uint32_t *hcnt,
+                              uint32_t *hstart, uint32_t *tmp, hipStream_t s) {
+  if (g.n == 0 || nblk == 0) return hipSuccess;
+  const int rowlen = part_rowlen(g, ldc);
+  hipLaunchKernelGGL(part_local_kernel, dim3((unsigned)nblk), dim3(g.part_threads),
+                     part_lds(g, rowlen, 1), s, g, codes, ldc, lens, rowlen, nblk, cap, hcnt,
+                     hstart, tmp);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const uint32_t *hcnt,
+                               const uint32_t *hstart, const uint32_t *tmp, uint32_t *off,
+                               uint16_t *ent, hipStream_t s) {
+  const int64_t nbk = g.nbuckets();
+  const size_t lds = index_gather_lds(g, nblk);
+  if (lds > 160 * 1024 - 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(part_gather_kernel, dim3((unsigned)nbk), dim3(FINE_THREADS), lds, s, g, nblk,
+                     cap, hcnt, hstart, tmp, off, ent);
   return hipGetLastError();
 }
 

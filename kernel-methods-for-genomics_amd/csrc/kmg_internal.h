@@ -59,6 +59,15 @@ hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uin
                              hipStream_t s);
 hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
                           int64_t ldc, uint32_t *kmers, hipStream_t s);
+// index build v2 (no device-scope atomics): per-block local sort, then per-bucket gather.
+// hcnt/hstart: nbuckets x nblk (bucket-major); tmp: nblk x cap items.
+size_t index_gather_lds(const IndexGeom &g, int64_t nblk);
+hipError_t launch_index_local(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
+                              int64_t ldc, int nblk, uint32_t cap, uint32_t *hcnt,
+                              uint32_t *hstart, uint32_t *tmp, hipStream_t s);
+hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const uint32_t *hcnt,
+                               const uint32_t *hstart, const uint32_t *tmp, uint32_t *off,
+                               uint16_t *ent, hipStream_t s);
 // rotated mismatch index (rot = 1): one KMG_SLOT_BYTES line per 4-bin group
 hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint16_t *ent,
                             uint4 *slots, hipStream_t s);
@@ -93,9 +102,10 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
                                        int w1, int w2, const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
+// max_dist: largest Hamming distance with a non-zero weight (min(2m, k) for mismatch)
 hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                               int64_t ldc, const int64_t *wtab, double *diagv, double *dsq,
-                               hipStream_t s);
+                               int64_t ldc, const int64_t *wtab, int max_dist, double *diagv,
+                               double *dsq, hipStream_t s);
 
 struct SeqSpec {
   const uint8_t *codes;
@@ -120,6 +130,19 @@ hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int6
                                  int8_t *F, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
                              const OutSpec &o, hipStream_t s);
+
+// kernel-combination consumers (kmg_combine.hip): K = device array of p matrix pointers
+#define KMG_COMBINE_PMAX 12
+hipError_t launch_combine(const double *const *K, const double *u, int p, int degree, int64_t n,
+                          int64_t ld, double *out, int64_t ld_out, hipStream_t s);
+// part: n x p scratch; grad: p
+hipError_t launch_nlck_grad(const double *const *K, const double *u, int p, int degree,
+                            const double *alpha, int64_t n, int64_t ld, double *part,
+                            double *grad, hipStream_t s);
+// rmean/cmean: p x n, tmean: p, part: n x (p + p(p+1)/2), out: p + p(p+1)/2
+hipError_t launch_alignf(const double *const *K, int p, const double *y, int64_t n, int64_t ld,
+                         double *rmean, double *cmean, double *tmean, double *part, double *out,
+                         hipStream_t s);
 
 // host-matrix helpers (normalize_K / center_K)
 hipError_t launch_normalize_dense(double *K, int64_t n, int64_t ld, hipStream_t s);

@@ -27,7 +27,8 @@ EXPORTS = (
     "kmg_gram", "kmg_gram_device", "kmg_normalize", "kmg_center", "kmg_dmalloc", "kmg_dfree",
     "kmg_h2d", "kmg_d2h", "kmg_memset", "kmg_synchronize", "kmg_stream", "kmg_set_timing",
     "kmg_timing_reset", "kmg_stage_ms", "kmg_stage_stats", "kmg_comm_unique_id", "kmg_comm_init", "kmg_allgather_rows",
-    "kmg_comm_destroy",
+    "kmg_comm_destroy", "kmg_combine", "kmg_combine_device", "kmg_nlck_grad",
+    "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device",
 )
 
 
@@ -99,6 +100,12 @@ def load():
             "kmg_comm_init": ([P, P, I32, I32], ctypes.c_int),
             "kmg_allgather_rows": ([P, P, I64, I64, I32, P], ctypes.c_int),
             "kmg_comm_destroy": ([P], ctypes.c_int),
+            "kmg_combine": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
+            "kmg_combine_device": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
+            "kmg_nlck_grad": ([P, P, I32, P, I32, P, I64, I64, P], ctypes.c_int),
+            "kmg_nlck_grad_device": ([P, P, I32, P, I32, P, I64, I64, P], ctypes.c_int),
+            "kmg_alignf": ([P, P, I32, P, I64, I64, P, P], ctypes.c_int),
+            "kmg_alignf_device": ([P, P, I32, P, I64, I64, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -178,6 +185,44 @@ class Context:
         out = np.empty((n, n), dtype=np.float64)
         check(self.lib.kmg_center(self._h, ptr(K), K.strides[0] // 8, ptr(out), n, n))
         return out
+
+    # ---------------------------------------------------------------- combination consumers
+    @staticmethod
+    def _mats(kernels):
+        mats = [np.ascontiguousarray(K, dtype=np.float64) for K in kernels]
+        n = mats[0].shape[0]
+        for K in mats:
+            if K.shape != (n, n):
+                raise ValueError("every kernel must be a square matrix of the same size")
+        arr = (ctypes.c_void_p * len(mats))(*[K.ctypes.data for K in mats])
+        return mats, arr, n
+
+    def combine(self, kernels, u, degree, out=None):
+        """(sum_m u[m] K_m) ** degree on the device (kmg_combine)."""
+        mats, arr, n = self._mats(kernels)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if out is None:
+            out = np.empty((n, n), dtype=np.float64)
+        check(self.lib.kmg_combine(self._h, arr, len(mats), ptr(u), int(degree), n, n, ptr(out), n))
+        return out
+
+    def nlck_grad(self, kernels, u, degree, alpha):
+        mats, arr, n = self._mats(kernels)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        alpha = np.ascontiguousarray(alpha, dtype=np.float64)
+        grad = np.empty(len(mats), dtype=np.float64)
+        check(self.lib.kmg_nlck_grad(self._h, arr, len(mats), ptr(u), int(degree), ptr(alpha), n,
+                                     n, ptr(grad)))
+        return grad
+
+    def alignf(self, kernels, y):
+        mats, arr, n = self._mats(kernels)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        p = len(mats)
+        a = np.empty(p, dtype=np.float64)
+        M = np.empty((p, p), dtype=np.float64)
+        check(self.lib.kmg_alignf(self._h, arr, p, ptr(y), n, n, ptr(a), ptr(M)))
+        return a, M
 
     # ---------------------------------------------------------------- device memory
     def dmalloc(self, nbytes):

@@ -251,3 +251,32 @@ def center(K):
     n = K.shape[0]
     B = np.eye(n) - np.ones((n, n)) / n
     return np.linalg.multi_dot([B, K, B])
+
+
+# --------------------------------------------------------------------- combination consumers
+def nlck_combine(kernels, u, degree):
+    """NLCK.svm_step / get_K (NLCKernels.py:52, 97): np.sum(kernels * u[:, None, None],
+    axis=0) ** degree."""
+    return np.sum(np.asarray(kernels) * np.asarray(u)[:, None, None], axis=0) ** degree
+
+
+def nlck_grad(kernels_fit, u, degree, alpha):
+    """NLCK.grad (NLCKernels.py:61-66)."""
+    K_t = np.sum(np.asarray(kernels_fit) * np.asarray(u)[:, None, None], axis=0) ** (degree - 1)
+    grad = np.zeros(len(kernels_fit))
+    for m, Km in enumerate(kernels_fit):
+        grad[m] = alpha.T.dot(K_t * Km).dot(alpha)
+    return -degree * grad
+
+
+def alignf_stats(kernels_fit, y):
+    """ALIGNF.get_a / get_M (ALIGNF.py:43-58) on center_K (kernels.py:387-395)."""
+    Y = np.outer(y, y)
+    Kc = [center(K) for K in kernels_fit]
+    p = len(Kc)
+    a = np.array([(K * Y).sum() for K in Kc])
+    M = np.zeros((p, p))
+    for i in range(p):
+        for j in range(i, p):
+            M[i, j] = M[j, i] = (Kc[i] * Kc[j]).sum()
+    return a, M

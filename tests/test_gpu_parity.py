@@ -117,6 +117,46 @@ def test_spectrum_ragged_and_chunks(ctx, monkeypatch):
         assert np.array_equal(K.astype(np.int64), ref), chunk
 
 
+@pytest.mark.parametrize("G", ["1", "2", "4"])
+def test_spectrum_lane_groups(ctx, monkeypatch, G):
+    """Every compiled lanes-per-posting-list width of the posting-list spectrum kernel,
+    on ragged + non-ACGT input and at k=8."""
+    monkeypatch.setenv("KMG_SP_G", G)
+    monkeypatch.setenv("KMG_ALGO", "2")
+    rng = np.random.default_rng(6)
+    seqs = ["".join(rng.choice(list("ACGTN"), p=[.24, .24, .24, .24, .04], size=rng.integers(0, 120)))
+            for _ in range(500)]
+    codes, lens = E.encode(seqs)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=4), codes, lens, L.KMG_I32)
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 4))
+    codes, lens = E.synthetic(3000, 101, seed=8)
+    codes[7] = 0  # one list of 94 * (rows holding AAAAAAAA) entries
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 8))
+
+
+@pytest.mark.parametrize("v2", ["0", "1"])
+def test_index_builds(ctx, monkeypatch, v2):
+    """Both posting-index builds (v1: atomics-based MSD partition; v2: per-block local
+    sort + per-bucket gather) give bit-identical Grams, over chunkings and block sizes."""
+    monkeypatch.setenv("KMG_IDX_V2", v2)
+    monkeypatch.setenv("KMG_ALGO", "2")
+    codes, lens = E.synthetic(2500, 101, seed=91)
+    codes[3] = 0
+    ref = cref.spectrum(codes, lens, 8)
+    for chunk, seqs_pb in (("24576", "80"), ("700", "7"), ("24576", "1")):
+        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
+        monkeypatch.setenv("KMG_IDX_SEQS", seqs_pb)
+        K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+        assert np.array_equal(K.astype(np.int64), ref), (chunk, seqs_pb)
+    c2, l2 = codes[:1200], lens[:1200]
+    refm = cref.mismatch_raw(c2, l2, 9, 1)
+    for seqs_pb in ("80", "7"):
+        monkeypatch.setenv("KMG_IDX_SEQS", seqs_pb)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), c2, l2, L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), refm), seqs_pb
+
+
 def test_spectrum_long_sequences_unpacked(ctx):
     """P > 255: the 32-bit LDS accumulator variant."""
     codes, lens = E.synthetic(64, 400, seed=9)
