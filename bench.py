@@ -156,8 +156,42 @@ def spot_check(ctx, name, codes, lens, n, r0, d_rows, out_dtype):
 
 
 def cpu_baseline(name, n, budget_s):
-    """The C oracle (oracle/kmg_oracle.c, OpenMP) on a bounded row sample of the same
-    workload, on this box's host cores."""
+    """The strongest CPU restatement of the reference we have, timed on this box's host
+    cores: scipy-sparse Phi Phi^T (oracle/cpu_ref.py spectrum_phi / mismatch_phi; the
+    reference's own get_phi_u / get_phi_km feature maps, kernels.py:12-25, 161-175, and its
+    np.dot pair loop, kernels.py:41-45, 211-215, as one sparse product).  Phi is built for
+    all N (timed); the product runs on a bounded row sample and the whole job is
+    extrapolated as t_phi + (N / rows) * t_rows.  Single-threaded (scipy's sparse product)."""
+    import cpu_ref
+    seed = 2 if name == "spectrum_k8" else 3
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    t0 = time.perf_counter()
+    F = (cpu_ref.spectrum_phi(codes, lens, 8) if name == "spectrum_k8"
+         else cpu_ref.mismatch_phi(codes, lens, 9, 1))
+    FT = F.T.tocsr()
+    t_phi = time.perf_counter() - t0
+    r = 16
+    while True:
+        t0 = time.perf_counter()
+        (F[:r] @ FT).toarray()
+        t = time.perf_counter() - t0
+        if t >= budget_s / 4 or r >= n:
+            break
+        r = min(n, max(r * 2, int(r * (budget_s / 4) / max(t, 1e-3))))
+    rows = min(n, max(r, int(r * (budget_s / 2) / max(t, 1e-6))))
+    t0 = time.perf_counter()
+    (F[:rows] @ FT).toarray()
+    t_rows = time.perf_counter() - t0
+    t_job = t_phi + (n / rows) * t_rows
+    return {"value": n * n / t_job, "unit": "Gram pairs/s", "cores": 1, "kind": "port",
+            "sample": f"scipy-sparse Phi Phi^T (oracle/cpu_ref.py {'spectrum_phi' if name == 'spectrum_k8' else 'mismatch_phi'}): "
+                      f"Phi of all {n} sequences {t_phi:.2f} s + rows 0..{rows} x {n} in "
+                      f"{t_rows:.2f} s, whole job extrapolated to {t_job:.1f} s, 1 thread"}
+
+
+def cpu_baseline_openmp(name, n, budget_s):
+    """The C oracle (oracle/kmg_oracle.c, pairwise merge / Hamming, OpenMP) on a bounded row
+    sample of the same workload, on this box's host cores."""
     import cref
     cref.load()
     cores = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
@@ -181,6 +215,100 @@ def cpu_baseline(name, n, budget_s):
             "sample": f"oracle/kmg_oracle.c {'kmo_spectrum' if name == 'spectrum_k8' else 'kmo_mismatch_raw'}"
                       f" rows 0..{rows} x {n} columns ({rows * n} pairs) in {t:.2f} s, "
                       f"{cores} OpenMP threads"}
+
+
+# reference kernels.py cost model (measured in the survey container: 8-core
+# Xeon, numpy/OpenBLAS; not this box): seconds for the whole Gram build
+def reference_model_s(kind, n):
+    if kind == "spectrum_k8":
+        return 1.10 * n + 10.0e-6 * n * (n + 1) / 2
+    return 78.0 * n + 35e-6 * n * (n + 1) / 2 + 0.46e-6 * n * n / 2
+
+
+def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, oracle_row):
+    """One workload on rows [r0, r1) x all n columns, device-resident, this rank only."""
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc((r1 - r0) * n * esz)
+    try:
+        def step():
+            ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, d_out, n)
+
+        for _ in range(warmup):
+            step()
+        ctx.synchronize()
+        ctx.set_timing(True)
+        ctx.timing_reset()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.synchronize()
+        wall = time.perf_counter() - t0
+        ctx.set_timing(False)
+        stages = {}
+        for st in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram"):
+            tot, cnt = ctx.stage_stats(st)
+            if cnt:
+                stages[st] = round(tot / cnt, 4)
+        ok = True
+        for r in spot_rows:
+            row = np.empty(n, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + (r - r0) * n * esz))
+            ref = oracle_row(codes, lens, r)
+            ok &= bool(np.array_equal(row.astype(ref.dtype), ref))
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    ms = wall / steps * 1e3
+    return {"N": n, "rows": r1 - r0, "steps": steps, "ms_per_step": ms,
+            "pairs_per_s": (r1 - r0) * n / (ms / 1e3), "stages_ms": stages,
+            "spot_check_rows": list(spot_rows), "spot_check": ok}
+
+
+def extras(ctx, cpu_rates):
+    """BASELINE configs[3] and [4] and the drop-in host path, on this GPU (N=1 runs only)."""
+    import cref
+    out = {}
+    sp = lambda c, l, r: cref.spectrum(c, l, 8, rows=(r, r + 1))[0]  # noqa: E731
+    mm = lambda c, l, r: cref.mismatch_rows(c, l, 9, 1, rows=(r, r + 1))[0]  # noqa: E731
+    n4 = 100000
+    c4 = run_slab(ctx, P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n4, 4, 0, n4, 3, 1,
+                  (0, 54321, n4 - 1), sp)
+    c4["workload"] = ("BASELINE configs[3]: spectrum k=8, N=100000 x L=101, full K on 1 GPU, "
+                      "int32 (40 GB), posting-list formulation (DESIGN.md: why not the fp32 GEMM)")
+    c4["gram_hbm_frac"] = (4.0 * n4 * n4 + 26.0 * n4) / (c4["stages_ms"]["gram"] / 1e3) / HBM_PEAK
+    c4["reference_model_s"] = reference_model_s("spectrum_k8", n4)
+    c4["speedup_vs_reference_model"] = c4["reference_model_s"] / (c4["ms_per_step"] / 1e3)
+    if cpu_rates.get("spectrum_k8"):
+        c4["speedup_vs_cpu_baseline"] = c4["pairs_per_s"] / cpu_rates["spectrum_k8"]
+    out["config4_spectrum_k8_n100000"] = c4
+    n5 = 200000
+    c5 = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64, n5,
+                  5, 0, n5 // 8, 2, 1, (0, n5 // 8 - 1), mm)
+    c5["workload"] = ("BASELINE configs[4] per-GPU share: mismatch (9,1), N=200000, rows "
+                      "0..25000 (one of 8 ranks) x 200000 columns, float64 normalised (40 GB)")
+    c5["projected_8gpu_ms_per_step"] = c5["ms_per_step"]
+    c5["projected_8gpu_pairs_per_s"] = 8 * c5["pairs_per_s"]
+    c5["reference_model_s"] = reference_model_s("mismatch_k9_m1", n5)
+    out["config5_mismatch_k9_n200000_rank_slab"] = c5
+    # drop-in host path: kmg_gram with a host float64 output (what kernels.get_spectrum_K
+    # returns), PCIe D2H included; never `value`
+    codes, lens = E.synthetic(20000, 101, seed=2)
+    p8 = P.make(L.KMG_SPECTRUM, k=8)
+    K = ctx.gram(p8, codes, lens, L.KMG_F64)
+    t0 = time.perf_counter()
+    K = ctx.gram(p8, codes, lens, L.KMG_F64, out=K)
+    t = time.perf_counter() - t0
+    out["host_path_spectrum_k8_n20000"] = {
+        "ms": t * 1e3, "pairs_per_s": 20000 ** 2 / t,
+        "note": "kmg_gram: H2D codes + device build + 3.2 GB float64 D2H into a numpy array"}
+    del K
+    return out
 
 
 def load_traffic(workload):
@@ -207,6 +335,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mismatch", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the N=100000 / N=200000 slab / host-path lines (N=1 only)")
     args = ap.parse_args()
 
     dist = Dist()
@@ -222,6 +352,17 @@ def main():
         mm = run_workload(ctx, dist, "mismatch_k9_m1",
                           P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
                           n, 3, max(3, args.steps // 4), 1, args.allgather)
+    cpu = {}
+    if dist.world == 1 and dist.rank == 0 and not args.no_cpu:
+        cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
+        cpu["spectrum_k8_openmp"] = cpu_baseline_openmp("spectrum_k8", n, args.cpu_budget / 2)
+        if mm:
+            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", n, args.cpu_budget / 2)
+            cpu["mismatch_k9_m1_openmp"] = cpu_baseline_openmp("mismatch_k9_m1", n,
+                                                               args.cpu_budget / 4)
+    extra = None
+    if dist.world == 1 and not args.no_extra:
+        extra = extras(ctx, {k: v["value"] for k, v in cpu.items()})
     ctx.close()
 
     rows = sp["rows"]
@@ -260,11 +401,17 @@ def main():
             "hbm_frac_of_gram_kernel": (mm_bytes / (mm["gram_kernel_ms"] / 1e3)) / HBM_PEAK,
             "spot_check": mm["spot_check"],
         }
-    if dist.world == 1 and dist.rank == 0 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
+    if cpu:
+        line["cpu_baseline"] = cpu["spectrum_k8"]
+        line["cpu_baseline_alt"] = cpu["spectrum_k8_openmp"]
+        line["reference_model"] = {
+            "s": reference_model_s("spectrum_k8", n),
+            "note": "reference kernels.py cost model (BASELINE.md), survey container 8-core Xeon"}
         if mm:
-            line["secondary"]["cpu_baseline"] = cpu_baseline("mismatch_k9_m1", n,
-                                                             args.cpu_budget / 2)
+            line["secondary"]["cpu_baseline"] = cpu["mismatch_k9_m1"]
+            line["secondary"]["cpu_baseline_alt"] = cpu["mismatch_k9_m1_openmp"]
+    if extra:
+        line["configs"] = extra
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()

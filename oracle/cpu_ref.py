@@ -280,3 +280,54 @@ def alignf_stats(kernels_fit, y):
         for j in range(i, p):
             M[i, j] = M[j, i] = (Kc[i] * Kc[j]).sum()
     return a, M
+
+
+# --------------------------------------------------------------------- sparse CPU comparator
+def _kmer_matrix(codes, lens, k, P):
+    km = np.zeros((codes.shape[0], P), dtype=np.int64)
+    for q in range(k):
+        km = km * 4 + (codes[:, q:q + P] & 3)
+    return km
+
+
+def spectrum_phi(codes, lens, k):
+    """Phi of get_phi_u (kernels.py:12-25) as a CSR count matrix (N x 4^k); windows
+    range(len(x)-k+1), windows holding a non-ACGT symbol dropped."""
+    n = len(lens)
+    P = int(lens.max()) - k + 1 if n else 0
+    if P <= 0:
+        return sp.csr_matrix((n, 4 ** k), dtype=np.int32)
+    km = _kmer_matrix(codes, lens, k, P)
+    bad = np.zeros(km.shape, dtype=bool)
+    for q in range(k):
+        bad |= codes[:, q:q + P] >= 4
+    valid = (np.arange(P)[None, :] <= (lens[:, None] - k)) & ~bad
+    r, c = np.nonzero(valid)
+    return sp.csr_matrix((np.ones(r.size, dtype=np.int32), (r, km[r, c])), shape=(n, 4 ** k))
+
+
+def neighbour_masks(k, m):
+    """xor masks of every k-mer within Hamming distance m of a k-mer (2-bit letters)."""
+    from itertools import combinations, product
+    masks = [0]
+    for t in range(1, min(m, k) + 1):
+        for pos in combinations(range(k), t):
+            for letters in product((1, 2, 3), repeat=t):
+                v = 0
+                for p_, x in zip(pos, letters):
+                    v |= x << (2 * p_)
+                masks.append(v)
+    return np.array(masks, dtype=np.int64)
+
+
+def mismatch_phi(codes, lens, k, m, window=101):
+    """Phi_km of get_phi_km (kernels.py:161-175) as a CSR count matrix: each window a adds
+    1 to every k-mer within Hamming distance m of x[a:a+k] (ACGT input, length >= window)."""
+    n = len(lens)
+    P = window - k + 1
+    km = _kmer_matrix(codes, lens, k, P)
+    masks = neighbour_masks(k, m)
+    cols = (km[:, :, None] ^ masks[None, None, :]).reshape(n, -1)
+    rows = np.repeat(np.arange(n), cols.shape[1])
+    return sp.csr_matrix((np.ones(rows.size, dtype=np.int32), (rows, cols.ravel())),
+                         shape=(n, 4 ** k))

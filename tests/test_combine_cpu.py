@@ -39,3 +39,19 @@ def test_alignf_centring_identity():
         t = r.mean()
         fast = (K - (r - t)[:, None]) - c[None, :]
         assert np.allclose(fast, cpu_ref.center(K), rtol=0, atol=1e-12)
+
+
+def test_sparse_comparator_matches_oracle():
+    """The scipy-sparse Phi Phi^T CPU comparator (bench.py cpu_baseline) equals the C oracle."""
+    import cref
+    from kmgram import encode as E
+    codes, lens = E.synthetic(120, 101, seed=4)
+    F = cpu_ref.spectrum_phi(codes, lens, 8)
+    assert np.array_equal((F @ F.T).toarray(), cref.spectrum(codes, lens, 8))
+    G = cpu_ref.mismatch_phi(codes, lens, 9, 1)
+    assert np.array_equal((G[:30] @ G.T).toarray(), cref.mismatch_raw(codes, lens, 9, 1, rows=(0, 30)))
+    rng = np.random.default_rng(5)
+    seqs = ["".join(rng.choice(list("ACGTN"), size=rng.integers(0, 60))) for _ in range(50)]
+    c2, l2 = E.encode(seqs)
+    F2 = cpu_ref.spectrum_phi(c2, l2, 3)
+    assert np.array_equal((F2 @ F2.T).toarray(), cref.spectrum(c2, l2, 3))
