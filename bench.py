@@ -308,6 +308,78 @@ def extras(ctx, cpu_rates):
         "ms": t * 1e3, "pairs_per_s": 20000 ** 2 / t,
         "note": "kmg_gram: H2D codes + device build + 3.2 GB float64 D2H into a numpy array"}
     del K
+    out["downstream"] = downstream(ctx)
+    return out
+
+
+FP64_PEAK = 78.6e12  # MI355X dense fp64 (spec sheet)
+
+
+def downstream(ctx):
+    """§8f consumers of the Gram on device-resident float64 matrices at the production size
+    (n = 9000 = train + val + test of the 3 TFs, utils.py:151-153): NLCK combination
+    (HBM-bound) and the KRR / KLR solves (fp64 factorisation)."""
+    import ctypes
+    n, p, reps = 9000, 3, 5
+    rng = np.random.default_rng(9)
+    A = rng.standard_normal((n, 64))
+    K = A @ A.T
+    K += n * 1e-3 * np.eye(n)
+    d = np.sqrt(np.diag(K))
+    K = K / d[:, None] / d[None, :]
+    nbytes = K.nbytes
+    dK = [ctx.dmalloc(nbytes) for _ in range(p)]
+    for x in dK:
+        ctx.h2d(x, K)
+    d_out = ctx.dmalloc(nbytes)
+    d_u = ctx.dmalloc(8 * p)
+    ctx.h2d(d_u, np.array([0.5, 0.3, 0.2]))
+    y = np.where(rng.random(n) > 0.5, 1.0, -1.0)
+    d_y, d_a = ctx.dmalloc(8 * n), ctx.dmalloc(8 * n)
+    ctx.h2d(d_y, y)
+    ptrs = (ctypes.c_void_p * p)(*[x.value for x in dK])
+    out = {}
+    try:
+        ctx.set_timing(True)
+        L.check(ctx.lib.kmg_combine_device(ctx.handle, ptrs, p, d_u, 2, n, n, d_out, n))
+        ctx.synchronize()
+        ctx.timing_reset()
+        for _ in range(reps):
+            L.check(ctx.lib.kmg_combine_device(ctx.handle, ptrs, p, d_u, 2, n, n, d_out, n))
+        tot, cnt = ctx.stage_stats("combine")
+        ms = tot / cnt
+        alg = 8.0 * (p + 1) * n * n
+        out["nlck_combine_n9000_p3_deg2"] = {
+            "ms": ms, "alg_bytes": alg, "achieved_GBps": alg / (ms / 1e3) / 1e9,
+            "hbm_frac": alg / (ms / 1e3) / HBM_PEAK, "source": "NLCKernels.py:52,97",
+            "note": "(sum_m u_m K_m)**2 on 3 device-resident 9000x9000 fp64 K, 1 write"}
+        for m_ in (n, 2000):
+            L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[0], n, m_, d_y, 0.1, d_a))
+            ctx.synchronize()
+            ctx.timing_reset()
+            for _ in range(reps):
+                L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[0], n, m_, d_y, 0.1, d_a))
+            tot, cnt = ctx.stage_stats("solve")
+            ms = tot / cnt
+            fl = m_ ** 3 / 3.0 + 2.0 * m_ * m_
+            out[f"krr_solve_n{m_}"] = {
+                "ms": ms, "alg_flops": fl, "achieved_TFLOPs": fl / (ms / 1e3) / 1e12,
+                "fp64_frac": fl / (ms / 1e3) / FP64_PEAK, "source": "KRR.py:33",
+                "note": "Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I, fp64"}
+        it = ctypes.c_int32(0)
+        m_ = 2000
+        ctx.timing_reset()
+        L.check(ctx.lib.kmg_klr_fit_device(ctx.handle, dK[0], n, m_, d_y, 0.1, 1e-5, 50, d_a,
+                                           ctypes.byref(it)))
+        tot, cnt = ctx.stage_stats("solve")
+        out["klr_fit_n2000"] = {"ms": tot, "iterations": it.value,
+                                "ms_per_iteration": tot / max(1, it.value),
+                                "source": "KLR.py:57-75",
+                                "note": "IRLS: dgemv + HIP IRLS kernel + Cholesky per step"}
+    finally:
+        ctx.set_timing(False)
+        for x in dK + [d_out, d_u, d_y, d_a]:
+            ctx.dfree(x)
     return out
 
 

@@ -40,7 +40,8 @@ enum {
   KMG_EHIP = 3,         /* HIP runtime error */
   KMG_ENOMEM = 4,       /* device allocation failed */
   KMG_ERCCL = 5,        /* RCCL error */
-  KMG_ENODEV = 6        /* no HIP device visible */
+  KMG_ENODEV = 6,       /* no HIP device visible */
+  KMG_ESINGULAR = 7     /* dense learner: the system matrix is singular (LinAlgError) */
 };
 
 /* kernel families (one per reference get_*_K) */
@@ -145,6 +146,25 @@ int kmg_alignf(kmg_ctx *ctx, const double *const *K, int32_t p, const double *y,
 int kmg_alignf_device(kmg_ctx *ctx, const double *const *d_K, int32_t p, const double *d_y,
                       int64_t n, int64_t ld, double *d_out);
 
+/*
+ * Dense learners on a Gram matrix.  K: n x n float64, row stride ld.
+ * The system is factorised on the device (rocSOLVER Cholesky, LU with partial pivoting if
+ * it is not positive definite); KMG_ESINGULAR where np.linalg.inv raises LinAlgError.
+ */
+/* KRR.fit (KRR.py:33): alpha = inv(K + lambda * n * I) . y */
+int kmg_krr_solve(kmg_ctx *ctx, const double *K, int64_t ld, int64_t n, const double *y,
+                  double lambda, double *alpha);
+int kmg_krr_solve_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
+                         const double *d_y, double lambda, double *d_alpha);
+/* KLR.fit (KLR.py:30-75): IRLS from alpha = 0; each step m = K.alpha, W = s(m)s(-m),
+ * z = m + y / s(-y m), alpha = W^1/2 inv(W^1/2 K W^1/2 + n lambda I) W^1/2 z, repeated
+ * while ||alpha - alpha_prev||_2 > tol, at most maxiter times; iters = steps taken */
+int kmg_klr_fit(kmg_ctx *ctx, const double *K, int64_t ld, int64_t n, const double *y,
+                double lambda, double tol, int32_t maxiter, double *alpha, int32_t *iters);
+int kmg_klr_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
+                       const double *d_y, double lambda, double tol, int32_t maxiter,
+                       double *d_alpha, int32_t *iters);
+
 /* device memory / stream helpers for device-resident callers */
 int kmg_dmalloc(kmg_ctx *ctx, void **ptr, size_t bytes);
 int kmg_dfree(kmg_ctx *ctx, void *ptr);
@@ -156,8 +176,8 @@ int kmg_stream(kmg_ctx *ctx, void **hip_stream);
 
 /* Per-stage device timings from HIP events recorded on the context stream around
  * every launch while timing is enabled (kmg_set_timing(ctx,1)); nothing is
- * synchronised until a stage time is read.  Stage names: "extract", "scan",
- * "scatter", "diag", "gram".
+ * synchronised until a stage time is read.  Stage names: "count", "scan",
+ * "place", "fine", "diag", "gram", "extract", "features", "pack", "combine", "solve".
  *   kmg_stage_ms:    that stage in the last call (-1 if it did not run)
  *   kmg_stage_stats: sum and count over every call since kmg_timing_reset */
 int kmg_set_timing(kmg_ctx *ctx, int32_t enable);

@@ -8,6 +8,8 @@
 //   normalize_K 398-415, center_K 387-395.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -80,12 +82,12 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"count",   "scan",     "place", "fine",   "diag",
-                             "gram",    "extract",  "features", "pack", "combine"};
-constexpr int kNumStages = 10;
+const char *kStageNames[] = {"count",   "scan",     "place", "fine",   "diag",  "gram",
+                             "extract", "features", "pack",  "combine", "solve"};
+constexpr int kNumStages = 11;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES, ST_PACK,
-  ST_COMBINE
+  ST_COMBINE, ST_SOLVE
 };
 
 }  // namespace
@@ -99,6 +101,8 @@ struct kmg_ctx {
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
+  DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
+  rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
   bool timing = false;
@@ -620,11 +624,12 @@ int kmg_destroy(kmg_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->blas) rocblas_destroy_handle(c->blas);
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
-                    &c->cmb_out, &c->cmb_tmp};
+                    &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -983,6 +988,193 @@ int kmg_alignf(kmg_ctx *c, const double *const *K, int32_t p, const double *y, i
   size_t q = p;
   for (int l = 0; l < p; ++l)
     for (int m = l; m < p; ++m, ++q) M[(size_t)l * p + m] = M[(size_t)m * p + l] = host[q];
+  return KMG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ dense learners on K
+// KRR.fit (KRR.py:33) and KLR.fit (KLR.py:30-75): the reference inverts the n x n system
+// with np.linalg.inv and multiplies; here the same system is factorised on the device
+// (rocSOLVER Cholesky; LU with partial pivoting when the matrix is not positive definite,
+// as inv() would still succeed there) and solved for the one right-hand side.
+static int blas_handle(kmg_ctx *c) {
+  if (!c->blas) {
+    if (rocblas_create_handle(&c->blas) != rocblas_status_success) {
+      c->blas = nullptr;
+      return fail(KMG_EHIP, "rocblas_create_handle failed");
+    }
+  }
+  if (rocblas_set_stream(c->blas, c->stream) != rocblas_status_success)
+    return fail(KMG_EHIP, "rocblas_set_stream failed");
+  return KMG_OK;
+}
+
+#define KMG_BLAS(expr)                                                                \
+  do {                                                                                \
+    rocblas_status _s = (expr);                                                       \
+    if (_s != rocblas_status_success)                                                 \
+      return fail(KMG_EHIP, "%s failed: %s (%s:%d)", #expr, rocblas_status_to_string(_s), \
+                  __FILE__, __LINE__);                                                \
+  } while (0)
+
+// Build the system into sv_mat (build()), factorise, solve in place into rhs.
+// B = diag(s) K diag(s) + shift I is symmetric, so its row-major image is its own
+// column-major image and rocSOLVER's column-major routines apply unchanged.
+template <typename Build>
+static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs) {
+  if (n > INT32_MAX / 2) return fail(KMG_EUNSUPPORTED, "n=%lld too large for rocSOLVER", (long long)n);
+  const rocblas_int ni = (rocblas_int)n;
+  double *B = c->sv_mat.as<double>();
+  rocblas_int *info = c->sv_info.as<rocblas_int>();
+  rocblas_int *ipiv = info + 4;
+  rocblas_int hinfo = 0;
+  KMG_TRY(build());
+  KMG_BLAS(rocsolver_dpotrf(c->blas, rocblas_fill_lower, ni, B, ni, info));
+  KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  if (hinfo == 0) {
+    KMG_BLAS(rocsolver_dpotrs(c->blas, rocblas_fill_lower, ni, 1, B, ni, rhs, ni));
+    return KMG_OK;
+  }
+  KMG_TRY(build());  // not positive definite: rebuild and use LU, like inv()
+  KMG_BLAS(rocsolver_dgetrf(c->blas, ni, ni, B, ni, ipiv, info));
+  KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  if (hinfo != 0) return fail(KMG_ESINGULAR, "Singular matrix");
+  // B holds the row-major A, i.e. A^T in column-major terms: solve A^T^T x = rhs
+  KMG_BLAS(rocsolver_dgetrs(c->blas, rocblas_operation_transpose, ni, 1, B, ni, ipiv, rhs, ni));
+  return KMG_OK;
+}
+
+static int solver_workspace(kmg_ctx *c, int64_t n, size_t nvec) {
+  KMG_TRY(blas_handle(c));
+  KMG_TRY(c->sv_mat.ensure(sizeof(double) * (size_t)n * (size_t)n));
+  KMG_TRY(c->sv_vec.ensure(sizeof(double) * (size_t)n * nvec + 64));
+  KMG_TRY(c->sv_info.ensure(sizeof(rocblas_int) * ((size_t)n + 8)));
+  return KMG_OK;
+}
+
+static int krr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                   double lambda, double *d_alpha) {
+  KMG_TRY(solver_workspace(c, n, 0));
+  StageTimer t(c, ST_SOLVE);
+  KMG_HIP(hipMemcpyAsync(d_alpha, d_y, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
+                         c->stream));
+  const double shift = lambda * (double)n;  // self.lbda * self.n (KRR.py:33)
+  auto build = [&]() -> int {
+    KMG_HIP(launch_shift_scale(d_K, ld, nullptr, shift, n, c->sv_mat.as<double>(), n, c->stream));
+    return KMG_OK;
+  };
+  return solve_system(c, build, n, d_alpha);
+}
+
+static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                   double lambda, double tol, int32_t maxiter, double *d_alpha, int32_t *iters) {
+  KMG_TRY(solver_workspace(c, n, 5));
+  StageTimer t(c, ST_SOLVE);
+  double *prev = c->sv_vec.as<double>(), *m = prev + n, *s = m + n, *rhs = s + n;
+  double *cur = rhs + n, *dsum = cur + n;
+  KMG_HIP(hipMemsetAsync(prev, 0, sizeof(double) * (size_t)n, c->stream));
+  const double shift = (double)n * lambda;  // self.n * self.lbda (KLR.py:53)
+  const double one = 1.0, zero = 0.0;
+  auto build = [&]() -> int {
+    KMG_HIP(launch_shift_scale(d_K, ld, s, shift, n, c->sv_mat.as<double>(), n, c->stream));
+    return KMG_OK;
+  };
+  double diff = INFINITY;
+  int32_t it = 0;
+  for (int32_t r = 0; r < maxiter; ++r) {
+    if (!(diff > tol)) continue;  // the reference keeps looping without work (KLR.py:68-69)
+    // m = K . alpha_prev: row-major K is K^T column-major, so apply the transpose
+    KMG_BLAS(rocblas_dgemv(c->blas, rocblas_operation_transpose, (rocblas_int)n, (rocblas_int)n,
+                           &one, d_K, (rocblas_int)ld, prev, 1, &zero, m, 1));
+    KMG_HIP(launch_irls(m, d_y, n, s, rhs, c->stream));
+    KMG_TRY(solve_system(c, build, n, rhs));
+    KMG_HIP(launch_scale_diff(s, rhs, prev, n, cur, dsum, c->stream));
+    double h = 0.0;
+    KMG_HIP(hipMemcpyAsync(&h, dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    KMG_HIP(hipMemcpyAsync(prev, cur, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
+                           c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+    diff = std::sqrt(h);
+    ++it;
+  }
+  KMG_HIP(hipMemcpyAsync(d_alpha, prev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
+                         c->stream));
+  if (iters) *iters = it;
+  return KMG_OK;
+}
+
+static int check_solver(kmg_ctx *c, const void *K, int64_t n, int64_t ld, const void *y,
+                        const void *alpha) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  if (n < 0 || (n > 0 && ld < n)) return fail(KMG_EINVAL, "bad matrix shape");
+  if (n > 0 && (!K || !y || !alpha)) return fail(KMG_EINVAL, "NULL buffer");
+  return KMG_OK;
+}
+
+// host K / y -> device (K into sv staging cmb_k, y and alpha into cmb_vec)
+static int stage_solver_inputs(kmg_ctx *c, const double *K, int64_t ld, int64_t n,
+                               const double *y, double **dK, double **dy, double **da) {
+  KMG_TRY(c->cmb_k.ensure(sizeof(double) * (size_t)n * (size_t)n));
+  KMG_TRY(c->cmb_vec.ensure(sizeof(double) * 2 * (size_t)n));
+  *dK = c->cmb_k.as<double>();
+  *dy = c->cmb_vec.as<double>();
+  *da = *dy + n;
+  KMG_HIP(hipMemcpy2DAsync(*dK, n * 8, K, ld * 8, n * 8, n, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipMemcpyAsync(*dy, y, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  return KMG_OK;
+}
+
+extern "C" {
+
+int kmg_krr_solve_device(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                         double lambda, double *d_alpha) {
+  KMG_TRY(check_solver(c, d_K, n, ld, d_y, d_alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  return krr_run(c, d_K, ld, n, d_y, lambda, d_alpha);
+}
+
+int kmg_krr_solve(kmg_ctx *c, const double *K, int64_t ld, int64_t n, const double *y,
+                  double lambda, double *alpha) {
+  KMG_TRY(check_solver(c, K, n, ld, y, alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (n == 0) return KMG_OK;
+  double *dK, *dy, *da;
+  KMG_TRY(stage_solver_inputs(c, K, ld, n, y, &dK, &dy, &da));
+  KMG_TRY(krr_run(c, dK, n, n, dy, lambda, da));
+  KMG_HIP(hipMemcpyAsync(alpha, da, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_klr_fit_device(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                       double lambda, double tol, int32_t maxiter, double *d_alpha,
+                       int32_t *iters) {
+  KMG_TRY(check_solver(c, d_K, n, ld, d_y, d_alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (iters) *iters = 0;
+  if (n == 0) return KMG_OK;
+  return klr_run(c, d_K, ld, n, d_y, lambda, tol, maxiter, d_alpha, iters);
+}
+
+int kmg_klr_fit(kmg_ctx *c, const double *K, int64_t ld, int64_t n, const double *y,
+                double lambda, double tol, int32_t maxiter, double *alpha, int32_t *iters) {
+  KMG_TRY(check_solver(c, K, n, ld, y, alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (iters) *iters = 0;
+  if (n == 0) return KMG_OK;
+  double *dK, *dy, *da;
+  KMG_TRY(stage_solver_inputs(c, K, ld, n, y, &dK, &dy, &da));
+  KMG_TRY(klr_run(c, dK, n, n, dy, lambda, tol, maxiter, da, iters));
+  KMG_HIP(hipMemcpyAsync(alpha, da, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
   return KMG_OK;
 }
 

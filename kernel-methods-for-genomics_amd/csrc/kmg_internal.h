@@ -144,6 +144,16 @@ hipError_t launch_alignf(const double *const *K, int p, const double *y, int64_t
                          double *rmean, double *cmean, double *tmean, double *part, double *out,
                          hipStream_t s);
 
+// dense learners on K (kmg_solve.hip): B = diag(s) K diag(s) + shift I (s may be NULL)
+hipError_t launch_shift_scale(const double *K, int64_t ldk, const double *s, double shift,
+                              int64_t n, double *B, int64_t ldb, hipStream_t st);
+// KLR IRLS step: s = sqrt(sig(m) sig(-m)), rhs = s * (m + y / sig(-y m))
+hipError_t launch_irls(const double *m, const double *y, int64_t n, double *s, double *rhs,
+                       hipStream_t st);
+// alpha = s * x, out[0] = ||alpha - prev||^2
+hipError_t launch_scale_diff(const double *s, const double *x, const double *prev, int64_t n,
+                             double *alpha, double *out, hipStream_t st);
+
 // host-matrix helpers (normalize_K / center_K)
 hipError_t launch_normalize_dense(double *K, int64_t n, int64_t ld, hipStream_t s);
 hipError_t launch_center_dense(const double *K, int64_t ldk, double *out, int64_t ld_out,

@@ -13,7 +13,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "libkmgram.so")
 
-KMG_OK, KMG_EINVAL, KMG_EUNSUPPORTED, KMG_EHIP, KMG_ENOMEM, KMG_ERCCL, KMG_ENODEV = range(7)
+(KMG_OK, KMG_EINVAL, KMG_EUNSUPPORTED, KMG_EHIP, KMG_ENOMEM, KMG_ERCCL, KMG_ENODEV,
+ KMG_ESINGULAR) = range(8)
 KMG_SPECTRUM, KMG_MISMATCH, KMG_WD, KMG_WDS, KMG_SUBSTRING, KMG_LOCALALIGN, KMG_GAPPY = range(1, 8)
 KMG_I32, KMG_F32, KMG_F64 = 1, 2, 3
 KMG_LA_REFERENCE, KMG_LA_INTENDED = 0, 1
@@ -28,7 +29,8 @@ EXPORTS = (
     "kmg_h2d", "kmg_d2h", "kmg_memset", "kmg_synchronize", "kmg_stream", "kmg_set_timing",
     "kmg_timing_reset", "kmg_stage_ms", "kmg_stage_stats", "kmg_comm_unique_id", "kmg_comm_init", "kmg_allgather_rows",
     "kmg_comm_destroy", "kmg_combine", "kmg_combine_device", "kmg_nlck_grad",
-    "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device",
+    "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
+    "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device",
 )
 
 
@@ -73,6 +75,7 @@ def load():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         lib = ctypes.CDLL(LIB_PATH)
         P, I32, I64, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+        D = ctypes.c_double
         sig = {
             "kmg_version": ([], ctypes.c_int),
             "kmg_last_error": ([], ctypes.c_char_p),
@@ -106,6 +109,12 @@ def load():
             "kmg_nlck_grad_device": ([P, P, I32, P, I32, P, I64, I64, P], ctypes.c_int),
             "kmg_alignf": ([P, P, I32, P, I64, I64, P, P], ctypes.c_int),
             "kmg_alignf_device": ([P, P, I32, P, I64, I64, P], ctypes.c_int),
+            "kmg_krr_solve": ([P, P, I64, I64, P, D, P], ctypes.c_int),
+            "kmg_krr_solve_device": ([P, P, I64, I64, P, D, P], ctypes.c_int),
+            "kmg_klr_fit": ([P, P, I64, I64, P, D, D, I32, P, ctypes.POINTER(I32)],
+                            ctypes.c_int),
+            "kmg_klr_fit_device": ([P, P, I64, I64, P, D, D, I32, P, ctypes.POINTER(I32)],
+                                   ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -120,6 +129,8 @@ def check(status):
         msg = load().kmg_last_error().decode(errors="replace")
         if status == KMG_EUNSUPPORTED:
             raise KmgUnsupported(status, msg)
+        if status == KMG_ESINGULAR:
+            raise np.linalg.LinAlgError(msg)
         raise KmgError(status, msg)
 
 
@@ -223,6 +234,38 @@ class Context:
         M = np.empty((p, p), dtype=np.float64)
         check(self.lib.kmg_alignf(self._h, arr, p, ptr(y), n, n, ptr(a), ptr(M)))
         return a, M
+
+    # ---------------------------------------------------------------- dense learners
+    @staticmethod
+    def _system(K, y):
+        K = np.asarray(K, dtype=np.float64)
+        if K.ndim != 2 or K.shape[0] != K.shape[1]:
+            raise ValueError("K must be a square matrix")
+        if K.strides[1] != 8 or K.strides[0] % 8:
+            K = np.ascontiguousarray(K)
+        y = np.ascontiguousarray(y, dtype=np.float64).reshape(-1)
+        if y.shape[0] != K.shape[0]:
+            raise ValueError(f"y has {y.shape[0]} entries for a {K.shape[0]} x {K.shape[0]} K")
+        return K, y
+
+    def krr_solve(self, K, y, lbda):
+        """alpha = inv(K + lbda * n * I) . y (KRR.py:33), factorised on the device."""
+        K, y = self._system(K, y)
+        n = K.shape[0]
+        alpha = np.empty(n, dtype=np.float64)
+        check(self.lib.kmg_krr_solve(self._h, ptr(K), K.strides[0] // 8, n, ptr(y), float(lbda),
+                                     ptr(alpha)))
+        return alpha
+
+    def klr_fit(self, K, y, lbda, tol, maxiter):
+        """IRLS of KLR.fit (KLR.py:57-75); returns (alpha, iterations)."""
+        K, y = self._system(K, y)
+        n = K.shape[0]
+        alpha = np.empty(n, dtype=np.float64)
+        it = ctypes.c_int32(0)
+        check(self.lib.kmg_klr_fit(self._h, ptr(K), K.strides[0] // 8, n, ptr(y), float(lbda),
+                                   float(tol), int(maxiter), ptr(alpha), ctypes.byref(it)))
+        return alpha, it.value
 
     # ---------------------------------------------------------------- device memory
     def dmalloc(self, nbytes):

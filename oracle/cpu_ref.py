@@ -331,3 +331,36 @@ def mismatch_phi(codes, lens, k, m, window=101):
     rows = np.repeat(np.arange(n), cols.shape[1])
     return sp.csr_matrix((np.ones(rows.size, dtype=np.int32), (rows, cols.ravel())),
                          shape=(n, 4 ** k))
+
+
+# --------------------------------------------------------------------- dense learners on K
+def krr_alpha(K_fit, y, lbda):
+    """KRR.fit's solve (KRR.py:33): inv(K_fit + lbda * n * I) . y, with np.linalg.inv."""
+    n = K_fit.shape[0]
+    return np.dot(np.linalg.inv(K_fit + lbda * n * np.eye(n)), y)
+
+
+def _sig(x):
+    return 1 / (1 + np.exp(-x))
+
+
+def klr_alpha(K_fit, y, lbda, tol=1e-5, maxiter=50):
+    """KLR.fit's IRLS (KLR.py:30-75): from alpha = 0, m = K alpha, W = s(m) s(-m),
+    z = m + y / s(-y m), alpha = Ws inv(Ws K Ws + n lbda I) Ws z while the step's 2-norm
+    exceeds tol, at most maxiter steps.  Returns (alpha, steps)."""
+    n = K_fit.shape[0]
+    prev = np.zeros(n)
+    diff, steps = np.inf, 0
+    for _ in range(maxiter):
+        if not diff > tol:
+            continue
+        m = K_fit @ prev
+        W = _sig(m) * _sig(-m)
+        z = m + y / _sig(-y * m)
+        s = np.sqrt(W)
+        A = s[:, None] * K_fit * s[None, :] + n * lbda * np.eye(n)
+        alpha = s * (np.linalg.inv(A) @ (s * z))
+        diff = np.linalg.norm(alpha - prev, ord=2)
+        prev = alpha
+        steps += 1
+    return prev, steps
