@@ -376,6 +376,16 @@ def downstream(ctx):
                                 "ms_per_iteration": tot / max(1, it.value),
                                 "source": "KLR.py:57-75",
                                 "note": "IRLS: dgemv + HIP IRLS kernel + Cholesky per step"}
+        for m_ in (2000, n):
+            it, obj = ctypes.c_int32(0), ctypes.c_double(0.0)
+            ctx.timing_reset()
+            L.check(ctx.lib.kmg_svm_fit_device(ctx.handle, dK[0], n, m_, d_y, 1.0, 1e-10, 100,
+                                               d_a, ctypes.byref(it), ctypes.byref(obj)))
+            tot, cnt = ctx.stage_stats("solve")
+            out[f"svm_fit_n{m_}"] = {
+                "ms": tot, "iterations": it.value, "ms_per_iteration": tot / max(1, it.value),
+                "objective": obj.value, "source": "SVM.py:78-89",
+                "note": "C=1 QP by Mehrotra interior point: dgemv + Cholesky + 2 solves per step"}
     finally:
         ctx.set_timing(False)
         for x in dK + [d_out, d_u, d_y, d_a]:

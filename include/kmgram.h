@@ -165,6 +165,17 @@ int kmg_klr_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
                        const double *d_y, double lambda, double tol, int32_t maxiter,
                        double *d_alpha, int32_t *iters);
 
+/* C_SVM.fit, solver 'CVX' (SVM.py:78-89): the QP cvxopt.solvers.qp(P=K, q=-y,
+ * G=[diag(y); -diag(y)], h=[C; 0]) = min 1/2 a'Ka - y'a s.t. 0 <= y_i a_i <= C (y in {-1,1}),
+ * by a Mehrotra predictor-corrector interior-point method; stops when the duality gap
+ * <= tol * max(1, |objective|) and ||dual residual||_inf <= tol (or after maxiter steps).
+ * iters = steps taken, objective = 1/2 a'Ka - y'a at the returned a. */
+int kmg_svm_fit(kmg_ctx *ctx, const double *K, int64_t ld, int64_t n, const double *y, double C,
+                double tol, int32_t maxiter, double *alpha, int32_t *iters, double *objective);
+int kmg_svm_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
+                       const double *d_y, double C, double tol, int32_t maxiter,
+                       double *d_alpha, int32_t *iters, double *objective);
+
 /* device memory / stream helpers for device-resident callers */
 int kmg_dmalloc(kmg_ctx *ctx, void **ptr, size_t bytes);
 int kmg_dfree(kmg_ctx *ctx, void *ptr);

@@ -1063,7 +1063,7 @@ static int krr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
                          c->stream));
   const double shift = lambda * (double)n;  // self.lbda * self.n (KRR.py:33)
   auto build = [&]() -> int {
-    KMG_HIP(launch_shift_scale(d_K, ld, nullptr, shift, n, c->sv_mat.as<double>(), n, c->stream));
+    KMG_HIP(launch_shift_scale(d_K, ld, nullptr, shift, nullptr, n, c->sv_mat.as<double>(), n, c->stream));
     return KMG_OK;
   };
   return solve_system(c, build, n, d_alpha);
@@ -1079,7 +1079,7 @@ static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
   const double shift = (double)n * lambda;  // self.n * self.lbda (KLR.py:53)
   const double one = 1.0, zero = 0.0;
   auto build = [&]() -> int {
-    KMG_HIP(launch_shift_scale(d_K, ld, s, shift, n, c->sv_mat.as<double>(), n, c->stream));
+    KMG_HIP(launch_shift_scale(d_K, ld, s, shift, nullptr, n, c->sv_mat.as<double>(), n, c->stream));
     return KMG_OK;
   };
   double diff = INFINITY;
@@ -1103,6 +1103,75 @@ static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
   KMG_HIP(hipMemcpyAsync(d_alpha, prev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice,
                          c->stream));
   if (iters) *iters = it;
+  return KMG_OK;
+}
+
+
+// C_SVM.fit (SVM.py:78-89): min 1/2 a'Ka - y'a, 0 <= y_i a_i <= C, by the primal-dual
+// interior-point iteration of kmg_solve.hip; one factorisation and two solves per step.
+static int svm_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                   double C, double tol, int32_t maxiter, double *d_alpha, int32_t *iters,
+                   double *objective) {
+  KMG_TRY(blas_handle(c));
+  KMG_TRY(c->sv_mat.ensure(sizeof(double) * (size_t)n * (size_t)n));
+  KMG_TRY(c->sv_vec.ensure(sizeof(double) * ((size_t)n * KMG_SVM_NVEC + 16)));
+  KMG_TRY(c->sv_info.ensure(sizeof(rocblas_int) * ((size_t)n + 8)));
+  if (n > INT32_MAX / 2) return fail(KMG_EUNSUPPORTED, "n=%lld too large for rocSOLVER", (long long)n);
+  StageTimer t(c, ST_SOLVE);
+  const rocblas_int ni = (rocblas_int)n;
+  double *vec = c->sv_vec.as<double>(), *sc = vec + (size_t)n * KMG_SVM_NVEC;
+  double *v = vec + (size_t)n * KMG_SVM_V, *u = vec + (size_t)n * KMG_SVM_U;
+  double *rhs = vec + (size_t)n * KMG_SVM_RHS, *D = vec + (size_t)n * 4;
+  double *B = c->sv_mat.as<double>();
+  rocblas_int *info = c->sv_info.as<rocblas_int>(), *ipiv = info + 4;
+  const double one = 1.0, zero = 0.0;
+  double h[3] = {0, 0, 0};
+  auto residual = [&]() -> int {
+    KMG_HIP(launch_svm(1, d_y, n, C, vec, sc, nullptr, c->stream));
+    KMG_BLAS(rocblas_dgemv(c->blas, rocblas_operation_transpose, ni, ni, &one, d_K,
+                           (rocblas_int)ld, v, 1, &zero, u, 1));
+    KMG_HIP(launch_svm(2, d_y, n, C, vec, sc, nullptr, c->stream));
+    KMG_HIP(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+    return KMG_OK;
+  };
+  KMG_HIP(launch_svm(0, d_y, n, C, vec, sc, nullptr, c->stream));
+  int32_t it = 0;
+  for (; it < maxiter; ++it) {
+    KMG_TRY(residual());
+    const double gap = 2.0 * (double)n * h[0];
+    if (gap <= tol * std::max(1.0, std::fabs(h[2])) && h[1] <= tol) break;
+    // M = YKY + diag(D), factorised once, solved for the predictor and the corrector
+    KMG_HIP(launch_shift_scale(d_K, ld, d_y, 0.0, D, n, B, n, c->stream));
+    KMG_BLAS(rocsolver_dpotrf(c->blas, rocblas_fill_lower, ni, B, ni, info));
+    rocblas_int hinfo = 0;
+    KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+    bool lu = false;
+    if (hinfo != 0) {  // K not numerically PSD: LU on the same system
+      KMG_HIP(launch_shift_scale(d_K, ld, d_y, 0.0, D, n, B, n, c->stream));
+      KMG_BLAS(rocsolver_dgetrf(c->blas, ni, ni, B, ni, ipiv, info));
+      KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
+      KMG_HIP(hipStreamSynchronize(c->stream));
+      if (hinfo != 0) return fail(KMG_ESINGULAR, "Singular KKT system");
+      lu = true;
+    }
+    auto solve = [&]() -> int {
+      if (lu)
+        KMG_BLAS(rocsolver_dgetrs(c->blas, rocblas_operation_transpose, ni, 1, B, ni, ipiv, rhs, ni));
+      else
+        KMG_BLAS(rocsolver_dpotrs(c->blas, rocblas_fill_lower, ni, 1, B, ni, rhs, ni));
+      return KMG_OK;
+    };
+    KMG_TRY(solve());
+    KMG_HIP(launch_svm(3, d_y, n, C, vec, sc, nullptr, c->stream));
+    KMG_TRY(solve());
+    KMG_HIP(launch_svm(4, d_y, n, C, vec, sc, nullptr, c->stream));
+  }
+  if (it == maxiter) KMG_TRY(residual());  // objective of the last iterate
+  KMG_HIP(launch_svm(5, d_y, n, C, vec, sc, d_alpha, c->stream));
+  if (iters) *iters = it;
+  if (objective) *objective = h[2];
   return KMG_OK;
 }
 
@@ -1173,6 +1242,38 @@ int kmg_klr_fit(kmg_ctx *c, const double *K, int64_t ld, int64_t n, const double
   double *dK, *dy, *da;
   KMG_TRY(stage_solver_inputs(c, K, ld, n, y, &dK, &dy, &da));
   KMG_TRY(klr_run(c, dK, n, n, dy, lambda, tol, maxiter, da, iters));
+  KMG_HIP(hipMemcpyAsync(alpha, da, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_svm_fit_device(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
+                       double C, double tol, int32_t maxiter, double *d_alpha, int32_t *iters,
+                       double *objective) {
+  KMG_TRY(check_solver(c, d_K, n, ld, d_y, d_alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (iters) *iters = 0;
+  if (objective) *objective = 0.0;
+  if (!(C > 0)) return fail(KMG_EINVAL, "C must be > 0");
+  if (n == 0) return KMG_OK;
+  return svm_run(c, d_K, ld, n, d_y, C, tol, maxiter, d_alpha, iters, objective);
+}
+
+int kmg_svm_fit(kmg_ctx *c, const double *K, int64_t ld, int64_t n, const double *y, double C,
+                double tol, int32_t maxiter, double *alpha, int32_t *iters, double *objective) {
+  KMG_TRY(check_solver(c, K, n, ld, y, alpha));
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_HIP(hipSetDevice(c->device));
+  if (iters) *iters = 0;
+  if (objective) *objective = 0.0;
+  if (!(C > 0)) return fail(KMG_EINVAL, "C must be > 0");
+  if (n == 0) return KMG_OK;
+  for (int64_t i = 0; i < n; ++i)
+    if (y[i] != 1.0 && y[i] != -1.0) return fail(KMG_EINVAL, "labels must be -1 or 1");
+  double *dK, *dy, *da;
+  KMG_TRY(stage_solver_inputs(c, K, ld, n, y, &dK, &dy, &da));
+  KMG_TRY(svm_run(c, dK, n, n, dy, C, tol, maxiter, da, iters, objective));
   KMG_HIP(hipMemcpyAsync(alpha, da, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
   return KMG_OK;

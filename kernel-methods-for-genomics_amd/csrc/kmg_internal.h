@@ -145,14 +145,26 @@ hipError_t launch_alignf(const double *const *K, int p, const double *y, int64_t
                          hipStream_t s);
 
 // dense learners on K (kmg_solve.hip): B = diag(s) K diag(s) + shift I (s may be NULL)
+// (dvec may be NULL; else B[i][i] += shift + dvec[i])
 hipError_t launch_shift_scale(const double *K, int64_t ldk, const double *s, double shift,
-                              int64_t n, double *B, int64_t ldb, hipStream_t st);
+                              const double *dvec, int64_t n, double *B, int64_t ldb,
+                              hipStream_t st);
 // KLR IRLS step: s = sqrt(sig(m) sig(-m)), rhs = s * (m + y / sig(-y m))
 hipError_t launch_irls(const double *m, const double *y, int64_t n, double *s, double *rhs,
                        hipStream_t st);
 // alpha = s * x, out[0] = ||alpha - prev||^2
 hipError_t launch_scale_diff(const double *s, const double *x, const double *prev, int64_t n,
                              double *alpha, double *out, hipStream_t st);
+
+// C-SVM dual QP interior point (kmg_solve.hip): vec = 11 x n doubles, sc >= 8 doubles.
+// phase 0 init, 1 v = y o x, 2 residual/D/predictor rhs (sc = mu, ||rd||_inf, obj),
+// 3 affine step + corrector rhs, 4 corrector step + update, 5 alpha = y o x
+#define KMG_SVM_NVEC 11
+#define KMG_SVM_V 8   // vector index of v (GEMV input)
+#define KMG_SVM_U 9   // vector index of u (GEMV output)
+#define KMG_SVM_RHS 10
+hipError_t launch_svm(int phase, const double *y, int64_t n, double C, double *vec, double *sc,
+                      double *alpha, hipStream_t st);
 
 // host-matrix helpers (normalize_K / center_K)
 hipError_t launch_normalize_dense(double *K, int64_t n, int64_t ld, hipStream_t s);

@@ -30,7 +30,8 @@ EXPORTS = (
     "kmg_timing_reset", "kmg_stage_ms", "kmg_stage_stats", "kmg_comm_unique_id", "kmg_comm_init", "kmg_allgather_rows",
     "kmg_comm_destroy", "kmg_combine", "kmg_combine_device", "kmg_nlck_grad",
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
-    "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device",
+    "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
+    "kmg_svm_fit_device",
 )
 
 
@@ -115,6 +116,10 @@ def load():
                             ctypes.c_int),
             "kmg_klr_fit_device": ([P, P, I64, I64, P, D, D, I32, P, ctypes.POINTER(I32)],
                                    ctypes.c_int),
+            "kmg_svm_fit": ([P, P, I64, I64, P, D, D, I32, P, ctypes.POINTER(I32),
+                             ctypes.POINTER(D)], ctypes.c_int),
+            "kmg_svm_fit_device": ([P, P, I64, I64, P, D, D, I32, P, ctypes.POINTER(I32),
+                                    ctypes.POINTER(D)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -266,6 +271,17 @@ class Context:
         check(self.lib.kmg_klr_fit(self._h, ptr(K), K.strides[0] // 8, n, ptr(y), float(lbda),
                                    float(tol), int(maxiter), ptr(alpha), ctypes.byref(it)))
         return alpha, it.value
+
+    def svm_fit(self, K, y, C, tol=1e-10, maxiter=100):
+        """C_SVM.fit's QP (SVM.py:78-89) on the device; returns (alpha, steps, objective)."""
+        K, y = self._system(K, y)
+        n = K.shape[0]
+        alpha = np.empty(n, dtype=np.float64)
+        it, obj = ctypes.c_int32(0), ctypes.c_double(0.0)
+        check(self.lib.kmg_svm_fit(self._h, ptr(K), K.strides[0] // 8, n, ptr(y), float(C),
+                                   float(tol), int(maxiter), ptr(alpha), ctypes.byref(it),
+                                   ctypes.byref(obj)))
+        return alpha, it.value, obj.value
 
     # ---------------------------------------------------------------- device memory
     def dmalloc(self, nbytes):

@@ -1,12 +1,15 @@
 """Dense learners on a precomputed Gram matrix, solved on the device.
 
-Mirrors of the reference's KRR (KRR.py:4-66) and KLR (KLR.py:4-110): same constructor
-arguments, same ``fit(X, y)`` / ``predict(X)`` / ``score(pred, y)`` contract on pandas
-frames with ``Id`` and ``Bound`` columns, same fitted attributes.  The n x n system that
-the reference inverts with ``np.linalg.inv`` (KRR.py:33, KLR.py:53-54) is factorised on
-the MI355X by libkmgram (``kmg_krr_solve`` / ``kmg_klr_fit``, rocSOLVER Cholesky with an
-LU fallback); the O(n_sv^2) bookkeeping around it (support-vector selection, intercept,
-decision values) stays on the host as vectorised numpy.  No CPU fallback for the solve.
+Mirrors of the reference's KRR (KRR.py:4-66), KLR (KLR.py:4-110) and C_SVM
+(SVM.py:6-128): same constructor arguments, same ``fit(X, y)`` / ``predict(X)`` /
+``score(pred, y)`` contract on pandas frames with ``Id`` and ``Bound`` columns, same fitted
+attributes.  The n x n system that the reference inverts with ``np.linalg.inv`` (KRR.py:33,
+KLR.py:53-54) is factorised on the MI355X by libkmgram (``kmg_krr_solve`` /
+``kmg_klr_fit``: rocSOLVER Cholesky with an LU fallback), and C_SVM's cvxopt QP
+(SVM.py:78-89; cvxopt is not installed here) is solved by a device interior-point method
+(``kmg_svm_fit``).  The O(n_sv^2) bookkeeping around the solve (support-vector selection,
+intercept, decision values) stays on the host as vectorised numpy.  No CPU fallback for
+the solve.
 """
 import numpy as np
 
@@ -28,7 +31,7 @@ def _labels(y):
 
 
 class _GramLearner:
-    """Shared fit/predict bookkeeping of KRR.py and KLR.py (identical in both files)."""
+    """Shared fit/predict bookkeeping (identical in KRR.py, KLR.py and SVM.py)."""
 
     def _solve(self, K_fit, y_fit):
         raise NotImplementedError
@@ -101,4 +104,40 @@ class KLR(_GramLearner):
     def _solve(self, K_fit, y_fit):
         alpha, self.iterations = default_engine().ctx.klr_fit(K_fit, y_fit, self.lbda, self.tol,
                                                                self.maxiter)
+        return alpha
+
+
+class C_SVM(_GramLearner):
+    """C-SVM without intercept in the QP (SVM.py:6-128): a = argmin 1/2 a'Ka - y'a with
+    0 <= y_i a_i <= C, then the shared support-vector / intercept bookkeeping.  Both of the
+    reference's solvers ('CVX': cvxopt.solvers.qp, SVM.py:78-89; 'BFGS': L-BFGS-B from a
+    random start, SVM.py:66-76) solve this same convex QP; here both run the device
+    interior-point method to a duality gap of ``tol`` (``iterations``, ``objective`` kept)."""
+
+    def __init__(self, K, ID, C=10, eps=1e-5, solver="CVX", print_callbacks=True, tol=1e-10,
+                 maxiter=100):
+        self.K = K
+        self.ID = ID
+        self.C = C
+        self.eps = eps
+        self.solver = solver
+        self.print_callbacks = print_callbacks
+        self.Nfeval = 1
+        self.tol = tol
+        self.maxiter = maxiter
+
+    def loss(self, a):
+        """a'Ka - 2 a'y, twice the QP objective (SVM.py:29-34; host evaluation)."""
+        return -(2 * np.dot(a, self.y_fit) - np.dot(a.T, np.dot(self.K_fit, a)))
+
+    def jac(self, a):
+        return -(2 * self.y_fit - 2 * np.dot(self.K_fit, a))
+
+    def _solve(self, K_fit, y_fit):
+        if self.solver not in ("CVX", "BFGS"):
+            # the reference leaves self.a unset and fails on its next line (SVM.py:91)
+            raise AttributeError("'C_SVM' object has no attribute 'a'")
+        y = np.asarray(y_fit, dtype=np.float64)
+        alpha, self.iterations, self.objective = default_engine().ctx.svm_fit(
+            K_fit, y, self.C, self.tol, self.maxiter)
         return alpha

@@ -364,3 +364,58 @@ def klr_alpha(K_fit, y, lbda, tol=1e-5, maxiter=50):
         prev = alpha
         steps += 1
     return prev, steps
+
+
+def svm_dual(K_fit, y, C, tol=1e-10, maxiter=100):
+    """C_SVM.fit's QP (SVM.py:78-89): cvxopt.solvers.qp(P=K, q=-y, G=[diag(y); -diag(y)],
+    h=[C; 0]), i.e. min 1/2 a'Ka - y'a s.t. 0 <= y_i a_i <= C.  cvxopt is not installed
+    here, so this restates the problem and solves it with a Mehrotra predictor-corrector
+    primal-dual interior-point method in x = y o a (box 0 <= x <= C, Q = YKY), the
+    algorithm family of cvxopt.solvers.qp.  Returns (a, steps, objective).  Pinned against
+    scipy's L-BFGS-B on the reference's own 'BFGS' formulation (SVM.py:70-76) in
+    tests/test_learners_cpu.py; cvxopt's own numbers are unavailable (parity unpinned)."""
+    K_fit = np.asarray(K_fit, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    n = K_fit.shape[0]
+    Q = y[:, None] * K_fit * y[None, :]
+    x = np.full(n, 0.5 * C)
+    z1 = np.ones(n)
+    z2 = np.ones(n)
+
+    def step_to_boundary(x, dx, z1, dz1, z2, dz2):
+        t = np.inf
+        for v, d in ((x, dx), (C - x, -dx), (z1, dz1), (z2, dz2)):
+            neg = d < 0  # v + t d >= 0 needs t <= -v / d
+            if neg.any():
+                t = min(t, np.min(-v[neg] / d[neg]))
+        return t
+
+    steps = 0
+    for steps in range(maxiter + 1):
+        s2 = C - x
+        qx = Q @ x
+        rd = qx - 1.0 - z1 + z2
+        mu = (x @ z1 + s2 @ z2) / (2 * n)
+        obj = 0.5 * x @ qx - x.sum()
+        if (2 * n * mu <= tol * max(1.0, abs(obj)) and np.max(np.abs(rd)) <= tol) or steps == maxiter:
+            break
+        M = Q + np.diag(z1 / x + z2 / s2)
+        L = np.linalg.cholesky(M)
+
+        def solve(r):
+            return np.linalg.solve(L.T, np.linalg.solve(L, r))
+
+        dxa = solve(-rd - z1 + z2)
+        dz1a = (-x * z1 - z1 * dxa) / x
+        dz2a = (-s2 * z2 + z2 * dxa) / s2
+        ta = min(1.0, step_to_boundary(x, dxa, z1, dz1a, z2, dz2a))
+        mu_aff = ((x + ta * dxa) @ (z1 + ta * dz1a) + (s2 - ta * dxa) @ (z2 + ta * dz2a)) / (2 * n)
+        smu = (mu_aff / mu) ** 3 * mu
+        t1 = smu - x * z1 - dxa * dz1a
+        t2 = smu - s2 * z2 + dxa * dz2a
+        dx = solve(-rd + t1 / x - t2 / s2)
+        dz1 = (t1 - z1 * dx) / x
+        dz2 = (t2 + z2 * dx) / s2
+        t = min(1.0, 0.99 * step_to_boundary(x, dx, z1, dz1, z2, dz2))
+        x, z1, z2 = x + t * dx, z1 + t * dz1, z2 + t * dz2
+    return y * x, steps, obj

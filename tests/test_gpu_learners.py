@@ -99,3 +99,50 @@ def test_learner_empty(ctx):
     assert ctx.krr_solve(np.zeros((0, 0)), np.zeros(0), 0.1).shape == (0,)
     a, it = ctx.klr_fit(np.zeros((0, 0)), np.zeros(0), 0.1, 1e-5, 10)
     assert a.shape == (0,) and it == 0
+
+
+# ---------------------------------------------------------------- C_SVM (SVM.py:78-89)
+# cvxopt is not installed, so the reference's own numbers cannot be produced here (parity
+# unpinned to cvxopt); the device interior point is checked against the oracle's
+# (oracle/cpu_ref.svm_dual, itself checked against L-BFGS-B in test_learners_cpu.py):
+# same optimum to 1e-9 relative in the objective, alpha within 1e-5 * C.
+@pytest.mark.parametrize("n,C", [(1, 1.0), (40, 0.1), (300, 1.0), (300, 10.0), (2000, 2.0)])
+def test_svm_fit_vs_oracle(ctx, n, C):
+    K = _psd(n, max(1, n // 4), 3 * n + 1)
+    y = np.where(np.random.default_rng(n).random(n) > 0.5, 1.0, -1.0)
+    a, steps, obj = ctx.svm_fit(K, y, C)
+    ra, rsteps, robj = cpu_ref.svm_dual(K, y, C)
+    assert steps < 100
+    assert obj == pytest.approx(robj, rel=1e-9, abs=1e-12)
+    np.testing.assert_allclose(a, ra, atol=1e-5 * C, rtol=0)
+    x = y * a
+    assert np.all(x >= 0) and np.all(x <= C)
+
+
+@pytest.mark.parametrize("C", [0.5, 1.9])
+def test_dropin_csvm_on_xtr0(engine, C):
+    """run.py's learner (C_SVM(K, ID, C=...), run.py:15) through the drop-in SVM.py on the
+    normalised SP k=6 Gram of Xtr0 rows 0..399: predictions equal the oracle's."""
+    from SVM import C_SVM
+    K, labels, _, _ = LC.load()
+    ID = np.arange(LC.N_ALL)
+    svm = C_SVM(K, ID, C=C, print_callbacks=False)
+    svm.fit(pd.DataFrame({"Id": ID[:LC.N_FIT]}),
+            pd.DataFrame({"Id": ID[:LC.N_FIT], "Bound": labels[:LC.N_FIT]}))
+    pred = svm.predict(pd.DataFrame({"Id": ID[LC.N_FIT:]}))
+    idx_fit = np.arange(LC.N_FIT)
+    ra, _, robj = cpu_ref.svm_dual(K[:LC.N_FIT, :LC.N_FIT], labels[:LC.N_FIT].astype(float), C)
+    _, _, rb, rpred = LC.bookkeeping(K, ra, idx_fit, labels[:LC.N_FIT], 1e-5,
+                                     np.arange(LC.N_FIT, LC.N_ALL))
+    assert svm.objective == pytest.approx(robj, rel=1e-9)
+    assert svm.b == pytest.approx(rb, rel=1e-4, abs=1e-6)
+    assert np.array_equal(pred, rpred)
+    assert 0.0 <= svm.score(pred, labels[LC.N_FIT:]) <= 1.0
+
+
+def test_svm_bad_arguments(ctx):
+    K = np.eye(3)
+    with pytest.raises(Exception):
+        ctx.svm_fit(K, np.array([1.0, -1.0, 1.0]), 0.0)
+    with pytest.raises(Exception):
+        ctx.svm_fit(K, np.array([1.0, 0.0, 1.0]), 1.0)
