@@ -474,7 +474,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         int max_chunk = std::min(65536, env_or("KMG_MM_CHUNK", 20480));
         if (use_slots) {  // mean list (4-bin group) length <= 40: inline in one line
           const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
-          max_chunk = (int)std::max<int64_t>(8, std::min<int64_t>(max_chunk, cap));
+          max_chunk = (int)std::max<int64_t>(8, std::min<int64_t>({max_chunk, cap, 64000}));
         }
         choose_chunks(g, max_chunk);
       } else {
@@ -501,11 +501,15 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_HIP(launch_gram_spectrum(g, d_codes, d_lens, ldc, c->off.as<uint32_t>(),
                                      c->ent.as<uint16_t>(), row0, row1, o, c->stream));
       } else {
-        if (use_slots)
+        if (use_slots) {
+          // full K on one device: upper triangle + mirror (halves the LDS atomics)
+          const int tri = (row0 == 0 && row1 == n && n >= 256 && env_or("KMG_MM_TRI", 1)) ? 1 : 0;
           KMG_HIP(launch_gram_mismatch1_slots(g, d_codes, ldc, c->slots.as<uint4>(),
                                               c->off.as<uint32_t>(), c->ent.as<uint16_t>(), row0,
-                                              row1, (int)w[0], (int)w[1], (int)w[2], o,
+                                              row1, (int)w[0], (int)w[1], (int)w[2], o, tri,
                                               c->stream));
+          if (tri) KMG_HIP(launch_mirror_lower(o.out, o.ld, n, o.dtype, c->stream));
+        }
         else if (use_rot)
           KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
                                             c->ent.as<uint16_t>(),

@@ -1209,6 +1209,233 @@ __global__ __launch_bounds__(1024) void gram_mm1s_kernel(IndexGeom g,
   }
 }
 
+// LDS byte address of the 16-bit column in halfword H of w (acc at LDS offset 0): one
+// SDWA shift instead of extract + shift-add.
+template <int H>
+__device__ __forceinline__ uint32_t col_addr_sdwa(uint32_t w) {
+  uint32_t r;
+  if constexpr (H == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+        "src1_sel:WORD_0"
+        : "=v"(r)
+        : "v"(w));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+        "src1_sel:WORD_1"
+        : "=v"(r)
+        : "v"(w));
+  return r;
+}
+
+// ------------------------------------------------------------------ mismatch m=1, v8
+// Same slot layout and list enumeration as v7 (gram_mm1s_kernel), two lanes per list,
+// with the per-slot work cut down (v7 is VALU-issue-bound, profiles/r01s5_mm_pmc.txt):
+//   * the two lanes of a list take the line's 16-byte pieces interleaved (lane gl takes
+//     pieces gl, gl+2, gl+4, gl+6), so step j covers halfwords [16j, 16j+16) of every list
+//     in the wave and a step is skipped when no list of the wave has entries there
+//     (lists average ~28 entries of 60: the last step is almost never needed);
+//   * SENT: positions past a group's entries hold sentinel columns (slot_pack_kernel)
+//     that land in a 1024-dword scratch tail of the accumulator, so a slot costs
+//     extract + weight select + ds_add with no validity test and no exec-mask juggling.
+//     Only the four header halfwords of piece 0 are predicated.
+template <int K, int D, int MODE>
+__global__ __launch_bounds__(1024) void gram_mm1t_kernel(IndexGeom g,
+                                                         const uint8_t *__restrict__ codes,
+                                                         int64_t ldc,
+                                                         const uint4 *__restrict__ slots,
+                                                         const uint32_t *__restrict__ off,
+                                                         const uint16_t *__restrict__ ent,
+                                                         int64_t row0, int64_t rows, int w0,
+                                                         int w1, int w2, OutSpec o, int tri,
+                                                         int porder) {
+  constexpr int G = 2, CH = 4;
+  constexpr bool SENT = MODE == 1;  // sentinel slots
+  constexpr bool DUMMY = MODE == 2;  // inactive lanes add into a per-lane dummy dword
+  constexpr int NSUB = K + 3 * K * (K - 1) / 2;
+  extern __shared__ __align__(16) uint32_t smem[];  // acc first: LDS offset 0 (col_addr_sdwa)
+  const int c = (int)(blockIdx.x / rows);
+  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  const int64_t i = row0 + il;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int accl = SENT ? accw + 1024 : DUMMY ? accw + 64 : accw;  // + scratch tail
+  // tri (full K, tested slots only): columns j >= i of row i; a chunk wholly left of the
+  // diagonal is skipped, the lower triangle is mirrored afterwards (mirror_lower_kernel)
+  const int64_t jlo = (tri && !SENT) ? max((int64_t)0, i - col0) : 0;
+  if (jlo >= cw) return;
+  const uint32_t thr4 = (uint32_t)jlo * 4u;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rotk = smem + accl;   // [P][K]: rot_p(u_a)
+  uint32_t *sub = rotk + P * K;   // [NSUB]: p | q << 8 | ci << 16 (q = 0xFF: type 1)
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accl >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  const uint8_t *rs = codes + i * ldc;
+  for (int t = threadIdx.x; t < P * K; t += blockDim.x) {
+    const int a = t / K, p = t - a * K;
+    const uint32_t u = window_code(rs, a, K);
+    rotk[t] = (drop_letter_g(u, p, K) << 2) | letter_at_g(u, p, K);
+  }
+  for (int s = threadIdx.x; s < NSUB; s += blockDim.x) {
+    uint32_t d;
+    if (porder) {
+      // copy-major: copy p owns 1 + 3p sub-lists (type 1, then (q < p, ci)); lists are
+      // walked sub-list-major, so the lists in flight on an XCD read one copy's slot
+      // table (2.1 MB at k = 9) and stay in its 4 MB L2
+      int pp = 0;
+      while ((pp + 1) + 3 * (pp + 1) * pp / 2 <= s) ++pp;
+      const int r = s - (pp + 3 * pp * (pp - 1) / 2);
+      d = r == 0 ? ((uint32_t)pp | (0xFFu << 8))
+                 : ((uint32_t)pp | ((uint32_t)((r - 1) / 3) << 8) | ((uint32_t)((r - 1) % 3) << 16));
+    } else if (s < K) {
+      d = (uint32_t)s | (0xFFu << 8);
+    } else {
+      const int t = s - K, pi = t / 3, ci = t - 3 * pi;
+      int pp = 1;
+      while ((pp + 1) * pp / 2 <= pi) ++pp;
+      d = (uint32_t)pp | ((uint32_t)(pi - pp * (pp - 1) / 2) << 8) | ((uint32_t)ci << 16);
+    }
+    sub[s] = d;
+  }
+  __syncthreads();
+
+  const uint32_t chunk_groups = (uint32_t)c * (g.nkeys >> 2);
+  const uint32_t copy_groups = (uint32_t)g.nchunks * (g.nkeys >> 2);
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int lane = threadIdx.x & 63;
+  const int total = P * NSUB;
+  const uint32_t dummy4 = (uint32_t)(accw + lane) * 4u;
+
+  auto describe = [&](int L, uint32_t &gidx, uint32_t &meta) {
+    const bool valid = L < total;
+    const int Lc = valid ? L : total - 1;
+    int a, s;
+    if (porder) {
+      s = Lc / P;
+      a = Lc - s * P;
+    } else {
+      a = Lc / NSUB;
+      s = Lc - a * NSUB;
+    }
+    const uint32_t d = sub[s];
+    const int p = d & 0xFF;
+    const bool t1 = ((d >> 8) & 0xFF) == 0xFF;
+    const int q = t1 ? 0 : (int)((d >> 8) & 0xFF);
+    const uint32_t rk = rotk[a * K + p];
+    const uint32_t key = rk >> 2;
+    const int sh = 2 * (K - 2 - q);
+    const uint32_t lq = (key >> sh) & 3u;
+    const uint32_t nl = (lq + 1u + (d >> 16)) & 3u;
+    const uint32_t key2 = key ^ ((lq ^ nl) << sh);
+    gidx = (uint32_t)p * copy_groups + chunk_groups + (t1 ? key : key2);
+    const uint32_t wa = (valid && t1 && p == 0) ? (uint32_t)w0 : 0u;
+    const uint32_t wb = valid ? (uint32_t)(t1 ? w1 : w2) : 0u;
+    meta = (rk & 3u) | (wa << 8) | (wb << 16);
+  };
+  auto load = [&](uint32_t gidx, uint4(&b)[CH]) {
+    const uint4 *sp = slots + (size_t)gidx * 8 + gl;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) b[j] = sp[2 * j];
+  };
+  auto csr_tail = [&](uint32_t gidx, uint32_t t0, uint32_t meta) {
+    const uint32_t *ob = off + (size_t)gidx * 4;
+    const uint32_t o0 = ob[0], o4 = ob[4];
+    const uint32_t up = meta & 3u;
+    const uint32_t lo = ob[up], hi = ob[up + 1];
+    const int wa = (int)((meta >> 8) & 0xFFu), wb = (int)(meta >> 16);
+    for (uint32_t e = o0 + t0 + (uint32_t)gl; e < o4; e += G) {
+      const int w = (e - lo < hi - lo) ? wa : wb;
+      if (w) atomicAdd(&acc[ent[e]], w);
+    }
+  };
+  auto process = [&](const uint4(&b)[CH], uint32_t gidx, uint32_t meta) {
+    // header = halfwords 0..3 of piece 0, held by lane gl == 0
+    const int src = lane & ~(G - 1);
+    const uint32_t h0 = (uint32_t)__shfl((int)b[0].x, src, 64);
+    const uint32_t h1 = (uint32_t)__shfl((int)b[0].y, src, 64);
+    const uint32_t e1 = h0 & 0xFFFFu, e2 = h0 >> 16, e3 = h1 & 0xFFFFu, tot = h1 >> 16;
+    const uint32_t up = meta & 3u;
+    const int wa = (int)((meta >> 8) & 0xFFu), wb = (int)(meta >> 16);
+    const uint32_t lo = up == 0 ? 0u : up == 1 ? e1 : up == 2 ? e2 : e3;
+    const uint32_t hi = up == 0 ? e1 : up == 1 ? e2 : up == 2 ? e3 : tot;
+    const bool big = tot == 0xFFFFu;
+    const uint32_t lim = (big || wb == 0) ? 0u : min(tot, (uint32_t)KMG_SLOT_INLINE);
+    const uint32_t span = hi - lo;
+    // entry index of halfword v of this lane's piece in step j: 16j + 8gl + v - 4
+    const uint32_t lo_l = lo + 4u - 8u * (uint32_t)gl;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (j > 0 && !__any((int)lim > 16 * j - 4)) break;
+      const uint32_t wd[4] = {b[j].x, b[j].y, b[j].z, b[j].w};
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const uint32_t col = (wd[v >> 1] >> ((v & 1) * 16)) & 0xFFFFu;
+        const uint32_t rel = (uint32_t)(16 * j + v) - lo_l;  // = t - lo
+        if constexpr (SENT) {
+          const int w = rel < span ? wa : wb;
+          if (j == 0 && v < 4) {
+            if (gl != 0 && w) atomicAdd(&acc[col], w);
+          } else {
+            atomicAdd(&acc[col], w);
+          }
+        } else {
+          // active: a valid inline entry outside the query letter's bin (weight wb); the
+          // in-bin entries (weight wa: Hamming 0, copy 0 only) are added below
+          const int t = 16 * j + 8 * gl + v - 4;
+          const uint32_t ad = (v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]);
+          const bool act = t >= 0 && (uint32_t)t < lim && rel >= span && ad >= thr4;
+          if constexpr (DUMMY) {  // no exec-mask change: independent slots interleave
+            __hip_atomic_fetch_add(
+                (__attribute__((address_space(3))) int32_t *)(uintptr_t)(act ? ad : dummy4), wb,
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else if (act) {
+            __hip_atomic_fetch_add((__attribute__((address_space(3))) int32_t *)(uintptr_t)ad, wb,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+      }
+    }
+    if constexpr (!SENT) {
+      if (wa && !big) {  // in-bin inline entries [lo, min(hi, lim)) with weight wa, from the CSR
+        const uint32_t o0 = off[(size_t)gidx * 4];
+        const uint32_t e1x = o0 + min(hi, lim);
+        for (uint32_t e = o0 + lo + (uint32_t)gl; e < e1x; e += G) atomicAdd(&acc[ent[e]], wa);
+      }
+    }
+    if (big || tot > (uint32_t)KMG_SLOT_INLINE)
+      csr_tail(gidx, big ? 0u : (uint32_t)KMG_SLOT_INLINE, meta);
+  };
+
+  uint4 buf[D][CH];
+  uint32_t gid[D], met[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    describe(grp + r * ngrp, gid[r], met[r]);
+    load(gid[r], buf[r]);
+  }
+  for (int L = grp; L < total; L += D * ngrp) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      if (L + r * ngrp < total) process(buf[r], gid[r], met[r]);
+      describe(L + (r + D) * ngrp, gid[r], met[r]);
+      load(gid[r], buf[r]);
+    }
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = (int)(jlo & ~(int64_t)3) + threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
 // ------------------------------------------------------------------ Hamming forms
 __device__ __forceinline__ int ham2bit(uint32_t a, uint32_t b, uint32_t mask55) {
   const uint32_t x = a ^ b;
@@ -1527,7 +1754,7 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
 hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
                                        const uint4 *slots, const uint32_t *off,
                                        const uint16_t *ent, int64_t row0, int64_t row1, int w0,
-                                       int w1, int w2, const OutSpec &o, hipStream_t s) {
+                                       int w1, int w2, const OutSpec &o, int tri, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (g.k < 8 || g.k > 12 || !g.rot) return hipErrorNotSupported;
@@ -1539,7 +1766,28 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
   const int threads = env_int("KMG_MM_THREADS", 1024) >= 1024 ? 1024 : 512;
   const int G7 = env_int("KMG_MM_G", 2);
   const int D7 = env_int("KMG_MM_D", 2);
+  // 0: v7, 1: v8 tested, 2: v8 sentinel slots, 3: v8 per-lane dummy
+  const int V8 = env_int("KMG_MM_SLOTV", 1);
   bool launched = false;
+  // v8 is built for two lanes per list and a 2- or 3-deep ring; other (G, D) choices
+  // select the v7 instances below
+  if (V8 >= 1 && V8 <= 3 && G7 == 2 && (D7 == 2 || D7 == 3)) {
+    const size_t lds8 = lds + (V8 == 2 ? 1024 * 4 : V8 == 3 ? 64 * 4 : 0);
+    const int porder = env_int("KMG_MM_PORDER", 1);
+#define KMG_MM8(KK, DD, SS)                                                                      \
+  if (g.k == KK && D7 == DD && V8 - 1 == SS) {                                                   \
+    hipLaunchKernelGGL((gram_mm1t_kernel<KK, DD, SS>), grid, dim3(threads), lds8, s, g, codes,   \
+                       ldc, slots, off, ent, row0, rows, w0, w1, w2, o, tri, porder);            \
+    launched = true;                                                                             \
+  }
+#define KMG_MM8K(KK)                                                                             \
+  KMG_MM8(KK, 2, 0) KMG_MM8(KK, 2, 1) KMG_MM8(KK, 2, 2) KMG_MM8(KK, 3, 0) KMG_MM8(KK, 3, 1)        \
+  KMG_MM8(KK, 3, 2)
+    KMG_MM8K(8) KMG_MM8K(9) KMG_MM8K(10) KMG_MM8K(11) KMG_MM8K(12)
+#undef KMG_MM8K
+#undef KMG_MM8
+    return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
+  }
 #define KMG_MM7(KK, GG, DD)                                                                      \
   if (g.k == KK && G7 == GG && D7 == DD) {                                                       \
     hipLaunchKernelGGL((gram_mm1s_kernel<KK, GG, DD>), grid, dim3(threads), lds, s, g, codes,    \
@@ -1553,6 +1801,48 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
 #undef KMG_MM7K
 #undef KMG_MM7
   return launched ? hipGetLastError() : hipErrorInvalidConfiguration;
+}
+
+// ------------------------------------------------------------------ mirror
+// K[j][i] = K[i][j] for j > i on a full row-major n x n K (the reference fills j > i and
+// mirrors, kernels.py:409-413): one 64 x 64 tile per workgroup, staged through LDS so both
+// the upper-tile read and the lower-tile write are row-contiguous.
+template <typename T>
+__global__ __launch_bounds__(256) void mirror_lower_kernel(T *__restrict__ K, int64_t ld, int64_t n,
+                                                           int64_t ntile) {
+  __shared__ T tile[64][65];
+  // blockIdx.x -> (bi >= bj) over the lower tile triangle
+  const int64_t b = blockIdx.x;
+  int64_t bi = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+  while (bi * (bi + 1) / 2 > b) --bi;
+  while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
+  const int64_t bj = b - bi * (bi + 1) / 2;
+  if (bi >= ntile) return;
+  const int64_t r0 = bj * 64, c0 = bi * 64;  // source: upper tile (rows of bj, cols of bi)
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t gr = r0 + r, gc = c0 + tx;
+    if (gr < n && gc < n) tile[r][tx] = K[gr * ld + gc];
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {  // destination row c0 + r, column r0 + tx
+    const int64_t gr = c0 + r, gc = r0 + tx;
+    if (gr < n && gc < n && gc < gr) K[gr * ld + gc] = tile[tx][r];
+  }
+}
+
+hipError_t launch_mirror_lower(void *K, int64_t ld, int64_t n, int32_t dtype, hipStream_t s) {
+  if (n <= 1) return hipSuccess;
+  const int64_t nt = (n + 63) / 64;
+  const int64_t blocks = nt * (nt + 1) / 2;
+  if (blocks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (dtype == KMG_F64)
+    hipLaunchKernelGGL(mirror_lower_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (double *)K, ld, n, nt);
+  else
+    hipLaunchKernelGGL(mirror_lower_kernel<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (uint32_t *)K, ld, n, nt);
+  return hipGetLastError();
 }
 
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,

@@ -332,9 +332,13 @@ __global__ __launch_bounds__(FINE_THREADS) void part_gather_kernel(
 // relative to the group start, group total), halfwords 4.. = the group's first
 // KMG_SLOT_INLINE entries in CSR order.  A group of >= 0xFFFF entries gets tot = 0xFFFF
 // and no inline entries (the kernel then reads it from the CSR).  8 threads per group,
-// each writes 16 bytes of the line.
+// each writes 16 bytes of the line.  Inline positions past the group's entries hold
+// sentinel columns sent_base + hash(group, position) in [sent_base, sent_base + 1024):
+// gram_mm1t_kernel<SENT> adds them into a scratch tail of its LDS accumulator instead of
+// testing every slot (spread over 1024 dwords so lanes of one wave rarely collide).
 __global__ __launch_bounds__(256) void slot_pack_kernel(int64_t ngroups, const uint32_t *__restrict__ off,
                                                         const uint16_t *__restrict__ ent,
+                                                        uint32_t sent_base,
                                                         uint4 *__restrict__ slots) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gi = t >> 3;
@@ -353,7 +357,8 @@ __global__ __launch_bounds__(256) void slot_pack_kernel(int64_t ngroups, const u
       v = big ? (h == 3 ? 0xFFFFu : 0u) : (h == 3 ? tot : ob[h + 1] - o0);
     } else {
       const uint32_t e = (uint32_t)(h - 4);
-      if (!big && e < tot) v = ent[o0 + e];
+      v = (!big && e < tot) ? (uint32_t)ent[o0 + e]
+                            : sent_base + (((uint32_t)gi * 97u + (uint32_t)h * 31u) & 1023u);
     }
     hw[s] = v;
   }
@@ -368,8 +373,10 @@ hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint1
   const int64_t ngroups = g.nbins() >> 2;
   if (ngroups == 0) return hipSuccess;
   const int64_t threads = ngroups * 8;
+  const uint32_t sent_base = (uint32_t)(((g.chunk + 3) >> 2) << 2);
+  if (sent_base + 1024u > 0xFFFFu) return hipErrorInvalidValue;
   hipLaunchKernelGGL(slot_pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                     ngroups, off, ent, slots);
+                     ngroups, off, ent, sent_base, slots);
   return hipGetLastError();
 }
 

@@ -99,7 +99,9 @@ hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, i
 hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
                                        const uint4 *slots, const uint32_t *off,
                                        const uint16_t *ent, int64_t row0, int64_t row1, int w0,
-                                       int w1, int w2, const OutSpec &o, hipStream_t s);
+                                       int w1, int w2, const OutSpec &o, int tri, hipStream_t s);
+// lower triangle := transpose of the upper triangle of a full n x n row-major K
+hipError_t launch_mirror_lower(void *K, int64_t ld, int64_t n, int32_t dtype, hipStream_t s);
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
 // max_dist: largest Hamming distance with a non-zero weight (min(2m, k) for mismatch)

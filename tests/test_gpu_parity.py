@@ -217,21 +217,42 @@ def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u, d):
         assert np.array_equal(raw.astype(np.int64), ref), (variant, g, v, u, d, chunk)
 
 
-@pytest.mark.parametrize("k", [8, 10, 11, 12])
-def test_mismatch_slots_k_range(ctx, monkeypatch, k):
-    """Slot layout (v7, the default for 8 <= k <= 12) at every compiled k."""
+# (KMG_MM_SLOTV, KMG_MM_D, KMG_MM_TRI): v7 slot kernel, v8 with tested slots (upper
+# triangle + mirror, or full rows), v8 with sentinel slots
+SLOT_KERNELS = [("0", "2", "1"), ("1", "2", "1"), ("1", "3", "1"), ("1", "2", "0"),
+                ("2", "2", "1"), ("2", "3", "1"), ("3", "2", "1"), ("3", "3", "0")]
+
+
+@pytest.mark.parametrize("slotv,d,tri", SLOT_KERNELS)
+@pytest.mark.parametrize("k", [8, 9, 10, 11, 12])
+def test_mismatch_slots_k_range(ctx, monkeypatch, k, slotv, d, tri):
+    """Slot layout (the default for 8 <= k <= 12) at every compiled k, every slot kernel."""
     monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
+    monkeypatch.setenv("KMG_MM_SLOTV", slotv)
+    monkeypatch.setenv("KMG_MM_D", d)
+    monkeypatch.setenv("KMG_MM_TRI", tri)
     codes, lens = E.synthetic(400, 101, seed=50 + k)
     raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
                    L.KMG_I32)
     assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1))
+    Kn = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
+                  L.KMG_F64)
+    assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
+    for chunk in (("64", "300") if k <= 9 else ()):  # several column chunks (slot tables
+        # grow with 4^(k-1) per chunk: k >= 10 stays single-chunk here)
+        monkeypatch.setenv("KMG_MM_CHUNK", chunk)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1)), chunk
 
 
-def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch):
+@pytest.mark.parametrize("slotv", ["0", "1", "2", "3"])
+def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch, slotv):
     """Slot groups longer than the 60 inline entries (CSR tail) and groups of >= 65535
     entries (16-bit header overflow, CSR only): 720 poly-A rows put 720 * 93 = 66960
     occurrences in the AAAAAAAAA groups of every copy."""
     monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
+    monkeypatch.setenv("KMG_MM_SLOTV", slotv)
     monkeypatch.setenv("KMG_MM_CHUNK", "20480")
     codes, lens = E.synthetic(760, 101, seed=61)
     codes[:720] = 0
