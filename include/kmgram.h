@@ -188,7 +188,8 @@ int kmg_stream(kmg_ctx *ctx, void **hip_stream);
 /* Per-stage device timings from HIP events recorded on the context stream around
  * every launch while timing is enabled (kmg_set_timing(ctx,1)); nothing is
  * synchronised until a stage time is read.  Stage names: "count", "scan",
- * "place", "fine", "diag", "gram", "extract", "features", "pack", "combine", "solve".
+ * "place", "fine", "diag", "gram", "extract", "features", "pack", "combine", "solve",
+ * "mirror" (inside "gram": the lower-triangle copy of a full mismatch K), "memset".
  *   kmg_stage_ms:    that stage in the last call (-1 if it did not run)
  *   kmg_stage_stats: sum and count over every call since kmg_timing_reset */
 int kmg_set_timing(kmg_ctx *ctx, int32_t enable);

@@ -82,12 +82,13 @@ struct DevBuf {
   }
 };
 
-const char *kStageNames[] = {"count",   "scan",     "place", "fine",   "diag",  "gram",
-                             "extract", "features", "pack",  "combine", "solve"};
-constexpr int kNumStages = 11;
+const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
+                             "gram",    "extract",  "pack",  "features", "combine",
+                             "solve",   "mirror",   "memset"};
+constexpr int kNumStages = 13;
 enum {
-  ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_FEATURES, ST_PACK,
-  ST_COMBINE, ST_SOLVE
+  ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
+  ST_COMBINE, ST_SOLVE, ST_MIRROR, ST_MEMSET  // "mirror" is nested inside "gram"
 };
 
 }  // namespace
@@ -502,13 +503,17 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                      c->ent.as<uint16_t>(), row0, row1, o, c->stream));
       } else {
         if (use_slots) {
-          // full K on one device: upper triangle + mirror (halves the LDS atomics)
-          const int tri = (row0 == 0 && row1 == n && n >= 256 && env_or("KMG_MM_TRI", 1)) ? 1 : 0;
+          // KMG_MM_TRI=1, full K on one device: upper triangle + mirror (halves the LDS
+          // atomics, but the mirror costs what the Gram kernel saves: off by default)
+          const int tri = (row0 == 0 && row1 == n && n >= 256 && env_or("KMG_MM_TRI", 0)) ? 1 : 0;
           KMG_HIP(launch_gram_mismatch1_slots(g, d_codes, ldc, c->slots.as<uint4>(),
                                               c->off.as<uint32_t>(), c->ent.as<uint16_t>(), row0,
                                               row1, (int)w[0], (int)w[1], (int)w[2], o, tri,
                                               c->stream));
-          if (tri) KMG_HIP(launch_mirror_lower(o.out, o.ld, n, o.dtype, c->stream));
+          if (tri) {
+            StageTimer tm(c, ST_MIRROR);
+            KMG_HIP(launch_mirror_lower(o.out, o.ld, n, o.dtype, c->stream));
+          }
         }
         else if (use_rot)
           KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
@@ -757,6 +762,7 @@ int kmg_d2h(kmg_ctx *c, void *dst, const void *src, size_t bytes) {
 int kmg_memset(kmg_ctx *c, void *dst, int value, size_t bytes) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   KMG_HIP(hipSetDevice(c->device));
+  StageTimer t(c, ST_MEMSET);
   KMG_HIP(hipMemsetAsync(dst, value, bytes, c->stream));
   return KMG_OK;
 }

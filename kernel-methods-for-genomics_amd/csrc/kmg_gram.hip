@@ -1810,24 +1810,52 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
 template <typename T>
 __global__ __launch_bounds__(256) void mirror_lower_kernel(T *__restrict__ K, int64_t ld, int64_t n,
                                                            int64_t ntile) {
-  __shared__ T tile[64][65];
-  // blockIdx.x -> (bi >= bj) over the lower tile triangle
-  const int64_t b = blockIdx.x;
+  // 16-byte row segments: V elements per lane, 64 / V lanes per tile row
+  constexpr int V = 16 / (int)sizeof(T), LPR = 64 / V, RPP = 256 / LPR;
+  __shared__ T tile[64][64 + 1];
+  const int64_t b = blockIdx.x;  // -> (bi >= bj) over the lower tile triangle
   int64_t bi = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
   while (bi * (bi + 1) / 2 > b) --bi;
   while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
   const int64_t bj = b - bi * (bi + 1) / 2;
   if (bi >= ntile) return;
   const int64_t r0 = bj * 64, c0 = bi * 64;  // source: upper tile (rows of bj, cols of bi)
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {
-    const int64_t gr = r0 + r, gc = c0 + tx;
-    if (gr < n && gc < n) tile[r][tx] = K[gr * ld + gc];
+  const int cx = (threadIdx.x % LPR) * V, ry = threadIdx.x / LPR;
+  const bool vec = ((ld * (int64_t)sizeof(T)) & 15) == 0 && (((uintptr_t)K) & 15) == 0;
+  for (int r = ry; r < 64; r += RPP) {
+    const int64_t gr = r0 + r, gc = c0 + cx;
+    if (gr >= n) break;
+    const T *src = K + gr * ld + gc;
+    if (vec && gc + V <= n) {
+      const uint4 w = *(const uint4 *)src;
+      T v[V];
+      __builtin_memcpy(v, &w, 16);
+#pragma unroll
+      for (int q = 0; q < V; ++q) tile[r][cx + q] = v[q];
+    } else {
+      for (int q = 0; q < V; ++q)
+        if (gc + q < n) tile[r][cx + q] = src[q];
+    }
   }
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) {  // destination row c0 + r, column r0 + tx
-    const int64_t gr = c0 + r, gc = r0 + tx;
-    if (gr < n && gc < n && gc < gr) K[gr * ld + gc] = tile[tx][r];
+  for (int r = ry; r < 64; r += RPP) {  // destination row c0 + r, columns r0 + cx ..
+    const int64_t gr = c0 + r, gc = r0 + cx;
+    if (gr >= n) break;
+    T *dst = K + gr * ld + gc;
+    T v[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = tile[cx + q][r];
+    if (vec && gc + V <= gr && gc + V <= n) {  // whole segment strictly below the diagonal
+      uint4 w;
+      __builtin_memcpy(&w, v, 16);
+      __builtin_nontemporal_store(w.x, (uint32_t *)dst);
+      __builtin_nontemporal_store(w.y, (uint32_t *)dst + 1);
+      __builtin_nontemporal_store(w.z, (uint32_t *)dst + 2);
+      __builtin_nontemporal_store(w.w, (uint32_t *)dst + 3);
+    } else {
+      for (int q = 0; q < V; ++q)
+        if (gc + q < gr && gc + q < n) dst[q] = v[q];
+    }
   }
 }
 

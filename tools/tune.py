@@ -82,7 +82,7 @@ def main():
         wall = (time.perf_counter() - t0) / args.reps * 1e3
         ctx.set_timing(False)
         stages = {}
-        for s in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram"):
+        for s in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram", "mirror"):
             tot, cnt = ctx.stage_stats(s)
             if cnt:
                 stages[s] = round(tot / cnt * 1e3, 1)
