@@ -59,9 +59,13 @@ enum {
 /* output element types */
 enum { KMG_I32 = 1, KMG_F32 = 2, KMG_F64 = 3 };
 
-/* LA modes */
+/* semantics modes (kmg_params.la_mode; LA and GP) */
 enum { KMG_LA_REFERENCE = 0 /* bit-for-bit the reference: all zeros (kernels.py:238,262) */,
        KMG_LA_INTENDED = 1  /* aliasing fixed, report §3.5 recurrence; parity unpinned */ };
+enum { KMG_MODE_REFERENCE = 0 /* the reference's behaviour (GP: k=1,g=0 only) */,
+       KMG_MODE_INTENDED = 1  /* GP: binary (k-g)-mer presence over the gapped subsequences
+                                 of every 101-window k-mer, normalised (kernels.py:420-455 as
+                                 report §3.7 describes it); parity unpinned */ };
 
 #define KMG_MAX_COEF 64
 
@@ -75,7 +79,7 @@ typedef struct kmg_params {
   int32_t window;    /* MM/GP: fixed window the reference hard-codes (101, kernels.py:171,430) */
   int32_t normalize; /* 1: fused normalize_K epilogue (kernels.py:398-415) */
   int32_t smith;     /* LA: 1 = Smith_Waterman max form */
-  int32_t la_mode;   /* KMG_LA_REFERENCE / KMG_LA_INTENDED */
+  int32_t la_mode;   /* LA: KMG_LA_REFERENCE / KMG_LA_INTENDED; GP: KMG_MODE_* */
   int32_t reserved[6];
   double lambda;     /* SS lambda */
   double lambda2;    /* SS lambda**2 exactly as the host language computes it */

@@ -381,6 +381,49 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
   return KMG_OK;
 }
 
+// gappy (k, g), intended semantics (kernels.py:420-455 as the report describes it): binary
+// presence features over the (k-g)-mers, K = F F^T on the int8 MFMA path, normalize_K fused
+int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_codes,
+                        int64_t n, int64_t ldc, int64_t row0, int64_t row1, OutSpec o,
+                        bool normalize) {
+  const int kk = k - g;
+  const int dp = (int)std::max<int64_t>(128, pow4(kk));
+  std::vector<uint32_t> combos;  // kept positions of every C(k, kk) combination, 4 bits each
+  for (uint32_t sel = 0; sel < (1u << k); ++sel) {
+    if (__builtin_popcount(sel) != kk) continue;
+    uint32_t cm = 0;
+    int q = 0;
+    for (int pos = 0; pos < k; ++pos)
+      if (sel >> pos & 1u) cm |= (uint32_t)pos << (4 * q++);
+    combos.push_back(cm);
+  }
+  KMG_TRY(c->masks.ensure(sizeof(uint32_t) * combos.size()));
+  KMG_HIP(hipMemcpyAsync(c->masks.p, combos.data(), sizeof(uint32_t) * combos.size(),
+                         hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));  // pageable source
+  c->masks_k = -1;                           // the neighbour-mask cache no longer holds masks
+  const int64_t rows_alloc = ((n + 127) & ~127LL) + 128;
+  KMG_TRY(c->feat.ensure((size_t)rows_alloc * dp));
+  KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+  KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
+  {
+    StageTimer t(c, ST_FEATURES);
+    KMG_HIP(hipMemsetAsync(c->feat.as<int8_t>() + n * (int64_t)dp, 0,
+                           (size_t)(rows_alloc - n) * dp, c->stream));
+    KMG_HIP(launch_gappy_features(d_codes, ldc, n, k, kk, window, dp, c->masks.as<uint32_t>(),
+                                  (int)combos.size(), c->feat.as<int8_t>(),
+                                  c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+  }
+  if (normalize) {
+    o.normalize = 1;
+    o.diagv = c->diagv.as<double>();
+    o.dsq = c->dsq.as<double>();
+  }
+  StageTimer t(c, ST_GRAM);
+  KMG_HIP(launch_gram_dense(c->feat.as<int8_t>(), dp, n, row0, row1, o, c->stream));
+  return KMG_OK;
+}
+
 // ----------------------------------------------------------------- dispatch
 int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
                 int maxlen, int64_t n, int64_t ldc, int64_t row0, int64_t row1, int32_t dt,
@@ -571,6 +614,17 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       return KMG_OK;
     }
     case KMG_GAPPY: {
+      if (p->la_mode == KMG_MODE_INTENDED) {
+        const int W = p->window > 0 ? p->window : 101;
+        if (p->k < 1 || p->k > 15 || p->g < 0 || p->g >= p->k || p->k - p->g > 8)
+          return fail(KMG_EUNSUPPORTED, "intended gappy: need 1 <= k <= 15, 0 <= g < k, k-g <= 8");
+        if (n > 0 && ldc < W)  // windows read x[0 : W); padding codes (>= 4) are skipped
+          return fail(KMG_EINVAL, "intended gappy: code rows (%lld) shorter than the window %d",
+                      (long long)ldc, W);
+        if (dt == KMG_I32 && p->normalize) return fail(KMG_EINVAL, "normalised GP is float64");
+        return gram_gappy_intended(c, p->k, p->g, W, d_codes, n, ldc, row0, row1, o,
+                                   p->normalize != 0);
+      }
       if (!(p->k == 1 && p->g == 0))
         return fail(KMG_EUNSUPPORTED, "gappy kernel defined only for k=1, g=0");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "GP produces float64 values");

@@ -234,6 +234,68 @@ hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int6
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ gappy features
+// Gappy (k, g) with the semantics get_gappy_K intends (kernels.py:420-455, report §3.7;
+// the reference itself raises for every (k, g) but (1, 0)): F[i][b] = 1 if the (k-g)-mer b
+// occurs as an order-preserving subsequence of k-g of the k positions of some window
+// x[a : a+k], a < window - k + 1 (the reference's range(101 - k + 1)).  Presence, not
+// count (``b in gap_set``).  combos[t] = the kept positions of combination t, 4 bits each
+// (lowest nibble first, ascending).  One workgroup per sequence, byte flags in LDS.
+__global__ __launch_bounds__(256) void gappy_feat_kernel(
+    const uint8_t *__restrict__ codes, int64_t ldc, int k, int kk, int window, int dp,
+    const uint32_t *__restrict__ combos, int ncomb, int8_t *__restrict__ F,
+    double *__restrict__ diagv, double *__restrict__ dsq) {
+  extern __shared__ __align__(16) uint32_t flags[];  // dp / 4 words
+  __shared__ int64_t red[4];
+  const int64_t i = blockIdx.x;
+  const int words = dp >> 2;
+  for (int w = threadIdx.x; w < words; w += blockDim.x) flags[w] = 0;
+  __syncthreads();
+  const int P = window - k + 1;
+  const uint8_t *rs = codes + i * ldc;
+  const int items = P > 0 ? P * ncomb : 0;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int a = it / ncomb;
+    const uint32_t cm = combos[it - a * ncomb];
+    uint32_t c = 0, bad = 0;
+    for (int q = 0; q < kk; ++q) {
+      const uint32_t v = rs[a + ((cm >> (4 * q)) & 15u)];
+      bad |= v & ~3u;
+      c = (c << 2) | (v & 3u);
+    }
+    if (!bad) atomicOr(&flags[c >> 2], 1u << ((c & 3) << 3));
+  }
+  __syncthreads();
+  int64_t sq = 0;
+  uint4 *dst = (uint4 *)(F + i * (int64_t)dp);
+  for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) {
+    const uint4 v = ((const uint4 *)flags)[w];
+    sq += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // bytes are 0 or 1
+    dst[w] = v;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sq += __shfl_down(sq, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += red[w];
+    const double d = (double)tot;
+    diagv[i] = d;
+    dsq[i] = sqrt(d);
+  }
+}
+
+hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, int k, int kk,
+                                 int window, int dp, const uint32_t *combos, int ncomb, int8_t *F,
+                                 double *diagv, double *dsq, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if ((dp & 127) || dp > 65536 || kk < 1 || kk > 8 || k > 15) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gappy_feat_kernel, dim3((unsigned)n), dim3(256), (size_t)dp, s, codes, ldc, k,
+                     kk, window, dp, combos, ncomb, F, diagv, dsq);
+  return hipGetLastError();
+}
+
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
                              const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;

@@ -126,6 +126,10 @@ hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int 
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);
 
+// gappy (k, g), intended semantics: binary (k-g)-mer presence features (kmg_dense.hip)
+hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, int k, int kk,
+                                 int window, int dp, const uint32_t *combos, int ncomb, int8_t *F,
+                                 double *diagv, double *dsq, hipStream_t s);
 // dense count-vector formulation (kmg_dense.hip): int8 F [rows >= n + 128][dp], K = F F^T
 hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t n,
                                  int k, int window, int dp, const uint32_t *masks, int nmask,

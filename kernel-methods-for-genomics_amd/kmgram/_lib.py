@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "libkmgram.so")
 KMG_SPECTRUM, KMG_MISMATCH, KMG_WD, KMG_WDS, KMG_SUBSTRING, KMG_LOCALALIGN, KMG_GAPPY = range(1, 8)
 KMG_I32, KMG_F32, KMG_F64 = 1, 2, 3
 KMG_LA_REFERENCE, KMG_LA_INTENDED = 0, 1
+KMG_MODE_REFERENCE, KMG_MODE_INTENDED = 0, 1  # GP semantics (include/kmgram.h)
 KMG_MAX_COEF = 64
 
 DTYPES = {KMG_I32: np.int32, KMG_F32: np.float32, KMG_F64: np.float64}

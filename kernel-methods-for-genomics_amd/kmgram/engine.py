@@ -104,11 +104,25 @@ class GramEngine:
                    la_e=e, la_d=d, la_beta=beta)
         return self._run(p, seqs)
 
-    def gappy(self, seqs, k, g):
-        """get_gappy_K (kernels.py:436-455)."""
+    def gappy(self, seqs, k, g, intended=False):
+        """get_gappy_K (kernels.py:436-455).
+
+        intended=True: the kernel the reference means to compute (report §3.7) instead of
+        its numpy-2 failure: phi_b(x) = [the (k-g)-mer b is an order-preserving
+        subsequence of some window x[a:a+k], a in range(101 - k + 1)], K = normalize_K of
+        the feature inner products (parity unpinned: the reference never produces it)."""
         seqs = list(seqs)
         self._require_acgt(seqs)
         k, g = int(k), int(g)
+        if intended:
+            if not (0 <= g < k):
+                raise ValueError("intended gappy kernel needs 0 <= g < k")
+            short = [len(s) for s in seqs if len(s) < 101]
+            if short:
+                raise ValueError(f"sequence of length {short[0]} shorter than the 101 window")
+            p = P.make(L.KMG_GAPPY, k=k, g=g, window=101, normalize=1,
+                       la_mode=L.KMG_MODE_INTENDED)
+            return self._run(p, seqs)
         if g > k:
             raise ValueError("r must be non-negative")  # itertools.combinations(..., k-g)
         if not (k == 1 and g == 0) and any(len(s) > 0 for s in seqs):

@@ -246,6 +246,34 @@ def gappy_k1g0(codes, lens, window=101):
     return normalize(Phi @ Phi.T)
 
 
+def gappy_intended_phi(codes, lens, k, g, window=101):
+    """Binary presence features of the intended gappy kernel (kernels.py:420-433 with the
+    betas over (k-g)-mers, as report §3.7 describes it): phi[i, b] = 1 if the (k-g)-mer b
+    (base-4 code, first letter most significant) is itertools.combinations(x[a:a+k], k-g)
+    of some window a in range(window - k + 1).  Parity unpinned (the reference raises)."""
+    from itertools import combinations
+    seqs = _codes_list(codes, lens)
+    kk = k - g
+    Phi = np.zeros((len(seqs), 4 ** kk), dtype=np.int64)
+    for i, s in enumerate(seqs):
+        seen = set()
+        for a in range(window - k + 1):
+            for sub in combinations(s[a:a + k], kk):
+                if len(sub) == kk and all(v < 4 for v in sub):
+                    c = 0
+                    for v in sub:
+                        c = c * 4 + int(v)
+                    seen.add(c)
+        Phi[i, sorted(seen)] = 1
+    return Phi
+
+
+def gappy_intended(codes, lens, k, g, window=101):
+    """get_gappy_K intended: normalize_K(Phi Phi^T) (kernels.py:449-454)."""
+    Phi = gappy_intended_phi(codes, lens, k, g, window)
+    return normalize((Phi @ Phi.T).astype(np.float64))
+
+
 def center(K):
     """center_K (kernels.py:387-395)."""
     n = K.shape[0]
