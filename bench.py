@@ -510,6 +510,9 @@ def main():
             "N": n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
             "hbm_frac_of_gram_kernel": (mm_bytes / (mm["gram_kernel_ms"] / 1e3)) / HBM_PEAK,
+            # the kernel's actual bound: one 128-byte slot line per posting
+            # list, (101-9+1) windows x (9 + 3*9*8/2) lists per row
+            "slot_line_GBps": 128.0 * mm_rows * 93 * 117 / (mm["gram_kernel_ms"] / 1e3) / 1e9,
             "spot_check": mm["spot_check"],
         }
     if cpu:
