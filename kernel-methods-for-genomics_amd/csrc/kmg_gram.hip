@@ -111,11 +111,14 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t
                                                       const int32_t *__restrict__ lens, int64_t ldc,
                                                       const uint32_t *__restrict__ off,
                                                       const uint16_t *__restrict__ ent,
-                                                      int64_t row0, OutSpec o) {
+                                                      int64_t row0, OutSpec o, int64_t nitems) {
   extern __shared__ __align__(16) uint32_t acc[];
-  const int64_t il = blockIdx.x / g.nchunks;
+  // nitems > gridDim.x: persistent blocks walk (row, chunk) items, so the row stores of
+  // one item drain while the block already accumulates the next
+  for (int64_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+  const int64_t il = item / g.nchunks;
   const int64_t i = row0 + il;
-  const int c = blockIdx.x - (int)il * g.nchunks;
+  const int c = (int)(item - il * g.nchunks);
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   const int words = PACK16 ? (((cw + 7) >> 3) << 2) : (((cw + 3) >> 2) << 2);
@@ -180,6 +183,8 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, const uint8_t
       v0 = w.x; v1 = w.y; v2 = w.z; v3 = w.w;
     }
     emit4<DT, NT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
+  }
+  __syncthreads();  // the accumulator is re-zeroed by the next item
   }
 }
 
@@ -1586,26 +1591,35 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const 
   const bool pack = g.pmax <= 255;
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   const size_t lds = (size_t)words * 4;
-  const dim3 grid((unsigned)(rows * g.nchunks));
+  const int64_t nitems = rows * g.nchunks;
+  // KMG_SP_PERSIST = p > 0: p waves of resident blocks (LDS-limited blocks per CU x 256
+  // CUs) loop over the items instead of one block per item
+  const int persist = env_int("KMG_SP_PERSIST", 0);
+  int64_t nblk = nitems;
+  if (persist > 0) {
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(8, (160 * 1024) / (int64_t)std::max<size_t>(lds, 1)));
+    nblk = std::min<int64_t>(nitems, 256 * per_cu * persist);
+  }
+  const dim3 grid((unsigned)nblk);
   const bool nt = env_int("KMG_SP_NT", 1) != 0;
   // lanes per posting list (KMG_SP_G; 1, 2 or 4): at k=8, N=20000 the kernel is bound by
   // its row stores, and G = 1 measured 291.6 us against 298.9 (G = 2) and 303.5 (G = 4)
   const int G = env_int("KMG_SP_G", 1);
   if (pack && nt && G == 2) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true, 2>), grid, dim3(256),
-                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o, nitems));
   } else if (pack && nt && G == 4) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true, 4>), grid, dim3(256),
-                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o, nitems));
   } else if (pack && nt) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true>), grid, dim3(256),
-                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o, nitems));
   } else if (pack) {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, false>), grid, dim3(256),
-                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o, nitems));
   } else {
     KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<false, D, false>), grid, dim3(256),
-                                                lds, s, g, codes, lens, ldc, off, ent, row0, o));
+                                                lds, s, g, codes, lens, ldc, off, ent, row0, o, nitems));
   }
   return hipGetLastError();
 }

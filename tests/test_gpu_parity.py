@@ -164,6 +164,19 @@ def test_spectrum_long_sequences_unpacked(ctx):
     assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 5))
 
 
+@pytest.mark.parametrize("persist", ["1", "2"])
+def test_spectrum_persistent_blocks(ctx, monkeypatch, persist):
+    """KMG_SP_PERSIST: resident blocks loop over (row, chunk) items (several per block)."""
+    monkeypatch.setenv("KMG_SP_PERSIST", persist)
+    codes, lens = E.synthetic(5000, 101, seed=31)
+    for chunk in ("24576", "1000"):
+        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
+        K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+        for r in (0, 2047, 2048, 4999):
+            assert np.array_equal(K[r].astype(np.int64), cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0]), (chunk, r)
+        assert np.array_equal(K, K.T)
+
+
 def test_mismatch_k9_n20000(ctx):
     """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows."""
     codes, lens = E.synthetic(20000, 101, seed=3)
