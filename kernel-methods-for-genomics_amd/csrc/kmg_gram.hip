@@ -1256,6 +1256,8 @@ __global__ __launch_bounds__(1024) void gram_mm1t_kernel(IndexGeom g,
   constexpr int G = 2, CH = 4;
   constexpr bool SENT = MODE == 1;  // sentinel slots
   constexpr bool DUMMY = MODE == 2;  // inactive lanes add into a per-lane dummy dword
+  constexpr bool HALF = MODE == 3;   // ring loads the first 64 B (header + 28 entries);
+                                     // the second 64 B only for groups of > 28 entries
   constexpr int NSUB = K + 3 * K * (K - 1) / 2;
   extern __shared__ __align__(16) uint32_t smem[];  // acc first: LDS offset 0 (col_addr_sdwa)
   const int c = (int)(blockIdx.x / rows);
@@ -1341,7 +1343,7 @@ __global__ __launch_bounds__(1024) void gram_mm1t_kernel(IndexGeom g,
   auto load = [&](uint32_t gidx, uint4(&b)[CH]) {
     const uint4 *sp = slots + (size_t)gidx * 8 + gl;
 #pragma unroll
-    for (int j = 0; j < CH; ++j) b[j] = sp[2 * j];
+    for (int j = 0; j < (HALF ? 2 : CH); ++j) b[j] = sp[2 * j];
   };
   auto csr_tail = [&](uint32_t gidx, uint32_t t0, uint32_t meta) {
     const uint32_t *ob = off + (size_t)gidx * 4;
@@ -1354,7 +1356,10 @@ __global__ __launch_bounds__(1024) void gram_mm1t_kernel(IndexGeom g,
       if (w) atomicAdd(&acc[ent[e]], w);
     }
   };
-  auto process = [&](const uint4(&b)[CH], uint32_t gidx, uint32_t meta) {
+  auto process = [&](const uint4(&bin)[CH], uint32_t gidx, uint32_t meta) {
+    uint4 b[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) b[j] = bin[j];
     // header = halfwords 0..3 of piece 0, held by lane gl == 0
     const int src = lane & ~(G - 1);
     const uint32_t h0 = (uint32_t)__shfl((int)b[0].x, src, 64);
@@ -1372,6 +1377,15 @@ __global__ __launch_bounds__(1024) void gram_mm1t_kernel(IndexGeom g,
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       if (j > 0 && !__any((int)lim > 16 * j - 4)) break;
+      if constexpr (HALF) {
+        if (j == 2) {  // second half of the line, loaded only by lists that reach it
+          const uint4 *sp = slots + (size_t)gidx * 8 + gl;
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          const bool need = (int)lim > 28;
+          b[2] = need ? sp[4] : z;
+          b[3] = need ? sp[6] : z;
+        }
+      }
       const uint32_t wd[4] = {b[j].x, b[j].y, b[j].z, b[j].w};
 #pragma unroll
       for (int v = 0; v < 8; ++v) {
@@ -1780,12 +1794,12 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
   const int threads = env_int("KMG_MM_THREADS", 1024) >= 1024 ? 1024 : 512;
   const int G7 = env_int("KMG_MM_G", 2);
   const int D7 = env_int("KMG_MM_D", 2);
-  // 0: v7, 1: v8 tested, 2: v8 sentinel slots, 3: v8 per-lane dummy
+  // 0: v7, 1: v8 tested, 2: v8 sentinel slots, 3: v8 per-lane dummy, 4: v8 half lines
   const int V8 = env_int("KMG_MM_SLOTV", 1);
   bool launched = false;
   // v8 is built for two lanes per list and a 2- or 3-deep ring; other (G, D) choices
   // select the v7 instances below
-  if (V8 >= 1 && V8 <= 3 && G7 == 2 && (D7 == 2 || D7 == 3)) {
+  if (V8 >= 1 && V8 <= 4 && G7 == 2 && (D7 == 2 || D7 == 3)) {
     const size_t lds8 = lds + (V8 == 2 ? 1024 * 4 : V8 == 3 ? 64 * 4 : 0);
     const int porder = env_int("KMG_MM_PORDER", 1);
 #define KMG_MM8(KK, DD, SS)                                                                      \
@@ -1796,7 +1810,7 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes,
   }
 #define KMG_MM8K(KK)                                                                             \
   KMG_MM8(KK, 2, 0) KMG_MM8(KK, 2, 1) KMG_MM8(KK, 2, 2) KMG_MM8(KK, 3, 0) KMG_MM8(KK, 3, 1)        \
-  KMG_MM8(KK, 3, 2)
+  KMG_MM8(KK, 3, 2) KMG_MM8(KK, 2, 3) KMG_MM8(KK, 3, 3)
     KMG_MM8K(8) KMG_MM8K(9) KMG_MM8K(10) KMG_MM8K(11) KMG_MM8K(12)
 #undef KMG_MM8K
 #undef KMG_MM8

@@ -233,7 +233,8 @@ def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u, d):
 # (KMG_MM_SLOTV, KMG_MM_D, KMG_MM_TRI): v7 slot kernel, v8 with tested slots (upper
 # triangle + mirror, or full rows), v8 with sentinel slots
 SLOT_KERNELS = [("0", "2", "1"), ("1", "2", "1"), ("1", "3", "1"), ("1", "2", "0"),
-                ("2", "2", "1"), ("2", "3", "1"), ("3", "2", "1"), ("3", "3", "0")]
+                ("2", "2", "1"), ("2", "3", "1"), ("3", "2", "1"), ("3", "3", "0"),
+                ("4", "2", "0"), ("4", "3", "1")]
 
 
 @pytest.mark.parametrize("slotv,d,tri", SLOT_KERNELS)
@@ -259,7 +260,7 @@ def test_mismatch_slots_k_range(ctx, monkeypatch, k, slotv, d, tri):
         assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1)), chunk
 
 
-@pytest.mark.parametrize("slotv", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("slotv", ["0", "1", "2", "3", "4"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch, slotv):
     """Slot groups longer than the 60 inline entries (CSR tail) and groups of >= 65535
     entries (16-bit header overflow, CSR only): 720 poly-A rows put 720 * 93 = 66960
