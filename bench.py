@@ -450,7 +450,10 @@ def main():
     dist = Dist()
     if dist.world != args.gpus and dist.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
-    ctx = L.Context(dist.local)
+    # KMG_BENCH_DEVICE: pin every rank to one device (rehearsing the multi-rank protocol
+    # on a one-GPU box); by default rank r uses device LOCAL_RANK
+    dev = os.environ.get("KMG_BENCH_DEVICE")
+    ctx = L.Context(int(dev) if dev is not None else dist.local)
     n = weak_scaled_n(args.n, dist.world)
 
     sp = run_workload(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
