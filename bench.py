@@ -446,6 +446,11 @@ def main():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the N=100000 / N=200000 slab / host-path lines (N=1 only)")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: everything else written to fd 1 (gloo's
+    # connection banner, runtime chatter) is sent to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     dist = Dist()
     if dist.world != args.gpus and dist.rank == 0:
@@ -530,7 +535,7 @@ def main():
     if extra:
         line["configs"] = extra
     if dist.rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     dist.close()
 
 
