@@ -1094,11 +1094,14 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs) {
   rocblas_int *ipiv = info + 4;
   rocblas_int hinfo = 0;
   KMG_TRY(build());
-  KMG_BLAS(rocsolver_dpotrf(c->blas, rocblas_fill_lower, ni, B, ni, info));
+  // B is symmetric: either triangle is the matrix (KMG_POTRF_UPPER selects rocSOLVER's
+  // upper-triangle variant)
+  const rocblas_fill fill = env_or("KMG_POTRF_UPPER", 0) ? rocblas_fill_upper : rocblas_fill_lower;
+  KMG_BLAS(rocsolver_dpotrf(c->blas, fill, ni, B, ni, info));
   KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
   if (hinfo == 0) {
-    KMG_BLAS(rocsolver_dpotrs(c->blas, rocblas_fill_lower, ni, 1, B, ni, rhs, ni));
+    KMG_BLAS(rocsolver_dpotrs(c->blas, fill, ni, 1, B, ni, rhs, ni));
     return KMG_OK;
   }
   KMG_TRY(build());  // not positive definite: rebuild and use LU, like inv()
