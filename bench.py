@@ -2,19 +2,24 @@
 """bench.py — Gram pairs/s of the MI355X string-kernel Gram engine.
 
 Workload (BASELINE.json configs[1]): spectrum k=8 Gram of N=20000 synthetic DNA
-sequences of length L=101 on one MI355X, int32 exact counts, device-resident
-(input codes already in HBM when the timed region starts).  A "step" is one full
-Gram build: k-mer extraction + posting-index build + Gram kernel over the rank's rows.
+sequences of length L=101, int32 exact counts, device-resident (input codes already in
+HBM when the timed region starts).  A "step" is one full-K build (SURVEY §8d t_build):
+2-bit packing + posting-index build + Gram kernel, and with G > 1 GPUs the RCCL
+all-gather that leaves the complete K on every GPU.
 
-Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`):
-one process per GPU, rows of K sharded across ranks with no data-path collective;
-weak scaling — N = 20000*sqrt(G) so every rank computes the same 20000^2 Gram pairs
-(rows N/G x N columns).  `value` = N^2 / max-over-ranks time.  `--allgather` adds the
-RCCL all-gather that assembles K on every GPU (reported separately).
+Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`): one
+process per GPU, the SAME N=20000 problem (strong scaling), rows dealt block-cyclically
+(kmg_gram_blocks): every rank builds the replicated index, computes its row blocks, and
+each round of G blocks is all-gathered in place over RCCL/xGMI on a second stream while
+the next round is computed.  `value` = N^2 / max-over-ranks step time including that
+all-gather; `collective_free` reports the same build without it.
 
-Also reported: the mismatch (k=9, m=1) Gram at the same N (BASELINE configs[2],
-float64 normalised, exact), per-stage device times from HIP events, the HBM roofline
-of the dominant kernel and the oracle timed on the host cores (cpu_baseline).
+Also reported: the mismatch (k=9, m=1) Gram at the same N (BASELINE configs[2], float64
+normalised), per-stage device times from HIP events, the HBM roofline of the dominant
+kernel, the oracle timed on the host cores (cpu_baseline), and (N=1) BASELINE configs[3]
+and [4], the drop-in host path, run.py's nine kernels at N=9000 and the downstream
+consumers.  At G > 1 the config[4] strong-scaling line (N=200000, raw int32 K gathered)
+is added.
 """
 import argparse
 import ctypes
@@ -32,11 +37,15 @@ import numpy as np  # noqa: E402
 from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
-from kmgram.shard import even_splits, weak_scaled_n  # noqa: E402
+from kmgram.shard import block_cyclic_ranges, default_block, rows_padded  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_IN_PEAK = 7 * 76.5e9  # per-GPU ingress: 7 xGMI links x ~76.5 GB/s per direction
+INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROARCH.md)
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
           "(k=9,m=1), 1/2/4/8 GPUs")
+STAGES = ("count", "scan", "place", "fine", "pack", "slots", "extract", "features", "diag",
+          "gram", "gather")
 
 
 class Dist:
@@ -44,11 +53,10 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")  # barrier / max on the host, no device traffic
+            dist.init_process_group("gloo")  # host barrier / max / uid broadcast only
             self.dist = dist
 
     def barrier(self):
@@ -63,6 +71,9 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def all_true(self, v):
+        return self.max(0.0 if v else 1.0) == 0.0
+
     def bcast_bytes(self, b):
         if self.world == 1:
             return b
@@ -75,93 +86,99 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def run_workload(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, allgather):
-    codes, lens = E.synthetic(n, 101, seed=seed)
-    ldc = codes.shape[1]
-    splits = even_splits(n, dist.world)
-    r0, r1 = splits[dist.rank], splits[dist.rank + 1]
-    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
-    d_codes = ctx.dmalloc(codes.nbytes)
-    d_lens = ctx.dmalloc(lens.nbytes)
-    ctx.h2d(d_codes, codes)
-    ctx.h2d(d_lens, lens)
-    full_rows = n if allgather else (r1 - r0)
-    d_out = ctx.dmalloc(full_rows * n * esz)
-    out_rows = ctypes.c_void_p(d_out.value + (r0 * n * esz if allgather else 0))
-
-    def step():
-        ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, out_rows, n)
-
-    for _ in range(warmup):
-        step()
-    ctx.synchronize()
-    ctx.set_timing(True)
-    ctx.timing_reset()
-    dist.barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    ctx.synchronize()
-    dist.barrier()
-    t1 = time.perf_counter()
-    ctx.set_timing(False)
-    wall = dist.max(t1 - t0)
-    stages = {}
-    for st in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram", "mirror"):
+def stage_means(ctx):
+    out = {}
+    for st in STAGES:
         tot, cnt = ctx.stage_stats(st)
         if cnt:
-            stages[st] = round(tot / cnt, 5)
-    res = {
-        "name": name, "n": n, "rows": r1 - r0, "wall_s": wall, "steps": steps,
-        "ms_per_step": wall / steps * 1e3, "pairs_per_s": n * n / (wall / steps),
-        "stages_ms": stages, "gram_kernel_ms": stages.get("gram"),
-    }
-    if allgather and dist.world > 1:
-        uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
-        ctx.comm_init(uid, dist.world, dist.rank)
-        ctx.allgather_rows(d_out, n, n, out_dtype, splits)  # warm
-        ctx.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-            ctx.allgather_rows(d_out, n, n, out_dtype, splits)
-        ctx.synchronize()
-        dist.barrier()
-        ag = dist.max(time.perf_counter() - t0)
-        res["with_allgather_ms_per_step"] = ag / steps * 1e3
-        res["with_allgather_pairs_per_s"] = n * n / (ag / steps)
-        ctx.comm_destroy()
-    # small parity spot-check of the measured output (first row of this rank vs oracle)
-    res["spot_check"] = spot_check(ctx, name, codes, lens, n, r0, out_rows, out_dtype, r1)
-    if name == "spectrum_k8":
-        res["write_ceiling_GBps"] = write_ceiling(ctx, out_rows, (r1 - r0) * n * esz)
-    ctx.dfree(d_out)
-    ctx.dfree(d_codes)
-    ctx.dfree(d_lens)
+            out[st] = round(tot / cnt, 5)
+            if st in ("gram", "gather"):
+                out[st + "_launches"] = cnt
+                out[st + "_total"] = round(tot, 5)
+    return out
+
+
+def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_row):
+    """Timed full-K builds of one workload: kmg_gram_blocks over this rank's block-cyclic
+    rows, all-gathered in place when G > 1.  Returns timings, stages and a spot check."""
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    world, rank = dist.world, dist.rank
+    block = n if world == 1 else default_block(n, world, n * esz)
+    npad = rows_padded(n, world, block)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(npad * n * esz)
+    gather = world > 1
+    res = {"name": name, "N": n, "block_rows": block, "rounds": npad // (world * block),
+           "rows_this_rank": sum(b - a for a, b in block_cyclic_ranges(n, world, rank, block))}
+    try:
+        def step(g):
+            ctx.gram_blocks(params, d_codes, d_lens, n, ldc, out_dtype, d_out, n, world, rank,
+                            block, g)
+
+        def timed(g, k):
+            for _ in range(warmup):
+                step(g)
+            ctx.synchronize()
+            ctx.set_timing(True)
+            ctx.timing_reset()
+            dist.barrier()
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(k):
+                step(g)
+            ctx.synchronize()
+            dist.barrier()
+            wall = dist.max(time.perf_counter() - t0)
+            ctx.set_timing(False)
+            return wall / k, stage_means(ctx)
+
+        t, stages = timed(gather, steps)
+        res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages})
+        if gather:
+            tcf, scf = timed(False, steps)
+            res["collective_free"] = {"ms_per_step": tcf * 1e3, "pairs_per_s": n * n / tcf,
+                                      "stages_ms": scf}
+            step(True)  # leave the gathered K for the spot check
+            ctx.synchronize()
+        # spot check: the first row of this rank's first block, plus (G > 1) a row computed
+        # by the next rank and received through the all-gather
+        rows = [block_cyclic_ranges(n, world, rank, block)[0][0]]
+        if gather:
+            rows.append(block_cyclic_ranges(n, world, (rank + 1) % world, block)[0][0])
+        ok = True
+        for r in rows:
+            row = np.empty(n, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * n * esz))
+            ok &= check_row(codes, lens, r, row)
+        res["spot_check_rows"] = rows
+        res["spot_check"] = dist.all_true(ok)
+        if name == "spectrum_k8" and world == 1:
+            res["write_ceiling_GBps"] = write_ceiling(ctx, d_out, n * n * esz)
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
     return res
 
 
-def spot_check(ctx, name, codes, lens, n, r0, d_rows, out_dtype, r1=None):
-    """Rows r0 and r1-1 of the measured output vs the oracle (the last row of a full K
-    lies in the mirrored lower triangle of the mismatch path)."""
-    try:
-        import cref
-    except Exception:
-        return None
-    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
-    ok = True
-    for r in sorted({r0, (r1 or r0 + 1) - 1}):
-        row = np.empty(n, dtype=L.DTYPES[out_dtype])
-        ctx.d2h(row, ctypes.c_void_p(d_rows.value + (r - r0) * n * esz))
-        if name == "spectrum_k8":
-            ref = cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0]
-            ok &= bool(np.array_equal(row.astype(np.int64), ref))
-        else:
-            ref = cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0]
-            ok &= bool(np.array_equal(row, ref))
-    return ok
+def check_spectrum(codes, lens, r, row):
+    import cref
+    return bool(np.array_equal(row.astype(np.int64), cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0]))
+
+
+def check_mismatch(codes, lens, r, row):
+    import cref
+    return bool(np.array_equal(row, cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0]))
+
+
+def check_mismatch_raw(codes, lens, r, row):
+    import cref
+    return bool(np.array_equal(row.astype(np.int64),
+                               cref.mismatch_raw(codes, lens, 9, 1, rows=(r, r + 1))[0]))
 
 
 def write_ceiling(ctx, d_out, nbytes, reps=10):
@@ -176,71 +193,67 @@ def write_ceiling(ctx, d_out, nbytes, reps=10):
     ctx.synchronize()
     tot, cnt = ctx.stage_stats("memset")
     ctx.set_timing(False)
-    if not cnt:
-        return None
-    return nbytes / (tot / cnt / 1e3) / 1e9
+    return nbytes / (tot / cnt / 1e3) / 1e9 if cnt else None
 
 
-def cpu_baseline(name, n, budget_s):
-    """The strongest CPU restatement of the reference we have, timed on this box's host
-    cores: scipy-sparse Phi Phi^T (oracle/cpu_ref.py spectrum_phi / mismatch_phi; the
-    reference's own get_phi_u / get_phi_km feature maps, kernels.py:12-25, 161-175, and its
-    np.dot pair loop, kernels.py:41-45, 211-215, as one sparse product).  Phi is built for
-    all N (timed); the product runs on a bounded row sample and the whole job is
-    extrapolated as t_phi + (N / rows) * t_rows.  Single-threaded (scipy's sparse product)."""
+# ----------------------------------------------------------------------- CPU baseline
+_F = _FT = None
+
+
+def _rows_product(ab):
+    a, b = ab
+    t0 = time.perf_counter()
+    (_F[a:b] @ _FT).toarray()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(name, n, budget_s, workers=None):
+    """The strongest CPU restatement of the reference we have, on this box's host cores:
+    scipy-sparse Phi Phi^T (oracle/cpu_ref.py spectrum_phi / mismatch_phi = the reference's
+    own feature maps get_phi_u / get_phi_km, kernels.py:12-25, 161-175, and its np.dot pair
+    loop, kernels.py:41-45, 211-215, as one sparse product).  Phi is built once for all N
+    (timed); the product runs over a bounded row sample split across `workers` forked
+    processes (one row block each, Phi shared copy-on-write), and the whole job is
+    extrapolated as t_phi + (N / rows) * t_rows.  Also returns the 1-process figure."""
+    import multiprocessing as mp
     import cpu_ref
+    global _F, _FT
+    workers = workers or min(16, os.cpu_count() or 1)
     seed = 2 if name == "spectrum_k8" else 3
     codes, lens = E.synthetic(n, 101, seed=seed)
     t0 = time.perf_counter()
-    F = (cpu_ref.spectrum_phi(codes, lens, 8) if name == "spectrum_k8"
-         else cpu_ref.mismatch_phi(codes, lens, 9, 1))
-    FT = F.T.tocsr()
+    _F = (cpu_ref.spectrum_phi(codes, lens, 8) if name == "spectrum_k8"
+          else cpu_ref.mismatch_phi(codes, lens, 9, 1))
+    _FT = _F.T.tocsr()
     t_phi = time.perf_counter() - t0
+    # 1 process: size the sample to ~budget/4
     r = 16
     while True:
-        t0 = time.perf_counter()
-        (F[:r] @ FT).toarray()
-        t = time.perf_counter() - t0
-        if t >= budget_s / 4 or r >= n:
+        t = _rows_product((0, r))
+        if t >= budget_s / 8 or r >= n:
             break
-        r = min(n, max(r * 2, int(r * (budget_s / 4) / max(t, 1e-3))))
-    rows = min(n, max(r, int(r * (budget_s / 2) / max(t, 1e-6))))
+        r = min(n, max(r * 2, int(r * (budget_s / 8) / max(t, 1e-3))))
+    rate1 = r / t  # rows per second, one process
+    # all workers: each takes a block sized for ~budget/2 of wall time
+    per = max(1, min(n // workers, int(rate1 * budget_s / 2)))
+    blocks = [(w * per, (w + 1) * per) for w in range(workers) if (w + 1) * per <= n]
+    ctx_mp = mp.get_context("fork")
     t0 = time.perf_counter()
-    (F[:rows] @ FT).toarray()
+    with ctx_mp.Pool(len(blocks)) as pool:
+        pool.map(_rows_product, blocks)
     t_rows = time.perf_counter() - t0
+    rows = per * len(blocks)
     t_job = t_phi + (n / rows) * t_rows
-    return {"value": n * n / t_job, "unit": "Gram pairs/s", "cores": 1, "kind": "port",
-            "sample": f"scipy-sparse Phi Phi^T (oracle/cpu_ref.py {'spectrum_phi' if name == 'spectrum_k8' else 'mismatch_phi'}): "
-                      f"Phi of all {n} sequences {t_phi:.2f} s + rows 0..{rows} x {n} in "
-                      f"{t_rows:.2f} s, whole job extrapolated to {t_job:.1f} s, 1 thread"}
-
-
-def cpu_baseline_openmp(name, n, budget_s):
-    """The C oracle (oracle/kmg_oracle.c, pairwise merge / Hamming, OpenMP) on a bounded row
-    sample of the same workload, on this box's host cores."""
-    import cref
-    cref.load()
-    cores = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
-    seed = 2 if name == "spectrum_k8" else 3
-    codes, lens = E.synthetic(n, 101, seed=seed)
-    fn = ((lambda r: cref.spectrum(codes, lens, 8, rows=(0, r))) if name == "spectrum_k8"
-          else (lambda r: cref.mismatch_raw(codes, lens, 9, 1, rows=(0, r))))
-    r = 8
-    while True:
-        t0 = time.perf_counter()
-        fn(r)
-        t = time.perf_counter() - t0
-        if t >= budget_s / 4 or r >= n:
-            break
-        r = min(n, max(r * 2, int(r * (budget_s / 4) / max(t, 1e-3))))
-    rows = min(n, max(r, int(r * budget_s / max(t, 1e-6))))
-    t0 = time.perf_counter()
-    fn(rows)
-    t = time.perf_counter() - t0
-    return {"value": rows * n / t, "unit": "Gram pairs/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/kmg_oracle.c {'kmo_spectrum' if name == 'spectrum_k8' else 'kmo_mismatch_raw'}"
-                      f" rows 0..{rows} x {n} columns ({rows * n} pairs) in {t:.2f} s, "
-                      f"{cores} OpenMP threads"}
+    t_job1 = t_phi + n / rate1
+    _F = _FT = None
+    label = "spectrum_phi" if name == "spectrum_k8" else "mismatch_phi"
+    return {"value": n * n / t_job, "unit": "Gram pairs/s", "cores": len(blocks), "kind": "port",
+            "sample": f"scipy-sparse Phi Phi^T (oracle/cpu_ref.py {label}): Phi of all {n} "
+                      f"sequences {t_phi:.2f} s (1 process) + rows 0..{rows} x {n} over "
+                      f"{len(blocks)} forked processes in {t_rows:.2f} s wall, whole job "
+                      f"extrapolated to {t_job:.1f} s",
+            "one_process": {"value": n * n / t_job1, "cores": 1,
+                            "sample": f"{r} rows in {t:.2f} s, whole job {t_job1:.1f} s"}}
 
 
 # reference kernels.py cost model (BASELINE.md, measured in the survey container: 8-core
@@ -251,8 +264,9 @@ def reference_model_s(kind, n):
     return 78.0 * n + 35e-6 * n * (n + 1) / 2 + 0.46e-6 * n * n / 2
 
 
+# ----------------------------------------------------------------------- N = 1 extras
 def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, oracle_row):
-    """One workload on rows [r0, r1) x all n columns, device-resident, this rank only."""
+    """One workload on rows [r0, r1) x all n columns, device-resident, one launch set."""
     codes, lens = E.synthetic(n, 101, seed=seed)
     ldc = codes.shape[1]
     esz = np.dtype(L.DTYPES[out_dtype]).itemsize
@@ -275,11 +289,7 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         ctx.synchronize()
         wall = time.perf_counter() - t0
         ctx.set_timing(False)
-        stages = {}
-        for st in ("count", "scan", "place", "fine", "pack", "extract", "features", "diag", "gram", "mirror"):
-            tot, cnt = ctx.stage_stats(st)
-            if cnt:
-                stages[st] = round(tot / cnt, 4)
+        stages = stage_means(ctx)
         ok = True
         for r in spot_rows:
             row = np.empty(n, dtype=L.DTYPES[out_dtype])
@@ -296,18 +306,20 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
             "spot_check_rows": list(spot_rows), "spot_check": ok}
 
 
-def extras(ctx, cpu_rates):
-    """BASELINE configs[3] and [4] and the drop-in host path, on this GPU (N=1 runs only)."""
+def extras(ctx, cpu_rates, steps4):
+    """BASELINE configs[3] and [4], the drop-in host path, run.py's kernels, downstream."""
     import cref
     out = {}
     sp = lambda c, l, r: cref.spectrum(c, l, 8, rows=(r, r + 1))[0]  # noqa: E731
+    mmr = lambda c, l, r: cref.mismatch_raw(c, l, 9, 1, rows=(r, r + 1))[0]  # noqa: E731
     mm = lambda c, l, r: cref.mismatch_rows(c, l, 9, 1, rows=(r, r + 1))[0]  # noqa: E731
     n4 = 100000
-    c4 = run_slab(ctx, P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n4, 4, 0, n4, 3, 1,
+    c4 = run_slab(ctx, P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n4, 4, 0, n4, steps4, 2,
                   (0, 54321, n4 - 1), sp)
     c4["workload"] = ("BASELINE configs[3]: spectrum k=8, N=100000 x L=101, full K on 1 GPU, "
-                      "int32 (40 GB), posting-list formulation (DESIGN.md: why not the fp32 GEMM)")
-    c4["gram_hbm_frac"] = (4.0 * n4 * n4 + 26.0 * n4) / (c4["stages_ms"]["gram"] / 1e3) / HBM_PEAK
+                      "int32 (40 GB), posting-list formulation (DESIGN.md §6: why not the "
+                      "count-vector fp32 GEMM)")
+    c4["gram_hbm_frac"] = (4.0 * n4 * n4 + 52.0 * n4) / (c4["stages_ms"]["gram"] / 1e3) / HBM_PEAK
     c4["reference_model_s"] = reference_model_s("spectrum_k8", n4)
     c4["speedup_vs_reference_model"] = c4["reference_model_s"] / (c4["ms_per_step"] / 1e3)
     if cpu_rates.get("spectrum_k8"):
@@ -318,10 +330,13 @@ def extras(ctx, cpu_rates):
                   5, 0, n5 // 8, 2, 1, (0, n5 // 8 - 1), mm)
     c5["workload"] = ("BASELINE configs[4] per-GPU share: mismatch (9,1), N=200000, rows "
                       "0..25000 (one of 8 ranks) x 200000 columns, float64 normalised (40 GB)")
-    c5["projected_8gpu_ms_per_step"] = c5["ms_per_step"]
-    c5["projected_8gpu_pairs_per_s"] = 8 * c5["pairs_per_s"]
     c5["reference_model_s"] = reference_model_s("mismatch_k9_m1", n5)
     out["config5_mismatch_k9_n200000_rank_slab"] = c5
+    c5f = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
+                   n5, 5, 0, n5, 1, 1, (0, n5 - 1), mmr)
+    c5f["workload"] = ("BASELINE configs[4] on ONE GPU: the full 200000 x 200000 raw int32 K "
+                       "(160 GB; the G=1 point of the config-5 strong-scaling line)")
+    out["config5_mismatch_k9_n200000_full_1gpu"] = c5f
     # drop-in host path: kmg_gram with a host float64 output (what kernels.get_spectrum_K
     # returns), PCIe D2H included; never `value`
     codes, lens = E.synthetic(20000, 101, seed=2)
@@ -334,7 +349,63 @@ def extras(ctx, cpu_rates):
         "ms": t * 1e3, "pairs_per_s": 20000 ** 2 / t,
         "note": "kmg_gram: H2D codes + device build + 3.2 GB float64 D2H into a numpy array"}
     del K
+    out["run_py_kernels_n9000"] = run_py_workload(ctx)
     out["downstream"] = downstream(ctx)
+    return out
+
+
+RUN_PY_METHODS = ["SP_k4", "SP_k5", "SP_k6", "MM_k4_m1", "MM_k5_m1", "MM_k6_m1", "WD_d4",
+                  "WD_d5", "WD_d10"]
+
+
+def run_py_workload(ctx, n=9000, reps=5):
+    """run.py's nine Gram matrices (reference run.py:6, built by utils.get_training_datas,
+    utils.py:149-153, over train+val+test = 9000 sequences), device-resident float64 K as
+    the drop-in returns it: per-kernel device time, its HBM fraction (8 B per entry) and,
+    for the int8-MFMA dense path, the MFMA fraction (2 * 4^k int ops per entry)."""
+    codes, lens = E.synthetic(n, 101, seed=9000)
+    ldc = codes.shape[1]
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(n * n * 8)
+    out = {}
+    try:
+        for m in RUN_PY_METHODS:
+            tok = m.split("_")
+            if tok[0] == "SP":
+                k = int(tok[1][1:])
+                params = P.make(L.KMG_SPECTRUM, k=k)
+            elif tok[0] == "MM":
+                k = int(tok[1][1:])
+                params = P.make(L.KMG_MISMATCH, k=k, m=int(tok[2][1:]), window=101, normalize=1)
+            else:
+                k = None
+                params = P.make(L.KMG_WD, d=int(tok[1][1:]))
+            ctx.gram_device(params, d_codes, d_lens, n, ldc, 0, n, L.KMG_F64, d_out, n)
+            ctx.synchronize()
+            ctx.set_timing(True)
+            ctx.timing_reset()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.gram_device(params, d_codes, d_lens, n, ldc, 0, n, L.KMG_F64, d_out, n)
+            ctx.synchronize()
+            wall = (time.perf_counter() - t0) / reps
+            ctx.set_timing(False)
+            st = stage_means(ctx)
+            g = st.get("gram")
+            rec = {"ms_per_build": wall * 1e3, "stages_ms": st,
+                   "gram_hbm_frac": 8.0 * n * n / (g / 1e3) / HBM_PEAK if g else None}
+            if st.get("features") is not None and k is not None:
+                dp = max(128, 4 ** k)
+                rec["dense_int8_dp"] = dp
+                rec["gram_mfma_frac"] = 2.0 * dp * n * n / (g / 1e3) / INT8_PEAK
+            out[m] = rec
+        out["total_ms"] = sum(v["ms_per_build"] for v in out.values())
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
     return out
 
 
@@ -344,8 +415,7 @@ FP64_PEAK = 78.6e12  # MI355X dense fp64 (spec sheet)
 def downstream(ctx):
     """§8f consumers of the Gram on device-resident float64 matrices at the production size
     (n = 9000 = train + val + test of the 3 TFs, utils.py:151-153): NLCK combination
-    (HBM-bound) and the KRR / KLR solves (fp64 factorisation)."""
-    import ctypes
+    (HBM-bound) and the KRR / KLR / C-SVM solves (fp64 factorisation)."""
     n, p, reps = 9000, 3, 5
     rng = np.random.default_rng(9)
     A = rng.standard_normal((n, 64))
@@ -391,7 +461,7 @@ def downstream(ctx):
             out[f"krr_solve_n{m_}"] = {
                 "ms": ms, "alg_flops": fl, "achieved_TFLOPs": fl / (ms / 1e3) / 1e12,
                 "fp64_frac": fl / (ms / 1e3) / FP64_PEAK, "source": "KRR.py:33",
-                "note": "Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I, fp64"}
+                "note": "symmetry check + Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I"}
         it = ctypes.c_int32(0)
         m_ = 2000
         ctx.timing_reset()
@@ -433,18 +503,33 @@ def load_traffic(workload):
     return best
 
 
+def gather_roofline(res, world, esz):
+    """All-gather over xGMI: bytes each rank receives per step / the gather's time on its
+    stream, against the per-GPU ingress peak."""
+    st = res.get("stages_ms", {})
+    if world <= 1 or "gather_total" not in st:
+        return None
+    n = res["N"]
+    npad = rows_padded(n, world, res["block_rows"])
+    recv = (world - 1) / world * npad * n * esz
+    launches_per_step = res["rounds"]
+    t = st["gather"] * launches_per_step / 1e3  # gather seconds per step
+    return {"bound": "xgmi", "bytes_received_per_step": recv, "gather_ms_per_step": t * 1e3,
+            "achieved_GBps": recv / t / 1e9, "peak_GBps": XGMI_IN_PEAK / 1e9,
+            "frac": recv / t / XGMI_IN_PEAK}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=20000, help="sequences at 1 GPU (weak-scaled)")
-    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--n", type=int, default=20000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mismatch", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the N=100000 / N=200000 slab / host-path lines (N=1 only)")
+                    help="skip the config 4 / 5, host-path, run.py and downstream lines")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: everything else written to fd 1 (gloo's
     # connection banner, runtime chatter) is sent to stderr
@@ -455,40 +540,48 @@ def main():
     dist = Dist()
     if dist.world != args.gpus and dist.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
-    # KMG_BENCH_DEVICE: pin every rank to one device (rehearsing the multi-rank protocol
-    # on a one-GPU box); by default rank r uses device LOCAL_RANK
     dev = os.environ.get("KMG_BENCH_DEVICE")
     ctx = L.Context(int(dev) if dev is not None else dist.local)
-    n = weak_scaled_n(args.n, dist.world)
+    if dist.world > 1:
+        uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
+        ctx.comm_init(uid, dist.world, dist.rank)
+    n = args.n
 
-    sp = run_workload(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
-                      args.steps, args.warmup, args.allgather)
+    sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
+                   args.steps, args.warmup, check_spectrum)
     mm = None
     if not args.no_mismatch:
-        mm = run_workload(ctx, dist, "mismatch_k9_m1",
-                          P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
-                          n, 3, max(3, args.steps // 4), 1, args.allgather)
+        mm = run_build(ctx, dist, "mismatch_k9_m1",
+                       P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
+                       n, 3, max(3, args.steps // 4), 1, check_mismatch)
+    c5 = None
+    if dist.world > 1 and not args.no_extra:
+        # config-5 strong scaling: the full 200000^2 raw int32 K (160 GB) on every GPU
+        c5 = run_build(ctx, dist, "mismatch_k9_m1_raw",
+                       P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
+                       200000, 5, 2, 1, check_mismatch_raw)
     cpu = {}
-    if dist.world == 1 and dist.rank == 0 and not args.no_cpu:
+    if dist.world == 1 and not args.no_cpu:
         cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
-        cpu["spectrum_k8_openmp"] = cpu_baseline_openmp("spectrum_k8", n, args.cpu_budget / 2)
         if mm:
             cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", n, args.cpu_budget / 2)
-            cpu["mismatch_k9_m1_openmp"] = cpu_baseline_openmp("mismatch_k9_m1", n,
-                                                               args.cpu_budget / 4)
     extra = None
     if dist.world == 1 and not args.no_extra:
-        extra = extras(ctx, {k: v["value"] for k, v in cpu.items()})
+        extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(10, args.steps // 2))
+    if dist.world > 1:
+        ctx.comm_destroy()
     ctx.close()
 
-    rows = sp["rows"]
-    alg_bytes = 4.0 * rows * n + 26.0 * n  # int32 K write + 2-bit packed input
-    kern_s = sp["gram_kernel_ms"] / 1e3
+    # roofline of the dominant kernel: gram_sp_kernel, one launch per round
+    st = sp["stages_ms"]
+    rows_per_launch = sp["rows_this_rank"] / max(1, st.get("gram_launches", 1) /
+                                                  max(1, args.steps))
+    alg_bytes = 4.0 * rows_per_launch * n + 52.0 * n  # int32 K write + packed input read
+    kern_s = st["gram"] / 1e3
     achieved = alg_bytes / kern_s
-    traffic = load_traffic("spectrum_k8")
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK, "traffic": traffic,
-            "kernel": "kmg::gram_sp_kernel<true,1,true,1>", "kernel_ms": sp["gram_kernel_ms"],
+            "frac": achieved / HBM_PEAK, "traffic": load_traffic("spectrum_k8"),
+            "kernel": "kmg::gram_sp_kernel<true,1,true>", "kernel_ms": st["gram"],
             "alg_bytes_per_launch": alg_bytes,
             "measured_write_ceiling_GBps": sp.get("write_ceiling_GBps"),
             "frac_of_measured_ceiling": (achieved / 1e9 / sp["write_ceiling_GBps"]
@@ -497,41 +590,48 @@ def main():
     line = {
         "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
         "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": sp["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": sp["ms_per_step"], "higher_is_better": True,
+        "scaling": "strong" if dist.world > 1 else "weak",
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(2)",
-        "config": {"workload": "spectrum k=8 Gram, N=20000 x L=101 per GPU-share "
-                               "(BASELINE configs[1]); weak-scaled N=20000*sqrt(G)",
-                   "N": n, "L": 101, "k": 8, "rows_per_rank": rows,
-                   "parallelism": f"row-shard x{dist.world}", "out_dtype": "int32",
-                   "full_k_build_ms": sp["ms_per_step"]},
+        "config": {"workload": "spectrum k=8 full-K build, N=20000 x L=101 (BASELINE "
+                               "configs[1]); G>1: same N, block-cyclic rows + in-place RCCL "
+                               "all-gather so every GPU ends with K",
+                   "N": n, "L": 101, "k": 8, "rows_this_rank": sp["rows_this_rank"],
+                   "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
+                   "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
         "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],
     }
-    if "with_allgather_ms_per_step" in sp:
-        line["allgather"] = {k: sp[k] for k in ("with_allgather_ms_per_step",
-                                                "with_allgather_pairs_per_s")}
+    if "collective_free" in sp:
+        line["collective_free"] = sp["collective_free"]
+        line["gather_roofline"] = gather_roofline(sp, dist.world, 4)
     if mm:
-        mm_rows = mm["rows"]
-        mm_bytes = 8.0 * mm_rows * n + 26.0 * n
+        mm_rows_launch = mm["rows_this_rank"] / max(1, mm["rounds"])
+        mm_bytes = 8.0 * mm_rows_launch * n + 52.0 * n
         line["secondary"] = {
-            "workload": "mismatch (k=9,m=1) Gram, float64 normalised (BASELINE configs[2])",
+            "workload": "mismatch (k=9,m=1) full-K build, float64 normalised (BASELINE configs[2])",
             "N": n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
-            "hbm_frac_of_gram_kernel": (mm_bytes / (mm["gram_kernel_ms"] / 1e3)) / HBM_PEAK,
-            # the kernel's actual bound: one 128-byte slot line per posting
-            # list, (101-9+1) windows x (9 + 3*9*8/2) lists per row
-            "slot_line_GBps": 128.0 * mm_rows * 93 * 117 / (mm["gram_kernel_ms"] / 1e3) / 1e9,
+            "hbm_frac_of_gram_kernel": mm_bytes / (mm["stages_ms"]["gram"] / 1e3) / HBM_PEAK,
             "spot_check": mm["spot_check"],
         }
+        if "collective_free" in mm:
+            line["secondary"]["collective_free"] = mm["collective_free"]
+    if c5:
+        line["config5_strong"] = {
+            "workload": "BASELINE configs[4]: mismatch (9,1), N=200000, raw int32 K (160 GB) "
+                        "assembled on every GPU (block-cyclic + in-place RCCL all-gather)",
+            **{k: c5[k] for k in ("ms_per_step", "pairs_per_s", "stages_ms", "block_rows",
+                                  "rounds", "spot_check", "collective_free")},
+            "gather_roofline": gather_roofline(c5, dist.world, 4)}
     if cpu:
-        line["cpu_baseline"] = cpu["spectrum_k8"]
-        line["cpu_baseline_alt"] = cpu["spectrum_k8_openmp"]
+        line["cpu_baseline"] = {k: v for k, v in cpu["spectrum_k8"].items() if k != "one_process"}
+        line["cpu_baseline_one_process"] = cpu["spectrum_k8"]["one_process"]
         line["reference_model"] = {
             "s": reference_model_s("spectrum_k8", n),
             "note": "reference kernels.py cost model (BASELINE.md), survey container 8-core Xeon"}
         if mm:
             line["secondary"]["cpu_baseline"] = cpu["mismatch_k9_m1"]
-            line["secondary"]["cpu_baseline_alt"] = cpu["mismatch_k9_m1_openmp"]
     if extra:
         line["configs"] = extra
     if dist.rank == 0:

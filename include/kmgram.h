@@ -180,6 +180,29 @@ int kmg_svm_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
                        const double *d_y, double C, double tol, int32_t maxiter,
                        double *d_alpha, int32_t *iters, double *objective);
 
+/*
+ * Multi-GPU full-K build ("the N x N tile space shards across the GPUs with a
+ * final RCCL all-gather over xGMI").  Rows are dealt block-cyclically: with `block` rows a
+ * block, round t holds rows [t*R, (t+1)*R), R = nranks * block, and rank r computes the
+ * block [t*R + r*block, +block) of every round (clipped to n).  The index is built once;
+ * the Gram kernel runs once per round.  gather = 1: as soon as a round's block is enqueued,
+ * the round is all-gathered IN PLACE (ncclAllGather(send = recv + rank*count), one
+ * contiguous R-row slab) on a second stream, overlapped with the next round's Gram kernel;
+ * when the call's work completes (context-stream order) every rank holds the full K.
+ * d_out: n_pad x ld_out elements, n_pad = kmg_rows_padded(n, nranks, block) (the padding
+ * rows of the last round travel but are never written by a kernel); gather = 0 writes only
+ * this rank's blocks and needs n rows.  gather = 1 with nranks > 1 needs kmg_comm_init with
+ * the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
+ * get_mismatch_K (kernels.py:41-45, 211-215) split over GPUs.
+ */
+int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block);
+int kmg_gram_blocks(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
+                    const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype, void *d_out,
+                    int64_t ld_out, int32_t nranks, int32_t rank, int64_t block, int32_t gather);
+
+/* Re-read the KMG_* tuning variables of the environment (read once at kmg_create). */
+int kmg_reload_tuning(kmg_ctx *ctx);
+
 /* device memory / stream helpers for device-resident callers */
 int kmg_dmalloc(kmg_ctx *ctx, void **ptr, size_t bytes);
 int kmg_dfree(kmg_ctx *ctx, void *ptr);
@@ -192,8 +215,9 @@ int kmg_stream(kmg_ctx *ctx, void **hip_stream);
 /* Per-stage device timings from HIP events recorded on the context stream around
  * every launch while timing is enabled (kmg_set_timing(ctx,1)); nothing is
  * synchronised until a stage time is read.  Stage names: "count", "scan",
- * "place", "fine", "diag", "gram", "extract", "features", "pack", "combine", "solve",
- * "mirror" (inside "gram": the lower-triangle copy of a full mismatch K), "memset".
+ * "place", "fine", "diag", "gram", "extract", "features", "pack" (2-bit packing of the
+ * input), "slots" (mismatch slot table), "combine", "solve", "memset", "gather" (the RCCL
+ * all-gathers of kmg_gram_blocks, timed on their own stream).
  *   kmg_stage_ms:    that stage in the last call (-1 if it did not run)
  *   kmg_stage_stats: sum and count over every call since kmg_timing_reset */
 int kmg_set_timing(kmg_ctx *ctx, int32_t enable);
@@ -204,7 +228,9 @@ int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *
 /* RCCL (one rank per process / GPU).  id is an opaque 128-byte ncclUniqueId. */
 int kmg_comm_unique_id(uint8_t id[128]);
 int kmg_comm_init(kmg_ctx *ctx, const uint8_t id[128], int32_t nranks, int32_t rank);
-/* Assemble the full n x n K on every rank: rank r owns rows [splits[r], splits[r+1]). */
+/* Assemble the full n x n K on every rank: rank r owns rows [splits[r], splits[r+1])
+ * (0 = splits[0] <= ... <= splits[nranks] = n, checked); one RCCL group of per-root
+ * broadcasts.  kmg_gram_blocks is the overlapped in-place ncclAllGather form. */
 int kmg_allgather_rows(kmg_ctx *ctx, void *d_K, int64_t n, int64_t ld, int32_t dtype,
                        const int64_t *splits);
 int kmg_comm_destroy(kmg_ctx *ctx);

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -82,14 +83,52 @@ struct DevBuf {
   }
 };
 
+// "pack" = 2-bit packing of the input, "slots" = slot layout of the mismatch index,
+// "gather" = the RCCL row all-gather (kmg_allgather_rows)
 const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
                              "gram",    "extract",  "pack",  "features", "combine",
-                             "solve",   "mirror",   "memset"};
-constexpr int kNumStages = 13;
+                             "solve",   "slots",    "memset", "gather"};
+constexpr int kNumStages = 14;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
-  ST_COMBINE, ST_SOLVE, ST_MIRROR, ST_MEMSET  // "mirror" is nested inside "gram"
+  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER
 };
+
+// Tuning knobs: read from the environment once per context (kmg_create) and again only on
+// kmg_reload_tuning, never per launch.
+struct Tuning {
+  int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
+  int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index
+  int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
+  int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
+  int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
+  int idx_v2 = 1;           // KMG_IDX_V2: index build without device-scope atomics
+  int idx_seqs = 80;        // KMG_IDX_SEQS: sequences per partition block
+  int idx_buckets = 0;      // KMG_IDX_BUCKETS: coarse buckets (0: 384 spectrum / 1024 mismatch)
+  int idx_threads = 1024;   // KMG_IDX_THREADS
+  int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
+  int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky
+};
+
+int env_or(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+void read_tuning(Tuning &t) {
+  const Tuning d;
+  t.sp_chunk = env_or("KMG_SP_CHUNK", d.sp_chunk);
+  t.mm_chunk = env_or("KMG_MM_CHUNK", d.mm_chunk);
+  t.algo = env_or("KMG_ALGO", d.algo);
+  t.dense_kmax_sp = env_or("KMG_DENSE_KMAX_SP", d.dense_kmax_sp);
+  t.dense_kmax_mm = env_or("KMG_DENSE_KMAX_MM", d.dense_kmax_mm);
+  t.idx_v2 = env_or("KMG_IDX_V2", d.idx_v2);
+  t.idx_seqs = env_or("KMG_IDX_SEQS", d.idx_seqs);
+  t.idx_buckets = env_or("KMG_IDX_BUCKETS", d.idx_buckets);
+  t.idx_threads = env_or("KMG_IDX_THREADS", d.idx_threads);
+  t.poison = env_or("KMG_POISON", d.poison);
+  t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
+}
 
 }  // namespace
 
@@ -101,6 +140,8 @@ struct kmg_ctx {
   DevBuf hcnt, hstart;            // index build v2: per-(bucket, block) counts / local starts
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
+  DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
+  Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
   rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
@@ -116,6 +157,8 @@ struct kmg_ctx {
   int64_t wtab_host[33] = {};
   bool wtab_valid = false;
   ncclComm_t comm = nullptr;
+  hipStream_t comm_stream = nullptr;  // RCCL all-gathers of kmg_gram_blocks
+  hipEvent_t ev_sync = nullptr;       // context stream <-> comm stream ordering
   int nranks = 1, rank = 0;
 };
 
@@ -186,38 +229,30 @@ int check_params(const kmg_params *p, int64_t n, int64_t ldc, int32_t dt) {
   return KMG_OK;
 }
 
-int env_or(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
-
 // ----------------------------------------------------------------- posting index
-int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
-                int64_t ldc) {
+int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
   // coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins: ~384 for the
   // spectrum index, ~1024 for the k-copy mismatch index (16.7M occurrences at N=20000,
   // where 288 buckets left the fine pass at 240 us and 576 halved it)
-  const int target_buckets = env_or("KMG_IDX_BUCKETS", g.copies > 1 ? 1024 : 384);
+  const int target_buckets = c->tune.idx_buckets > 0 ? c->tune.idx_buckets : (g.copies > 1 ? 1024 : 384);
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
-  g.seqs_per_block = std::max(1, env_or("KMG_IDX_SEQS", 80));
-  {
-    const int rowlen0 = g.window > 0 ? g.window : (int)ldc;
+  g.seqs_per_block = std::max(1, c->tune.idx_seqs);
+  {  // LDS: two bucket arrays + the staged packed records
     const int64_t budget = 150 * 1024 - 8 * (g.nbins() >> g.fine_bits) - 4096;
-    g.seqs_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(g.seqs_per_block, budget / (rowlen0 + 4)));
+    g.seqs_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(g.seqs_per_block, budget / (4 * pk.ldp)));
   }
-  g.part_threads = std::min(1024, std::max(64, env_or("KMG_IDX_THREADS", 1024)));
+  g.part_threads = std::min(1024, std::max(64, c->tune.idx_threads));
   const int64_t nb = g.nbins();
   const int64_t nbk = g.nbuckets();
   if (nbk > 16384) return fail(KMG_EUNSUPPORTED, "index too large (%lld bins)", (long long)nb);
-  const int rowlen = g.window > 0 ? g.window : (int)ldc;
-  if (rowlen > 4096) return fail(KMG_EUNSUPPORTED, "sequences longer than 4096");
+  if (pk.ldp * 4 > 8192) return fail(KMG_EUNSUPPORTED, "sequences longer than 8192");
   const int64_t items = g.n * g.pmax * g.copies;
   if ((double)items >= 4294967295.0)
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
   const int64_t nblk = (g.n + g.seqs_per_block - 1) / g.seqs_per_block;
   const int64_t cap = (int64_t)g.seqs_per_block * g.pmax * g.copies;
-  if (env_or("KMG_IDX_V2", 1) && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
+  if (c->tune.idx_v2 && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
       nblk * cap < ((int64_t)1 << 34)) {
     KMG_TRY(c->hcnt.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
     KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
@@ -226,7 +261,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
     KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 64)));  // + pad: clamped reads
     {
       StageTimer t(c, ST_PLACE);
-      KMG_HIP(launch_index_local(g, d_codes, d_lens, ldc, (int)nblk, (uint32_t)cap,
+      KMG_HIP(launch_index_local(g, pk, (int)nblk, (uint32_t)cap,
                                  c->hcnt.as<uint32_t>(), c->hstart.as<uint32_t>(),
                                  c->tmp.as<uint32_t>(), c->stream));
     }
@@ -255,11 +290,11 @@ int build_index(kmg_ctx *c, IndexGeom &g, const uint8_t *d_codes, const int32_t 
   c->index_dirty = true;
   {
     StageTimer t(c, ST_COUNT);
-    KMG_HIP(launch_index_count(g, d_codes, d_lens, ldc, c->bcount.as<uint32_t>(), c->stream));
+    KMG_HIP(launch_index_count(g, pk, c->bcount.as<uint32_t>(), c->stream));
   }
   {
     StageTimer t(c, ST_PLACE);
-    KMG_HIP(launch_index_place(g, d_codes, d_lens, ldc, c->bcount.as<uint32_t>(),
+    KMG_HIP(launch_index_place(g, pk, c->bcount.as<uint32_t>(),
                                c->bcursor.as<uint32_t>(), c->boff.as<uint32_t>(),
                                c->tmp.as<uint32_t>(), c->stream));
   }
@@ -298,8 +333,7 @@ int upload_wtab(kmg_ctx *c, const int64_t *w) {
   return KMG_OK;
 }
 
-int diag_hamming(kmg_ctx *c, const IndexGeom &g, const uint8_t *d_codes, const int32_t *d_lens,
-                 int64_t ldc) {
+int diag_hamming(kmg_ctx *c, const IndexGeom &g, const Packed &pk) {
   int max_dist = 0;  // weights are zero past this Hamming distance
   for (int d = 0; d <= 32; ++d)
     if (c->wtab_host[d] != 0) max_dist = d;
@@ -307,8 +341,8 @@ int diag_hamming(kmg_ctx *c, const IndexGeom &g, const uint8_t *d_codes, const i
   KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(g.n > 0 ? g.n : 1)));
   if (g.pmax > 4096) return fail(KMG_EUNSUPPORTED, "more than 4096 k-mers per sequence");
   StageTimer t(c, ST_DIAG);
-  KMG_HIP(launch_diag_hamming(g, d_codes, d_lens, ldc, c->wtab.as<int64_t>(), max_dist,
-                              c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+  KMG_HIP(launch_diag_hamming(g, pk, c->wtab.as<int64_t>(), max_dist, c->diagv.as<double>(),
+                              c->dsq.as<double>(), c->stream));
   return KMG_OK;
 }
 
@@ -353,10 +387,35 @@ int upload_masks(kmg_ctx *c, int k, int m) {
   return KMG_OK;
 }
 
+// Row ranges of one Gram call: every range [row0, row1) x all n columns is written at
+// `out` (row row0); the index / features / diagonal are built once per call.  `after(q)`
+// runs once range q's Gram launch is enqueued (the multi-GPU path hangs its all-gather of a
+// round there).
+struct RowRange {
+  int64_t row0, row1;
+  void *out;
+};
+using AfterRange = std::function<int(size_t)>;
+
+template <typename Launch>
+int each_range(kmg_ctx *c, const std::vector<RowRange> &ranges, const OutSpec &o,
+               const AfterRange &after, Launch &&launch) {
+  for (size_t q = 0; q < ranges.size(); ++q) {
+    OutSpec oq = o;
+    oq.out = ranges[q].out;
+    {
+      StageTimer t(c, ST_GRAM);
+      KMG_HIP(launch(ranges[q].row0, ranges[q].row1, oq));
+    }
+    if (after) KMG_TRY(after(q));
+  }
+  return KMG_OK;
+}
+
 // F = int8 count / neighbour-count rows, diagonal ||F_i||^2, then K = F F^T (MFMA)
 int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
-               const int32_t *d_lens, int64_t n, int64_t ldc, int64_t row0, int64_t row1,
-               OutSpec o, bool normalize) {
+               const int32_t *d_lens, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
+               OutSpec o, bool normalize, const AfterRange &after) {
   const int dp = (int)std::max<int64_t>(128, pow4(k));
   KMG_TRY(upload_masks(c, k, m));
   const int64_t rows_alloc = ((n + 127) & ~127LL) + 128;
@@ -376,16 +435,16 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
     o.diagv = c->diagv.as<double>();
     o.dsq = c->dsq.as<double>();
   }
-  StageTimer t(c, ST_GRAM);
-  KMG_HIP(launch_gram_dense(c->feat.as<int8_t>(), dp, n, row0, row1, o, c->stream));
-  return KMG_OK;
+  return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, oq, c->stream);
+  });
 }
 
 // gappy (k, g), intended semantics (kernels.py:420-455 as the report describes it): binary
 // presence features over the (k-g)-mers, K = F F^T on the int8 MFMA path, normalize_K fused
 int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_codes,
-                        int64_t n, int64_t ldc, int64_t row0, int64_t row1, OutSpec o,
-                        bool normalize) {
+                        int64_t n, int64_t ldc, const std::vector<RowRange> &ranges, OutSpec o,
+                        bool normalize, const AfterRange &after) {
   const int kk = k - g;
   const int dp = (int)std::max<int64_t>(128, pow4(kk));
   std::vector<uint32_t> combos;  // kept positions of every C(k, kk) combination, 4 bits each
@@ -419,23 +478,25 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
     o.diagv = c->diagv.as<double>();
     o.dsq = c->dsq.as<double>();
   }
-  StageTimer t(c, ST_GRAM);
-  KMG_HIP(launch_gram_dense(c->feat.as<int8_t>(), dp, n, row0, row1, o, c->stream));
-  return KMG_OK;
+  return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, oq, c->stream);
+  });
 }
 
 // ----------------------------------------------------------------- dispatch
 int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
-                int maxlen, int64_t n, int64_t ldc, int64_t row0, int64_t row1, int32_t dt,
-                void *d_out, int64_t ld) {
+                int maxlen, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
+                int32_t dt, int64_t ld, const AfterRange &after = nullptr) {
   c->last_call_first = (int)c->ev_log.size();
-  if (row0 < 0 || row1 > n || row0 > row1) return fail(KMG_EINVAL, "bad row range");
+  for (const RowRange &r : ranges)
+    if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
   if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
-  OutSpec o{d_out, ld, dt, 0, nullptr, nullptr};
-  const int64_t rows = row1 - row0;
-  if (env_or("KMG_POISON", 0) && rows > 0 && n > 0)  // testing: no stale output can pass
-    KMG_HIP(hipMemset2DAsync(d_out, (size_t)ld * dtype_size(dt), 0xA5, (size_t)n * dtype_size(dt),
-                             (size_t)rows, c->stream));
+  OutSpec o{nullptr, ld, dt, 0, nullptr, nullptr};
+  if (c->tune.poison && n > 0)  // testing: no stale output can pass
+    for (const RowRange &r : ranges)
+      if (r.row1 > r.row0)
+        KMG_HIP(hipMemset2DAsync(r.out, (size_t)ld * dtype_size(dt), 0xA5,
+                                 (size_t)n * dtype_size(dt), (size_t)(r.row1 - r.row0), c->stream));
   switch (p->kind) {
     case KMG_SPECTRUM:
     case KMG_MISMATCH: {
@@ -447,6 +508,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       g.k = k;
       g.n = n;
       g.window = mm ? (p->window > 0 ? p->window : 101) : 0;
+      // the mismatch window reads x[0 : window) of every row (kernels.py:171): rows narrower
+      // than the window would read into the next row
+      if (mm && n > 0 && ldc < g.window)
+        return fail(KMG_EINVAL, "mismatch: code rows (%lld) shorter than the window %d",
+                    (long long)ldc, g.window);
       const int L = mm ? g.window : maxlen;
       g.pmax = L - k + 1 > 0 ? L - k + 1 : 1;
       if (g.pmax > 4095) return fail(KMG_EUNSUPPORTED, "more than 4095 k-mers per sequence");
@@ -457,13 +523,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
-      const bool s1 = mm && p->m == 1 && k >= 2 && k <= 12;  // drop-one-letter index
-      const bool use_index = (exact && k <= 12) || s1;
-      // mismatch launch family: 7 = slot layout (k in [8,12]; v6 below that), 3..6 = rotated
-      // CSR variants, 2 = drop-one-letter CSR (see kmg_gram.hip)
-      const int mm_variant = env_or("KMG_MM_VARIANT", 7);
-      const bool use_rot = s1 && k >= 4 && mm_variant >= 3;
-      const bool use_slots = use_rot && mm_variant == 7 && k >= 8 && k <= 12;
+      const bool use_slots = mm && p->m == 1 && k >= 8 && k <= 12;  // drop-one-letter slots
+      const bool use_index = (exact && k <= 12) || use_slots;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
@@ -471,18 +532,27 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
       const int mm_eff = mm ? std::min(p->m, k) : 0;
       const bool dense_ok = k <= 8 && g.pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096;
-      const int algo = env_or("KMG_ALGO", 0);
+      const int algo = c->tune.algo;
       bool dense = false;
       if (algo == 1) {
         if (!dense_ok)
           return fail(KMG_EUNSUPPORTED, "dense formulation needs k <= 8 and <= 127 windows");
         dense = true;
       } else if (algo == 0 && dense_ok) {
-        dense = mm ? (k <= env_or("KMG_DENSE_KMAX_MM", 7)) : (k <= env_or("KMG_DENSE_KMAX_SP", 5));
+        dense = mm ? (k <= c->tune.dense_kmax_mm) : (k <= c->tune.dense_kmax_sp);
       }
       if (dense)
-        return gram_dense(c, k, mm_eff, mm ? g.window : 0, d_codes, d_lens, n, ldc, row0, row1,
-                          o, mm && p->normalize);
+        return gram_dense(c, k, mm_eff, mm ? g.window : 0, d_codes, d_lens, n, ldc, ranges, o,
+                          mm && p->normalize, after);
+      // 2-bit packed records of every sequence (kernels.py:187-193 `format`, as 2 bits a
+      // letter plus a validity mask), read by the index build and the Gram kernels
+      const int cw = packed_cw(ldc), mw = packed_mw(ldc);
+      KMG_TRY(c->packed.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(1, n) * (cw + mw)));
+      const Packed pkd{c->packed.as<uint32_t>(), (int64_t)(cw + mw), cw};
+      {
+        StageTimer t(c, ST_PACK);
+        KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, g.window, c->packed.as<uint32_t>(), c->stream));
+      }
       if (!use_index) {
         // all-pairs Hamming formulation (any m, k <= 16)
         if (g.pmax > 256) return fail(KMG_EUNSUPPORTED, "Hamming path needs <= 256 k-mers");
@@ -493,82 +563,60 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(c->kmers.ensure(sizeof(uint32_t) * (size_t)(n * g.pmax > 0 ? n * g.pmax : 1)));
         {
           StageTimer t(c, ST_EXTRACT);
-          KMG_HIP(launch_extract(g, d_codes, d_lens, ldc, c->kmers.as<uint32_t>(), c->stream));
+          KMG_HIP(launch_extract(g, pkd, c->kmers.as<uint32_t>(), c->stream));
         }
         KMG_TRY(upload_wtab(c, w));
         if (p->normalize) {
-          KMG_TRY(diag_hamming(c, g, d_codes, d_lens, ldc));
+          KMG_TRY(diag_hamming(c, g, pkd));
           o.normalize = 1;
           o.diagv = c->diagv.as<double>();
           o.dsq = c->dsq.as<double>();
         }
-        StageTimer t(c, ST_GRAM);
-        KMG_HIP(launch_gram_hamming(g, c->kmers.as<uint32_t>(), row0, row1,
-                                    c->wtab.as<int64_t>(), o, c->stream));
-        return KMG_OK;
+        return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          for (int64_t r = r0; r < r1; r += 65535) {  // grid.y <= 65535 rows per launch
+            OutSpec os = oq;
+            os.out = (char *)oq.out + (size_t)(r - r0) * oq.ld * dtype_size(dt);
+            hipError_t e = launch_gram_hamming(g, c->kmers.as<uint32_t>(), r, std::min(r1, r + 65535),
+                                               c->wtab.as<int64_t>(), os, c->stream);
+            if (e != hipSuccess) return e;
+          }
+          return hipSuccess;
+        });
       }
       if (exact) {
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, std::min(65536, env_or("KMG_SP_CHUNK", 24576)));
-      } else if (use_rot) {
+        choose_chunks(g, std::min(65536, c->tune.sp_chunk));
+      } else {
         g.copies = k;
         g.rot = 1;
         g.nkeys = (uint32_t)pow4(k);
-        int max_chunk = std::min(65536, env_or("KMG_MM_CHUNK", 20480));
-        if (use_slots) {  // mean list (4-bin group) length <= 40: inline in one line
-          const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
-          max_chunk = (int)std::max<int64_t>(8, std::min<int64_t>({max_chunk, cap, 64000}));
-        }
-        choose_chunks(g, max_chunk);
-      } else {
-        g.copies = k;
-        g.nkeys = (uint32_t)pow4(k - 1);
-        choose_chunks(g, std::min(16384, env_or("KMG_MM_CHUNK", 10240)));
+        // mean list (4-bin group) length <= 40: inline in one 128-byte line
+        const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
+        choose_chunks(g, (int)std::max<int64_t>(8, std::min<int64_t>({(int64_t)c->tune.mm_chunk, cap, 64000})));
       }
-      KMG_TRY(build_index(c, g, d_codes, d_lens, ldc));
+      KMG_TRY(build_index(c, g, pkd));
       if (use_slots) {
         KMG_TRY(c->slots.ensure((size_t)(g.nbins() >> 2) * KMG_SLOT_BYTES));
-        StageTimer t(c, ST_PACK);
+        StageTimer t(c, ST_SLOTS);
         KMG_HIP(launch_slot_pack(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                  c->slots.as<uint4>(), c->stream));
       }
       if (p->normalize) {
         KMG_TRY(upload_wtab(c, w));
-        KMG_TRY(diag_hamming(c, g, d_codes, d_lens, ldc));
+        KMG_TRY(diag_hamming(c, g, pkd));
         o.normalize = 1;
         o.diagv = c->diagv.as<double>();
         o.dsq = c->dsq.as<double>();
       }
-      StageTimer t(c, ST_GRAM);
-      if (exact) {
-        KMG_HIP(launch_gram_spectrum(g, d_codes, d_lens, ldc, c->off.as<uint32_t>(),
-                                     c->ent.as<uint16_t>(), row0, row1, o, c->stream));
-      } else {
-        if (use_slots) {
-          // KMG_MM_TRI=1, full K on one device: upper triangle + mirror (halves the LDS
-          // atomics, but the mirror costs what the Gram kernel saves: off by default)
-          const int tri = (row0 == 0 && row1 == n && n >= 256 && env_or("KMG_MM_TRI", 0)) ? 1 : 0;
-          KMG_HIP(launch_gram_mismatch1_slots(g, d_codes, ldc, c->slots.as<uint4>(),
-                                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), row0,
-                                              row1, (int)w[0], (int)w[1], (int)w[2], o, tri,
-                                              c->stream));
-          if (tri) {
-            StageTimer tm(c, ST_MIRROR);
-            KMG_HIP(launch_mirror_lower(o.out, o.ld, n, o.dtype, c->stream));
-          }
-        }
-        else if (use_rot)
-          KMG_HIP(launch_gram_mismatch1_rot(g, d_codes, ldc, c->off.as<uint32_t>(),
-                                            c->ent.as<uint16_t>(),
-                                            (uint32_t)(c->ent.bytes / sizeof(uint16_t)), row0,
-                                            row1, (int)w[0], (int)w[1], (int)w[2], o, c->stream));
-        else
-          KMG_HIP(launch_gram_mismatch1(g, d_codes, ldc, c->off.as<uint32_t>(),
-                                        c->ent.as<uint16_t>(), row0, row1, (int)w[0], (int)w[1],
-                                        (int)w[2], o, c->stream));
-      }
-      return KMG_OK;
+      return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        return exact ? launch_gram_spectrum(g, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                            r0, r1, oq, c->stream)
+                     : launch_gram_mismatch1_slots(g, pkd, c->slots.as<uint4>(),
+                                                   c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                                   r0, r1, (int)w[0], (int)w[1], (int)w[2], oq,
+                                                   c->stream);
+      });
     }
     case KMG_WD:
     case KMG_WDS: {
@@ -577,29 +625,41 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
-      StageTimer t(c, ST_GRAM);
-      hipError_t e = p->kind == KMG_WD
-                         ? launch_gram_wd(q, row0, row1, p->d, p->coef_a, o, c->stream)
-                         : launch_gram_wds(q, row0, row1, p->d, p->S, p->coef_a, p->coef_b, o,
-                                           c->stream);
-      if (e == hipErrorNotSupported)
+      bool unsupported = false;
+      const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        hipError_t e = p->kind == KMG_WD
+                           ? launch_gram_wd(q, r0, r1, p->d, p->coef_a, oq, c->stream)
+                           : launch_gram_wds(q, r0, r1, p->d, p->S, p->coef_a, p->coef_b, oq,
+                                             c->stream);
+        if (e == hipErrorNotSupported) {
+          unsupported = true;
+          return hipSuccess;
+        }
+        return e;
+      });
+      if (unsupported)
         return fail(KMG_EUNSUPPORTED, "WD/WDS: sequence length %d / shift %d not supported",
                     maxlen, p->S);
-      KMG_HIP(e);
-      return KMG_OK;
+      return r;
     }
     case KMG_SUBSTRING: {
       if (p->k < 0) return fail(KMG_EINVAL, "k < 0");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "SS produces float64 values");
       if (p->k > 16) return fail(KMG_EUNSUPPORTED, "SS k > 16");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
-      const int mirror = (row0 == 0 && row1 == n) ? 1 : 0;
-      StageTimer t(c, ST_GRAM);
-      hipError_t e =
-          launch_gram_ss(q, row0, row1, p->k, p->lambda, p->lambda2, mirror, o, c->stream);
-      if (e == hipErrorNotSupported) return fail(KMG_EUNSUPPORTED, "SS parameters");
-      KMG_HIP(e);
-      return KMG_OK;
+      // one range covering the whole matrix: upper triangle + mirror (kernels.py:378-381)
+      const int mirror = (ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n) ? 1 : 0;
+      bool unsupported = false;
+      const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        hipError_t e = launch_gram_ss(q, r0, r1, p->k, p->lambda, p->lambda2, mirror, oq, c->stream);
+        if (e == hipErrorNotSupported) {
+          unsupported = true;
+          return hipSuccess;
+        }
+        return e;
+      });
+      if (unsupported) return fail(KMG_EUNSUPPORTED, "SS parameters");
+      return r;
     }
     case KMG_LOCALALIGN: {
       if (dt == KMG_I32) return fail(KMG_EINVAL, "LA produces float64 values");
@@ -607,23 +667,25 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         return fail(KMG_EUNSUPPORTED, "LA intended mode not built in this version");
       // The reference aliases M,X,Y,X2,Y2 to one array and never writes cell
       // [n_x, n_y] (kernels.py:238-240, 262-264): every entry is log(1+0)/beta = 0.
-      StageTimer t(c, ST_GRAM);
-      if (rows > 0 && n > 0)
-        KMG_HIP(hipMemset2DAsync(d_out, (size_t)ld * dtype_size(dt), 0,
-                                 (size_t)n * dtype_size(dt), (size_t)rows, c->stream));
-      return KMG_OK;
+      return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        if (r1 <= r0 || n == 0) return hipSuccess;
+        return hipMemset2DAsync(oq.out, (size_t)ld * dtype_size(dt), 0, (size_t)n * dtype_size(dt),
+                                (size_t)(r1 - r0), c->stream);
+      });
     }
     case KMG_GAPPY: {
+      const int W = p->window > 0 ? p->window : 101;
+      // windows read x[0 : W) of every row (kernels.py:430): narrower rows would read into
+      // the next row (padding codes >= 4 inside a row are skipped)
+      if (n > 0 && ldc < W)
+        return fail(KMG_EINVAL, "gappy: code rows (%lld) shorter than the window %d",
+                    (long long)ldc, W);
       if (p->la_mode == KMG_MODE_INTENDED) {
-        const int W = p->window > 0 ? p->window : 101;
         if (p->k < 1 || p->k > 15 || p->g < 0 || p->g >= p->k || p->k - p->g > 8)
           return fail(KMG_EUNSUPPORTED, "intended gappy: need 1 <= k <= 15, 0 <= g < k, k-g <= 8");
-        if (n > 0 && ldc < W)  // windows read x[0 : W); padding codes (>= 4) are skipped
-          return fail(KMG_EINVAL, "intended gappy: code rows (%lld) shorter than the window %d",
-                      (long long)ldc, W);
         if (dt == KMG_I32 && p->normalize) return fail(KMG_EINVAL, "normalised GP is float64");
-        return gram_gappy_intended(c, p->k, p->g, W, d_codes, n, ldc, row0, row1, o,
-                                   p->normalize != 0);
+        return gram_gappy_intended(c, p->k, p->g, W, d_codes, n, ldc, ranges, o,
+                                   p->normalize != 0, after);
       }
       if (!(p->k == 1 && p->g == 0))
         return fail(KMG_EUNSUPPORTED, "gappy kernel defined only for k=1, g=0");
@@ -634,10 +696,10 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       o.normalize = 1;
       o.diagv = c->diagv.as<double>();
       o.dsq = c->dsq.as<double>();
-      StageTimer t(c, ST_GRAM);
-      KMG_HIP(launch_gram_gappy1(q, row0, row1, p->window > 0 ? p->window : 101, o,
-                                 c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
-      return KMG_OK;
+      return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        return launch_gram_gappy1(q, r0, r1, W, oq, c->diagv.as<double>(), c->dsq.as<double>(),
+                                  c->stream);
+      });
     }
     default:
       return fail(KMG_EINVAL, "unknown kernel kind %d", p->kind);
@@ -673,6 +735,7 @@ int kmg_create(kmg_ctx **out, int device_id) {
   KMG_HIP(hipSetDevice(device_id));
   kmg_ctx *c = new kmg_ctx();
   c->device = device_id;
+  read_tuning(c->tune);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -690,11 +753,13 @@ int kmg_destroy(kmg_ctx *c) {
   if (c->blas) rocblas_destroy_handle(c->blas);
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
-                    &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots,
+                    &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return KMG_OK;
@@ -726,8 +791,8 @@ int kmg_gram(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_
   KMG_TRY(c->h_out.ensure(esz * (size_t)n * ldd));
   KMG_HIP(hipMemcpyAsync(c->h_codes.p, codes, (size_t)n * ldc, hipMemcpyHostToDevice, c->stream));
   KMG_HIP(hipMemcpyAsync(c->h_lens.p, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
-  KMG_TRY(gram_device(c, p, c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), maxlen, n, ldc, 0,
-                      n, out_dtype, c->h_out.p, ldd));
+  KMG_TRY(gram_device(c, p, c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), maxlen, n, ldc,
+                      {RowRange{0, n, c->h_out.p}}, out_dtype, ldd));
   KMG_HIP(hipMemcpy2DAsync(out, (size_t)ld_out * esz, c->h_out.p, (size_t)ldd * esz,
                            (size_t)n * esz, (size_t)n, hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
@@ -743,8 +808,82 @@ int kmg_gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   KMG_HIP(hipSetDevice(c->device));
   // device-resident path: sequence lengths are device data; the caller promises
   // max(lens) <= ldc (checked in the host path).  maxlen = ldc bounds every kernel.
-  return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, row0, row1, out_dtype, d_out,
-                     ld_out);
+  return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, {RowRange{row0, row1, d_out}},
+                     out_dtype, ld_out);
+}
+
+int kmg_reload_tuning(kmg_ctx *c) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  read_tuning(c->tune);
+  return KMG_OK;
+}
+
+int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block) {
+  if (n <= 0 || nranks < 1 || block < 1) return n > 0 ? n : 0;
+  const int64_t round = (int64_t)nranks * block;
+  return (n + round - 1) / round * round;
+}
+
+int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                    const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype, void *d_out,
+                    int64_t ld_out, int32_t nranks, int32_t rank, int64_t block, int32_t gather) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_TRY(check_params(p, n, ldc, out_dtype));
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
+  if (block < 1) return fail(KMG_EINVAL, "block < 1");
+  if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
+  if (gather && nranks > 1 && (!c->comm || c->nranks != nranks || c->rank != rank))
+    return fail(KMG_EINVAL, "gather needs a communicator of %d ranks with this rank %d", nranks, rank);
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t esz = dtype_size(out_dtype);
+  const int64_t round = (int64_t)nranks * block;
+  const int64_t nround = (n + round - 1) / round;
+  // this rank's block of every round: rows [t*round + rank*block, +block) clipped to n
+  std::vector<RowRange> ranges;
+  for (int64_t t = 0; t < nround; ++t) {
+    const int64_t r0 = std::min(n, t * round + (int64_t)rank * block);
+    const int64_t r1 = std::min(n, r0 + block);
+    ranges.push_back(RowRange{r0, r1, (char *)d_out + (size_t)r0 * ld_out * esz});
+  }
+  AfterRange after = nullptr;
+  const bool do_gather = gather && nranks > 1;
+  if (do_gather) {
+    if (!c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+    after = [&](size_t t) -> int {
+      // round t's rows [t*round, (t+1)*round) are contiguous in d_out: rank q's block sits
+      // at q * block rows, i.e. send = recv + rank * count, so the all-gather is in place.
+      // It runs on its own stream behind an event of this rank's Gram launch, overlapped
+      // with the next round's Gram kernels.
+      // one event suffices: hipStreamWaitEvent captures the record made just before it
+      KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+      KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+      hipEvent_t b = nullptr, e = nullptr;
+      if (c->timing) {
+        b = pool_event(c);
+        e = pool_event(c);
+        KMG_HIP(hipEventRecord(b, c->comm_stream));
+      }
+      char *recv = (char *)d_out + (size_t)(t * round) * ld_out * esz;
+      const size_t count = (size_t)block * ld_out * esz;
+      ncclResult_t r = ncclAllGather(recv + (size_t)rank * count, recv, count, ncclChar, c->comm,
+                                     c->comm_stream);
+      if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+      if (c->timing) {
+        KMG_HIP(hipEventRecord(e, c->comm_stream));
+        c->ev_log.push_back({ST_GATHER, {b, e}});
+      }
+      return KMG_OK;
+    };
+  }
+  KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, ld_out, after));
+  if (do_gather) {  // stream order: later work on the context stream sees the full K
+    KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
+    KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+  }
+  return KMG_OK;
 }
 
 int kmg_normalize(kmg_ctx *c, double *K, int64_t n, int64_t ld, int32_t *skipped) {
@@ -1082,11 +1221,26 @@ static int blas_handle(kmg_ctx *c) {
                   __FILE__, __LINE__);                                                \
   } while (0)
 
+// K != K^T (bitwise)?  The reference inverts whatever K it is given (KRR.py:33,
+// KLR.py:55), so an asymmetric K (hand-made, or centred with rounding) must not be read
+// through one triangle by the Cholesky path.
+static int is_asymmetric(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, bool *asym) {
+  int *flag = (int *)(c->sv_info.as<rocblas_int>() + 2);
+  KMG_HIP(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
+  KMG_HIP(launch_asymmetry(d_K, ld, n, flag, c->stream));
+  int h = 0;
+  KMG_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  *asym = h != 0;
+  return KMG_OK;
+}
+
 // Build the system into sv_mat (build()), factorise, solve in place into rhs.
-// B = diag(s) K diag(s) + shift I is symmetric, so its row-major image is its own
-// column-major image and rocSOLVER's column-major routines apply unchanged.
+// B = diag(s) K diag(s) + shift I is symmetric when K is, so its row-major image is its
+// own column-major image and rocSOLVER's column-major routines apply unchanged; an
+// asymmetric K goes straight to LU on the transposed view.
 template <typename Build>
-static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs) {
+static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs, bool asym = false) {
   if (n > INT32_MAX / 2) return fail(KMG_EUNSUPPORTED, "n=%lld too large for rocSOLVER", (long long)n);
   const rocblas_int ni = (rocblas_int)n;
   double *B = c->sv_mat.as<double>();
@@ -1094,9 +1248,17 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs) {
   rocblas_int *ipiv = info + 4;
   rocblas_int hinfo = 0;
   KMG_TRY(build());
+  if (asym) {
+    KMG_BLAS(rocsolver_dgetrf(c->blas, ni, ni, B, ni, ipiv, info));
+    KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+    if (hinfo != 0) return fail(KMG_ESINGULAR, "Singular matrix");
+    KMG_BLAS(rocsolver_dgetrs(c->blas, rocblas_operation_transpose, ni, 1, B, ni, ipiv, rhs, ni));
+    return KMG_OK;
+  }
   // B is symmetric: either triangle is the matrix (KMG_POTRF_UPPER selects rocSOLVER's
   // upper-triangle variant)
-  const rocblas_fill fill = env_or("KMG_POTRF_UPPER", 0) ? rocblas_fill_upper : rocblas_fill_lower;
+  const rocblas_fill fill = c->tune.potrf_upper ? rocblas_fill_upper : rocblas_fill_lower;
   KMG_BLAS(rocsolver_dpotrf(c->blas, fill, ni, B, ni, info));
   KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
@@ -1133,7 +1295,9 @@ static int krr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     KMG_HIP(launch_shift_scale(d_K, ld, nullptr, shift, nullptr, n, c->sv_mat.as<double>(), n, c->stream));
     return KMG_OK;
   };
-  return solve_system(c, build, n, d_alpha);
+  bool asym = false;
+  KMG_TRY(is_asymmetric(c, d_K, ld, n, &asym));
+  return solve_system(c, build, n, d_alpha, asym);
 }
 
 static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const double *d_y,
@@ -1149,6 +1313,8 @@ static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     KMG_HIP(launch_shift_scale(d_K, ld, s, shift, nullptr, n, c->sv_mat.as<double>(), n, c->stream));
     return KMG_OK;
   };
+  bool asym = false;
+  KMG_TRY(is_asymmetric(c, d_K, ld, n, &asym));
   double diff = INFINITY;
   int32_t it = 0;
   for (int32_t r = 0; r < maxiter; ++r) {
@@ -1157,7 +1323,7 @@ static int klr_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     KMG_BLAS(rocblas_dgemv(c->blas, rocblas_operation_transpose, (rocblas_int)n, (rocblas_int)n,
                            &one, d_K, (rocblas_int)ld, prev, 1, &zero, m, 1));
     KMG_HIP(launch_irls(m, d_y, n, s, rhs, c->stream));
-    KMG_TRY(solve_system(c, build, n, rhs));
+    KMG_TRY(solve_system(c, build, n, rhs, asym));
     KMG_HIP(launch_scale_diff(s, rhs, prev, n, cur, dsum, c->stream));
     double h = 0.0;
     KMG_HIP(hipMemcpyAsync(&h, dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -1372,6 +1538,14 @@ int kmg_allgather_rows(kmg_ctx *c, void *d_K, int64_t n, int64_t ld, int32_t dt,
                        const int64_t *splits) {
   if (!c || !c->comm) return fail(KMG_EINVAL, "communicator not initialised");
   if (!splits) return fail(KMG_EINVAL, "splits is NULL");
+  if (!d_K && n > 0) return fail(KMG_EINVAL, "d_K is NULL");
+  if (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64) return fail(KMG_EINVAL, "unknown dtype %d", dt);
+  if (n < 0 || (n > 0 && ld < n)) return fail(KMG_EINVAL, "ld < n");
+  // rank r owns rows [splits[r], splits[r+1]): 0 = splits[0] <= ... <= splits[nranks] = n
+  if (splits[0] != 0 || splits[c->nranks] != n)
+    return fail(KMG_EINVAL, "splits must start at 0 and end at n");
+  for (int q = 0; q < c->nranks; ++q)
+    if (splits[q + 1] < splits[q]) return fail(KMG_EINVAL, "splits must be non-decreasing");
   KMG_HIP(hipSetDevice(c->device));
   const size_t esz = dtype_size(dt);
   // rows of rank r are contiguous ([splits[r], splits[r+1]) x ld): an all-gather with
@@ -1387,7 +1561,6 @@ int kmg_allgather_rows(kmg_ctx *c, void *d_K, int64_t n, int64_t ld, int32_t dt,
   if (r != ncclSuccess || r2 != ncclSuccess)
     return fail(KMG_ERCCL, "ncclBroadcast group: %s",
                 ncclGetErrorString(r != ncclSuccess ? r : r2));
-  (void)n;
   return KMG_OK;
 }
 

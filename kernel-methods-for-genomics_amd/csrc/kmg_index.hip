@@ -35,72 +35,52 @@ __device__ __forceinline__ uint32_t drop_letter(uint32_t code, int p, int k) {
 constexpr int IDX_THREADS = 1024;  // upper bound; blocks launch g.part_threads
 constexpr int FINE_THREADS = 1024;
 
-// stage IDX_SEQS rows of codes in LDS; returns number of staged sequences
-__device__ __forceinline__ int stage_rows(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                          const int32_t *lens, uint8_t *srow, int32_t *slen,
-                                          int rowlen, int64_t j0) {
+// stage the packed records (Packed, kmg_internal.h) of seqs_per_block sequences in LDS;
+// returns the number of staged sequences
+__device__ __forceinline__ int stage_rows(const IndexGeom &g, const Packed &pk, uint32_t *srec,
+                                          int64_t j0) {
   const int ns = (int)min((int64_t)g.seqs_per_block, g.n - j0);
-  for (int t = threadIdx.x; t < ns * rowlen; t += blockDim.x) {
-    const int s = t / rowlen, c = t - s * rowlen;
-    srow[t] = codes[(j0 + s) * ldc + c];
-  }
-  if ((int)threadIdx.x < ns) {
-    const int L = g.window > 0 ? g.window : lens[j0 + threadIdx.x];
-    slen[threadIdx.x] = min(L, rowlen);
-  }
+  const int words = ns * (int)pk.ldp;
+  const uint32_t *src = pk.w + j0 * pk.ldp;
+  for (int t = threadIdx.x; t < words; t += blockDim.x) srec[t] = src[t];
   __syncthreads();
   return ns;
 }
 
-// visit every (bin, value) item of the staged sequences
+// visit every (bin, value) item of the staged sequences: windows a < pmax whose k symbols
+// are all A/C/G/T and inside the sequence (mask bits clear; kernels.py:21-24 drops the rest)
 template <typename F>
-__device__ __forceinline__ void for_items(const IndexGeom &g, const uint8_t *srow,
-                                          const int32_t *slen, int rowlen, int ns, int64_t j0,
-                                          F &&f) {
+__device__ __forceinline__ void for_items(const IndexGeom &g, const Packed &pk, const uint32_t *srec,
+                                          int ns, int64_t j0, F &&f) {
   const int per = g.pmax;
   for (int t = threadIdx.x; t < ns * per; t += blockDim.x) {
     const int s = t / per, a = t - s * per;
-    if (a > slen[s] - g.k) continue;  // windows range(L-k+1)
-    const uint8_t *w = srow + s * rowlen + a;
-    uint32_t c = 0, bad = 0;
-    for (int q = 0; q < g.k; ++q) {
-      const uint32_t v = w[q];
-      bad |= v & ~3u;  // non-ACGT symbol: k-mer equals no beta (kernels.py:23-24)
-      c = (c << 2) | (v & 3u);
-    }
-    if (bad) continue;
+    const uint32_t c = pk_window(srec + s * pk.ldp, pk.cw, a, g.k);
+    if (c == KMG_INVALID) continue;
     const int64_t j = j0 + s;
     const int ch = (int)(j / g.chunk);
     const uint32_t col = (uint32_t)(j - (int64_t)ch * g.chunk);
     if (g.copies == 1) {
       f((uint32_t)(ch * (int64_t)g.nkeys + c), col);
-    } else if (g.rot) {
+    } else {
       for (int p = 0; p < g.copies; ++p) {
         const uint32_t rk = (drop_letter(c, p, g.k) << 2) | letter_at(c, p, g.k);
         f((uint32_t)(((int64_t)p * g.nchunks + ch) * g.nkeys + rk), col);
-      }
-    } else {
-      for (int p = 0; p < g.copies; ++p) {
-        const uint32_t bin = (uint32_t)(((int64_t)p * g.nchunks + ch) * g.nkeys + drop_letter(c, p, g.k));
-        f(bin, col | (letter_at(c, p, g.k) << 14));
       }
     }
   }
 }
 
-__global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
-                                                                   int64_t ldc, const int32_t *__restrict__ lens,
-                                                                   int rowlen, uint32_t *__restrict__ bcount) {
+__global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, Packed pk, uint32_t *__restrict__ bcount) {
   extern __shared__ __align__(16) uint32_t sm[];
   const int nbk = (int)g.nbuckets();
   uint32_t *hist = sm;
-  int32_t *slen = (int32_t *)(hist + nbk);
-  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
+  uint32_t *srec = hist + nbk;
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
   const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
-  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int ns = stage_rows(g, pk, srec, j0);
   const int fb = g.fine_bits;
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
+  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
   __syncthreads();
   for (int b = threadIdx.x; b < nbk; b += blockDim.x)
     if (hist[b]) atomicAdd(&bcount[b], hist[b]);
@@ -142,9 +122,7 @@ __device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
 // cheap) so no separate scan launch is needed; block 0 publishes it as boff[] for the
 // fine pass.  Positions inside a bucket: base + one returning add per (block, bucket)
 // on the relative cursor bcursor[] (zero on entry; re-zeroed by the fine pass).
-__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
-                                                                   int64_t ldc, const int32_t *__restrict__ lens,
-                                                                   int rowlen, const uint32_t *__restrict__ bcount,
+__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, Packed pk, const uint32_t *__restrict__ bcount,
                                                                    uint32_t *__restrict__ bcursor,
                                                                    uint32_t *__restrict__ boff,
                                                                    uint32_t *__restrict__ tmp) {
@@ -153,8 +131,7 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, 
   const int nbk = (int)g.nbuckets();
   uint32_t *hist = sm;
   uint32_t *base = hist + nbk;
-  int32_t *slen = (int32_t *)(base + nbk);
-  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
+  uint32_t *srec = base + nbk;
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
     hist[b] = 0;
     base[b] = bcount[b];
@@ -166,10 +143,10 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, 
     if (threadIdx.x == 0) boff[nbk] = total;
   }
   const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
-  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int ns = stage_rows(g, pk, srec, j0);
   const int fb = g.fine_bits;
   const uint32_t fmask = (1u << fb) - 1u;
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
+  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
   __syncthreads();
   // reserve this block's range inside every bucket it touches
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
@@ -177,7 +154,7 @@ __global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, 
     if (c) hist[b] = base[b] + atomicAdd(&bcursor[b], c);
   }
   __syncthreads();
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
+  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t val) {
     const uint32_t pos = atomicAdd(&hist[bin >> fb], 1u);
     tmp[pos] = ((bin & fmask) << 16) | val;
   });
@@ -234,22 +211,20 @@ __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, 
 //      sum_q hcnt[b][q]; LDS fine histogram + scan -> off[], then the items are gathered
 //      from every block's segment into ent[].  Results do not depend on dispatch order.
 __global__ __launch_bounds__(IDX_THREADS) void part_local_kernel(
-    IndexGeom g, const uint8_t *__restrict__ codes, int64_t ldc, const int32_t *__restrict__ lens,
-    int rowlen, int nblk, uint32_t cap, uint32_t *__restrict__ hcnt, uint32_t *__restrict__ hstart,
-    uint32_t *__restrict__ tmp) {
+    IndexGeom g, Packed pk, int nblk, uint32_t cap, uint32_t *__restrict__ hcnt,
+    uint32_t *__restrict__ hstart, uint32_t *__restrict__ tmp) {
   extern __shared__ __align__(16) uint32_t sm[];
   __shared__ uint32_t wtmp[IDX_THREADS / 64];
   const int nbk = (int)g.nbuckets();
   uint32_t *h = sm;
-  int32_t *slen = (int32_t *)(h + nbk);
-  uint8_t *srow = (uint8_t *)(slen + g.seqs_per_block);
+  uint32_t *srec = h + nbk;
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) h[b] = 0;
   const int q = blockIdx.x;
   const int64_t j0 = (int64_t)q * g.seqs_per_block;
-  const int ns = stage_rows(g, codes, ldc, lens, srow, slen, rowlen, j0);
+  const int ns = stage_rows(g, pk, srec, j0);
   const int fb = g.fine_bits;
   const uint32_t fmask = (1u << fb) - 1u;
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&h[bin >> fb], 1u); });
+  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&h[bin >> fb], 1u); });
   __syncthreads();
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) hcnt[(size_t)b * nblk + q] = h[b];
   __syncthreads();
@@ -257,7 +232,7 @@ __global__ __launch_bounds__(IDX_THREADS) void part_local_kernel(
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) hstart[(size_t)b * nblk + q] = h[b];
   __syncthreads();
   uint32_t *out = tmp + (size_t)q * cap;
-  for_items(g, srow, slen, rowlen, ns, j0, [&](uint32_t bin, uint32_t val) {
+  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t val) {
     const uint32_t pos = atomicAdd(&h[bin >> fb], 1u);
     out[pos] = ((bin & fmask) << 16) | val;
   });
@@ -380,27 +355,56 @@ hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint1
   return hipGetLastError();
 }
 
-// plain k-mer extraction (Hamming formulation and the diagonal kernels)
-__global__ __launch_bounds__(256) void extract_kernel(IndexGeom g, const uint8_t *__restrict__ codes,
-                                                      const int32_t *__restrict__ lens, int64_t ldc,
+// plain k-mer extraction (Hamming formulation)
+__global__ __launch_bounds__(256) void extract_kernel(IndexGeom g, Packed pk,
                                                       uint32_t *__restrict__ kmers) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= g.n * g.pmax) return;
   const int64_t j = t / g.pmax;
   const int a = (int)(t - j * g.pmax);
-  const int L = g.window > 0 ? g.window : lens[j];
-  uint32_t code = KMG_INVALID;
-  if (a <= L - g.k) {
-    const uint8_t *s = codes + j * ldc + a;
-    uint32_t c = 0, bad = 0;
-    for (int q = 0; q < g.k; ++q) {
-      const uint32_t v = s[q];
-      bad |= v & ~3u;
-      c = (c << 2) | (v & 3u);
-    }
-    if (!bad) code = c;
+  kmers[t] = pk_window(pk.w + j * pk.ldp, pk.cw, a, g.k);
+}
+
+// ------------------------------------------------------------------ 2-bit packing
+// one thread per (sequence, 32-symbol block): 2 code words + 1 mask word of the record
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ codes,
+                                                   const int32_t *__restrict__ lens, int64_t n,
+                                                   int64_t ldc, int cw, int mw, int nb,
+                                                   uint32_t *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * nb) return;
+  const int64_t j = t / nb;
+  const int b = (int)(t - j * nb);
+  const int len = min(max(lens[j], 0), (int)ldc);
+  const uint8_t *r = codes + j * ldc;
+  uint32_t c0 = 0, c1 = 0, m = 0;
+#pragma unroll 8
+  for (int q = 0; q < 32; ++q) {
+    const int pos = 32 * b + q;
+    const uint32_t v = pos < len ? (uint32_t)r[pos] : 4u;
+    m |= (v > 3u ? 1u : 0u) << q;
+    const uint32_t sym = v & 3u;
+    if (q < 16)
+      c0 |= sym << (30 - 2 * q);
+    else
+      c1 |= sym << (30 - 2 * (q - 16));
   }
-  kmers[t] = code;
+  uint32_t *rec = out + j * (int64_t)(cw + mw);
+  if (2 * b < cw) rec[2 * b] = c0;
+  if (2 * b + 1 < cw) rec[2 * b + 1] = c1;
+  if (b < mw) rec[cw + b] = m;
+}
+
+hipError_t launch_pack(const uint8_t *codes, const int32_t *lens, int64_t n, int64_t ldc,
+                       int window, uint32_t *packed, hipStream_t s) {
+  (void)window;
+  if (n == 0) return hipSuccess;
+  const int cw = packed_cw(ldc), mw = packed_mw(ldc);
+  const int nb = max((cw + 1) / 2, mw);
+  const int64_t threads = n * nb;
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, codes,
+                     lens, n, ldc, cw, mw, nb, packed);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ scan (bucket counts)
@@ -504,34 +508,25 @@ hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, in
 }
 
 // ------------------------------------------------------------------ launchers
-static int part_rowlen(const IndexGeom &g, int64_t ldc) {
-  return g.window > 0 ? g.window : (int)ldc;
+static size_t part_lds(const IndexGeom &g, const Packed &pk, int arrays) {
+  return sizeof(uint32_t) * ((size_t)g.nbuckets() * arrays + (size_t)g.seqs_per_block * pk.ldp) + 16;
 }
 
-static size_t part_lds(const IndexGeom &g, int rowlen, int arrays) {
-  return sizeof(uint32_t) * (size_t)g.nbuckets() * arrays + sizeof(int32_t) * g.seqs_per_block +
-         (size_t)g.seqs_per_block * rowlen + 16;
-}
-
-hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, uint32_t *bcount, hipStream_t s) {
+hipError_t launch_index_count(const IndexGeom &g, const Packed &pk, uint32_t *bcount,
+                              hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  const int rowlen = part_rowlen(g, ldc);
   const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, rowlen, 1), s,
-                     g, codes, ldc, lens, rowlen, bcount);
+  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, pk, 1), s,
+                     g, pk, bcount);
   return hipGetLastError();
 }
 
-hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, const uint32_t *bcount, uint32_t *bcursor,
-                              uint32_t *boff, uint32_t *tmp, hipStream_t s) {
+hipError_t launch_index_place(const IndexGeom &g, const Packed &pk, const uint32_t *bcount,
+                              uint32_t *bcursor, uint32_t *boff, uint32_t *tmp, hipStream_t s) {
   if (g.n == 0) return hipSuccess;
-  const int rowlen = part_rowlen(g, ldc);
   const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads),
-                     part_lds(g, rowlen, 2), s, g, codes, ldc, lens, rowlen, bcount, bcursor, boff,
-                     tmp);
+  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, pk, 2), s,
+                     g, pk, bcount, bcursor, boff, tmp);
   return hipGetLastError();
 }
 
@@ -549,14 +544,11 @@ size_t index_gather_lds(const IndexGeom &g, int64_t nblk) {
   return sizeof(uint32_t) * (((size_t)1 << g.fine_bits) + 2 * (size_t)nblk);
 }
 
-hipError_t launch_index_local(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, int nblk, uint32_t cap, uint32_t *hcnt,
-                              uint32_t *hstart, uint32_t *tmp, hipStream_t s) {
+hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, int nblk, uint32_t cap,
+                              uint32_t *hcnt, uint32_t *hstart, uint32_t *tmp, hipStream_t s) {
   if (g.n == 0 || nblk == 0) return hipSuccess;
-  const int rowlen = part_rowlen(g, ldc);
   hipLaunchKernelGGL(part_local_kernel, dim3((unsigned)nblk), dim3(g.part_threads),
-                     part_lds(g, rowlen, 1), s, g, codes, ldc, lens, rowlen, nblk, cap, hcnt,
-                     hstart, tmp);
+                     part_lds(g, pk, 1), s, g, pk, nblk, cap, hcnt, hstart, tmp);
   return hipGetLastError();
 }
 
@@ -571,13 +563,11 @@ hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const
   return hipGetLastError();
 }
 
-hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                          int64_t ldc, uint32_t *kmers, hipStream_t s) {
+hipError_t launch_extract(const IndexGeom &g, const Packed &pk, uint32_t *kmers, hipStream_t s) {
   const int64_t items = g.n * g.pmax;
   if (items == 0) return hipSuccess;
   const int64_t blocks = (items + 255) / 256;
-  hipLaunchKernelGGL(extract_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, codes, lens, ldc,
-                     kmers);
+  hipLaunchKernelGGL(extract_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g, pk, kmers);
   return hipGetLastError();
 }
 

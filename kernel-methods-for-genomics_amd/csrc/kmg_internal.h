@@ -43,28 +43,57 @@ struct IndexGeom {
   }
 };
 
-hipError_t launch_index_count(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, uint32_t *bcount, hipStream_t s);
+// 2-bit packed sequences (kmg_pack_kernel, kmg_index.hip).  Record of sequence j =
+// w + j * ldp words:
+//   words [0, cw)        symbols, 16 per word, big-endian: symbol t at bits 30 - 2 (t & 15)
+//                        of word t >> 4 (so a k-mer read off the words has its first
+//                        letter most significant, the base-4 order of kernels.py:37,206)
+//   words [cw, cw + mw)  invalid mask: bit t & 31 of word cw + (t >> 5) is set when symbol
+//                        t is not A/C/G/T (the reference drops such k-mers, kernels.py:23-24)
+//                        or t >= len (padding), so a window is valid iff its k mask bits are 0
+// cw = ldc / 16 + 2 and mw = ldc / 32 + 2 leave one zero word past the last symbol, so a
+// window read never leaves its record.
+struct Packed {
+  const uint32_t *w;
+  int64_t ldp;  // words per record = cw + mw
+  int cw;       // code words
+};
+inline int packed_cw(int64_t ldc) { return (int)(ldc / 16) + 2; }
+inline int packed_mw(int64_t ldc) { return (int)(ldc / 32) + 2; }
+
+// k-mer code (k <= 16) of window a of a packed record; KMG_INVALID if it holds a masked symbol
+__device__ __forceinline__ uint32_t pk_window(const uint32_t *rec, int cw, int a, int k) {
+  const int i = a >> 4, sh = 2 * (a & 15);
+  const uint64_t v = ((uint64_t)rec[i] << 32) | rec[i + 1];
+  const uint32_t code = (uint32_t)((v << sh) >> (64 - 2 * k));
+  const int j = a >> 5;
+  const uint64_t m = ((((uint64_t)rec[cw + j + 1]) << 32) | rec[cw + j]) >> (a & 31);
+  return (m & ((1ull << k) - 1ull)) ? KMG_INVALID : code;
+}
+
+// codes uint8 [n][ldc] (values 0..3 = ACGT, >= 4 other) + lens -> packed records
+hipError_t launch_pack(const uint8_t *codes, const int32_t *lens, int64_t n, int64_t ldc,
+                       int window, uint32_t *packed, hipStream_t s);
+
+hipError_t launch_index_count(const IndexGeom &g, const Packed &pk, uint32_t *bcount,
+                              hipStream_t s);
 // exclusive scan of hist[0..nb) into off[0..nb] (off[nb] = total); cursor = off[0..nb)
 hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, int64_t nb,
                        uint32_t *partials, hipStream_t s);
 size_t scan_partials_words(int64_t nb);
 // place: every block scans the bucket totals itself (block 0 publishes boff[])
-hipError_t launch_index_place(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, const uint32_t *bcount, uint32_t *bcursor,
-                              uint32_t *boff, uint32_t *tmp, hipStream_t s);
+hipError_t launch_index_place(const IndexGeom &g, const Packed &pk, const uint32_t *bcount,
+                              uint32_t *bcursor, uint32_t *boff, uint32_t *tmp, hipStream_t s);
 // fine: per-bucket fine histogram -> off[], ent[]; re-zeroes bcount[]/bcursor[]
 hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
                              uint32_t *off, uint16_t *ent, uint32_t *bcount, uint32_t *bcursor,
                              hipStream_t s);
-hipError_t launch_extract(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                          int64_t ldc, uint32_t *kmers, hipStream_t s);
+hipError_t launch_extract(const IndexGeom &g, const Packed &pk, uint32_t *kmers, hipStream_t s);
 // index build v2 (no device-scope atomics): per-block local sort, then per-bucket gather.
 // hcnt/hstart: nbuckets x nblk (bucket-major); tmp: nblk x cap items.
 size_t index_gather_lds(const IndexGeom &g, int64_t nblk);
-hipError_t launch_index_local(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                              int64_t ldc, int nblk, uint32_t cap, uint32_t *hcnt,
-                              uint32_t *hstart, uint32_t *tmp, hipStream_t s);
+hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, int nblk, uint32_t cap,
+                              uint32_t *hcnt, uint32_t *hstart, uint32_t *tmp, hipStream_t s);
 hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const uint32_t *hcnt,
                                const uint32_t *hstart, const uint32_t *tmp, uint32_t *off,
                                uint16_t *ent, hipStream_t s);
@@ -82,32 +111,20 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
 };
 
-hipError_t launch_gram_spectrum(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                                int64_t ldc, const uint32_t *off, const uint16_t *ent,
-                                int64_t row0, int64_t row1, const OutSpec &o, hipStream_t s);
-hipError_t launch_gram_mismatch1(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                 const uint32_t *off, const uint16_t *ent, int64_t row0,
-                                 int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                 hipStream_t s);
-// all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
-// mismatch (k,1) on the rotated layout (rot=1, nkeys = 4^k)
-hipError_t launch_gram_mismatch1_rot(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                     const uint32_t *off, const uint16_t *ent, uint32_t n_ent,
-                                     int64_t row0, int64_t row1, int w0, int w1, int w2,
-                                     const OutSpec &o, hipStream_t s);
+hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
+                                const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
+                                hipStream_t s);
 // mismatch (k,1), 8 <= k <= 12, on the slot layout (one line per list)
-hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const uint8_t *codes, int64_t ldc,
-                                       const uint4 *slots, const uint32_t *off,
-                                       const uint16_t *ent, int64_t row0, int64_t row1, int w0,
-                                       int w1, int w2, const OutSpec &o, int tri, hipStream_t s);
-// lower triangle := transpose of the upper triangle of a full n x n row-major K
-hipError_t launch_mirror_lower(void *K, int64_t ld, int64_t n, int32_t dtype, hipStream_t s);
+hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, const uint4 *slots,
+                                       const uint32_t *off, const uint16_t *ent, int64_t row0,
+                                       int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                       hipStream_t s);
+// all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
 // max_dist: largest Hamming distance with a non-zero weight (min(2m, k) for mismatch)
-hipError_t launch_diag_hamming(const IndexGeom &g, const uint8_t *codes, const int32_t *lens,
-                               int64_t ldc, const int64_t *wtab, int max_dist, double *diagv,
-                               double *dsq, hipStream_t s);
+hipError_t launch_diag_hamming(const IndexGeom &g, const Packed &pk, const int64_t *wtab,
+                               int max_dist, double *diagv, double *dsq, hipStream_t s);
 
 struct SeqSpec {
   const uint8_t *codes;
@@ -155,6 +172,8 @@ hipError_t launch_alignf(const double *const *K, int p, const double *y, int64_t
 hipError_t launch_shift_scale(const double *K, int64_t ldk, const double *s, double shift,
                               const double *dvec, int64_t n, double *B, int64_t ldb,
                               hipStream_t st);
+// *flag |= 1 when K is not exactly symmetric (flag must be zeroed before)
+hipError_t launch_asymmetry(const double *K, int64_t ld, int64_t n, int *flag, hipStream_t st);
 // KLR IRLS step: s = sqrt(sig(m) sig(-m)), rhs = s * (m + y / sig(-y m))
 hipError_t launch_irls(const double *m, const double *y, int64_t n, double *s, double *rhs,
                        hipStream_t st);

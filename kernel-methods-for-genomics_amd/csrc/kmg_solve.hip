@@ -252,6 +252,36 @@ __global__ void svm_init_kernel(int64_t n, double C, SvmVec V) {
   }
 }
 
+// flag[0] := 1 if K != K^T anywhere (bitwise compare of the upper triangle with the
+// lower): 32 x 32 tiles staged through LDS so both reads are row-contiguous
+__global__ __launch_bounds__(256) void asym_kernel(const double *__restrict__ K, int64_t ld,
+                                                   int64_t n, int *__restrict__ flag) {
+  __shared__ double t[32][33];
+  const int64_t bi = blockIdx.y, bj = blockIdx.x;
+  if (bj < bi) return;  // upper tile (bi, bj) against the transpose of (bj, bi)
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t gi = bj * 32 + r, gj = bi * 32 + tx;
+    if (gi < n && gj < n) t[r][tx] = K[gi * ld + gj];
+  }
+  __syncthreads();
+  bool diff = false;
+  for (int r = ty; r < 32; r += 8) {
+    const int64_t gi = bi * 32 + r, gj = bj * 32 + tx;
+    if (gi < n && gj < n)
+      diff |= __double_as_longlong(K[gi * ld + gj]) != __double_as_longlong(t[tx][r]);
+  }
+  if (__any(diff) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+hipError_t launch_asymmetry(const double *K, int64_t ld, int64_t n, int *flag, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nt = (n + 31) / 32;
+  if (nt > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(asym_kernel, dim3((unsigned)nt, (unsigned)nt), dim3(256), 0, st, K, ld, n, flag);
+  return hipGetLastError();
+}
+
 // a = y o x (the reference's alpha: cvxopt's solution vector)
 __global__ void svm_alpha_kernel(const double *__restrict__ y, int64_t n, const double *x,
                                  double *a) {

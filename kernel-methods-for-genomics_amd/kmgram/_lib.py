@@ -32,7 +32,7 @@ EXPORTS = (
     "kmg_comm_destroy", "kmg_combine", "kmg_combine_device", "kmg_nlck_grad",
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
-    "kmg_svm_fit_device",
+    "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
 )
 
 
@@ -105,6 +105,10 @@ def load():
             "kmg_comm_init": ([P, P, I32, I32], ctypes.c_int),
             "kmg_allgather_rows": ([P, P, I64, I64, I32, P], ctypes.c_int),
             "kmg_comm_destroy": ([P], ctypes.c_int),
+            "kmg_rows_padded": ([I64, I32, I64], I64),
+            "kmg_gram_blocks": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64, I32,
+                                 I32, I64, I32], ctypes.c_int),
+            "kmg_reload_tuning": ([P], ctypes.c_int),
             "kmg_combine": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
             "kmg_combine_device": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
             "kmg_nlck_grad": ([P, P, I32, P, I32, P, I64, I64, P], ctypes.c_int),
@@ -190,6 +194,17 @@ class Context:
     def gram_device(self, params, d_codes, d_lens, n, ldc, row0, row1, out_dtype, d_out, ld):
         check(self.lib.kmg_gram_device(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        row0, row1, out_dtype, d_out, ld))
+
+    def gram_blocks(self, params, d_codes, d_lens, n, ldc, out_dtype, d_out, ld, nranks, rank,
+                    block, gather):
+        """Block-cyclic rows of this rank (+ in-place RCCL all-gather per round when gather)."""
+        check(self.lib.kmg_gram_blocks(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
+                                       out_dtype, d_out, ld, int(nranks), int(rank), int(block),
+                                       1 if gather else 0))
+
+    def reload_tuning(self):
+        """Re-read the KMG_* environment knobs (read once at context creation)."""
+        check(self.lib.kmg_reload_tuning(self._h))
 
     def normalize(self, K):
         skipped = ctypes.c_int32(0)

@@ -45,8 +45,8 @@ def encode(seqs, ldc_align=4):
         ascii_mask = cps < 128
         vals[ascii_mask] = _LUT[cps[ascii_mask]]
         other = np.unique(cps[~ascii_mask])
-        if len(other) > 124:
-            raise ValueError("more than 124 distinct non-ASCII characters in the input")
+        if len(other) > 123:  # codes 132..254: 255 stays the padding code
+            raise ValueError("more than 123 distinct non-ASCII characters in the input")
         remap = {int(c): 132 + t for t, c in enumerate(other)}
         vals[~ascii_mask] = np.array([remap[int(c)] for c in cps[~ascii_mask]], dtype=np.uint8)
     rows = np.repeat(np.arange(n), lens)

@@ -138,6 +138,12 @@ class C_SVM(_GramLearner):
             # the reference leaves self.a unset and fails on its next line (SVM.py:91)
             raise AttributeError("'C_SVM' object has no attribute 'a'")
         y = np.asarray(y_fit, dtype=np.float64)
+        bad = ~np.isin(y, (-1.0, 1.0))
+        if bad.any():
+            # the device QP takes labels in {-1, 1}; the reference hands any y to cvxopt /
+            # L-BFGS-B (SVM.py:66-89) and so does not reject them
+            raise ValueError(f"C_SVM: the Bound column must hold -1 / 1 labels after the "
+                             f"fit() mapping (got {np.unique(y[bad])[:5].tolist()})")
         alpha, self.iterations, self.objective = default_engine().ctx.svm_fit(
             K_fit, y, self.C, self.tol, self.maxiter)
         return alpha

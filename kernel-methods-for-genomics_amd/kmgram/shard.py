@@ -1,9 +1,16 @@
-"""Row sharding of the Gram matrix across ranks (one process per GPU).
+"""Row distribution of the Gram matrix across ranks (one process per GPU).
 
 Every (i, j) entry depends only on the replicated input and the replicated posting
-index, so rank r computes rows [splits[r], splits[r+1]) against all N columns with no
-exchange; `gather` (RCCL, kmg_allgather_rows) assembles the full K on every rank when
-the caller needs it.
+index, so the N x N tile space splits by rows with no exchange until the
+final assembly.  Two layouts:
+
+* contiguous slabs (`even_splits`): rank r computes rows [splits[r], splits[r+1]); used
+  by `store.gram_to_npy` and `kmg_allgather_rows`.
+* block-cyclic (`block_cyclic_ranges`, the kmg_gram_blocks layout): round t holds rows
+  [t*R, (t+1)*R), R = world * block, and rank r owns the block [t*R + r*block, +block).
+  Each round is one contiguous R-row slab whose blocks sit in rank order, so assembling
+  it on every rank is ONE in-place all-gather (send = recv + rank * count) and the
+  rounds pipeline: round t is gathered while round t+1 is computed.
 """
 import math
 
@@ -26,3 +33,39 @@ def weak_scaled_n(n1, world, align=8):
 def rank_rows(n, world, rank):
     s = even_splits(n, world)
     return s[rank], s[rank + 1]
+
+
+def rows_padded(n, world, block):
+    """Rows of the gather buffer: whole rounds of world * block rows (kmg_rows_padded)."""
+    if n <= 0:
+        return 0
+    r = world * block
+    return -(-n // r) * r
+
+
+def block_cyclic_ranges(n, world, rank, block):
+    """[(row0, row1)] of this rank, one per round (clipped to n; may be empty)."""
+    if world < 1 or not 0 <= rank < world or block < 1:
+        raise ValueError("bad world / rank / block")
+    r = world * block
+    out = []
+    for t in range(-(-n // r) if n > 0 else 0):
+        a = min(n, t * r + rank * block)
+        out.append((a, min(n, a + block)))
+    return out
+
+
+def round_slab(t, world, block):
+    """Rows [t*R, (t+1)*R) of round t: the in-place all-gather target of that round."""
+    r = world * block
+    return t * r, (t + 1) * r
+
+
+def default_block(n, world, row_bytes, target_bytes=256 << 20):
+    """Rows per block so one round (world blocks) moves about target_bytes, and there are
+    at least 4 rounds to pipeline when the matrix allows it."""
+    if n <= 0:
+        return 1
+    b = max(1, target_bytes // max(1, world * row_bytes))
+    b = min(b, max(1, -(-n // (4 * world))))
+    return int(b)

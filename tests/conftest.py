@@ -41,3 +41,19 @@ def engine():
     e = GramEngine(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def tune(ctx, monkeypatch):
+    """Set KMG_* tuning variables for one test: the library reads them once per context
+    (kmg_create / kmg_reload_tuning), so every change is followed by a reload."""
+    def set_(**kv):
+        for k, v in kv.items():
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, str(v))
+        ctx.reload_tuning()
+    yield set_
+    monkeypatch.undo()
+    ctx.reload_tuning()

@@ -72,3 +72,72 @@ def test_gloo_world2_protocol(tmp_path):
     d = json.loads(line)
     assert d["rows"] == d["n"] == weak_scaled_n(20000, 2)
     assert d["max"] == 2.0 and d["obj"] == "uid-bytes"
+
+
+ASSEMBLY_WORKER = r"""
+import os, sys, json
+for p in ("kernel-methods-for-genomics_amd", "oracle"):
+    sys.path.insert(0, os.path.join(os.environ["ROOT"], p))
+import numpy as np
+import torch, torch.distributed as dist
+import cref
+from kmgram import encode as E
+from kmgram.shard import block_cyclic_ranges, round_slab, rows_padded
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+n, block = 701, 64
+codes, lens = E.synthetic(n, 101, seed=17)
+full = cref.spectrum(codes, lens, 6).astype(np.int32)
+npad = rows_padded(n, w, block)
+K = torch.full((npad, n), -7, dtype=torch.int32)
+# this rank's blocks, computed by the oracle (the GPU build writes the same rows)
+for a, b in block_cyclic_ranges(n, w, r, block):
+    if b > a:
+        K[a:b] = torch.from_numpy(cref.spectrum(codes, lens, 6, rows=(a, b)).astype(np.int32))
+# one in-place all-gather per round, exactly the kmg_gram_blocks layout: round t is the
+# contiguous slab [t*R, (t+1)*R) and rank q's block sits at q*block rows inside it
+for t in range(npad // (w * block)):
+    s0, s1 = round_slab(t, w, block)
+    parts = list(K[s0:s1].split(block))
+    mine = parts[r].clone()
+    dist.all_gather(parts, mine)
+ok = bool(np.array_equal(K[:n].numpy(), full))
+flag = torch.tensor([1 if ok else 0])
+dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+if r == 0:
+    print(json.dumps({"assembled_equal": int(flag.item()), "rounds": npad // (w * block)}))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_block_cyclic_assembly(tmp_path, world):
+    """Each rank builds its block-cyclic row blocks with the oracle, every round is
+    all-gathered in place (gloo), and the assembled matrix on every rank equals the
+    1-rank full K byte for byte."""
+    pytest.importorskip("torch")
+    script = tmp_path / "a.py"
+    script.write_text(ASSEMBLY_WORKER)
+    env = dict(os.environ, ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), str(script)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["assembled_equal"] == 1 and d["rounds"] >= 4
+
+
+@pytest.mark.parametrize("n,world,block", [(0, 2, 8), (1, 8, 4), (701, 2, 64), (20000, 8, 128),
+                                           (200000, 8, 3125), (99, 3, 7)])
+def test_block_cyclic_cover(n, world, block):
+    from kmgram.shard import block_cyclic_ranges, rows_padded
+    seen = []
+    for r in range(world):
+        for a, b in block_cyclic_ranges(n, world, r, block):
+            assert 0 <= a <= b <= n and b - a <= block
+            seen.extend(range(a, b))
+    assert sorted(seen) == list(range(n))
+    assert rows_padded(n, world, block) % (world * block) == 0
+    assert rows_padded(n, world, block) >= n

@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def dense(monkeypatch):
-    monkeypatch.setenv("KMG_ALGO", "1")
+def dense(tune):
+    tune(KMG_ALGO=1)
 
 
 @pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])
@@ -92,12 +92,12 @@ def test_dense_mismatch_repeats(ctx, dense):
         assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1)), k
 
 
-def test_dense_equals_index_path(ctx, monkeypatch):
+def test_dense_equals_index_path(ctx, tune):
     """The two formulations of the same Gram agree bit for bit."""
     codes, lens = E.synthetic(700, 101, seed=77)
     out = {}
     for algo in ("1", "2"):
-        monkeypatch.setenv("KMG_ALGO", algo)
+        tune(KMG_ALGO=algo)
         out[algo] = (ctx.gram(P.make(L.KMG_SPECTRUM, k=6), codes, lens, L.KMG_I32),
                      ctx.gram(P.make(L.KMG_MISMATCH, k=7, m=1, window=101, normalize=1), codes,
                               lens, L.KMG_F64))
@@ -134,10 +134,10 @@ def test_dense_row_slabs(ctx, dense):
         ctx.dfree(d_lens)
 
 
-def test_auto_picks_dense_for_run_py_kernels(ctx, monkeypatch):
+def test_auto_picks_dense_for_run_py_kernels(ctx, tune):
     """run.py's SP_k4/5 and MM_k4..6_m1 at the production shape (N=9000 train+val+test,
     utils.py:149-153) go through the dense path; checked on oracle rows."""
-    monkeypatch.delenv("KMG_ALGO", raising=False)
+    tune(KMG_ALGO=None)
     codes, lens = E.synthetic(9000, 101, seed=9000)
     ctx.set_timing(True)
     try:

@@ -146,3 +146,21 @@ def test_svm_bad_arguments(ctx):
         ctx.svm_fit(K, np.array([1.0, -1.0, 1.0]), 0.0)
     with pytest.raises(Exception):
         ctx.svm_fit(K, np.array([1.0, 0.0, 1.0]), 1.0)
+
+
+def test_krr_klr_asymmetric_K_match_inv(ctx):
+    """A K that is not exactly symmetric (the reference inverts whatever it is given,
+    KRR.py:33 / KLR.py:55): the device solves the full system (LU), not one triangle."""
+    rng = np.random.default_rng(13)
+    n = 300
+    A = rng.standard_normal((n, 40))
+    K = A @ A.T / 40 + 0.5 * np.eye(n)
+    K[3, 7] += 1e-3  # asymmetric by one entry
+    K[200, 11] -= 2e-3
+    y = np.where(rng.random(n) > 0.5, 1.0, -1.0)
+    lb = 0.05
+    ref = np.linalg.inv(K + lb * n * np.eye(n)) @ y
+    got = ctx.krr_solve(K, y, lb)
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+    sym = ctx.krr_solve((K + K.T) / 2, y, lb)
+    assert not np.allclose(sym, got, rtol=1e-9, atol=0)  # the triangle read would differ

@@ -1,0 +1,130 @@
+"""GPU tests of the multi-GPU build path on one device: kmg_gram_blocks (block-cyclic rows,
+index built once, Gram launched per round) and its in-place RCCL all-gather on a 1-rank
+communicator.  Two ranks' block sets written into one buffer must assemble the full K
+exactly (the rows each rank owns are disjoint and cover K).  Argument checks of the
+device entry points ride along."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from kmgram import _lib as L
+from kmgram import encode as E
+from kmgram import params as P
+from kmgram.shard import block_cyclic_ranges, rows_padded
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    (P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32),
+    (P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64),
+    (P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32),
+    (P.make(L.KMG_WD, d=5), L.KMG_F64),
+]
+
+
+@pytest.fixture(scope="module")
+def data(ctx):
+    codes, lens = E.synthetic(1500, 101, seed=71)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    yield codes, lens, d_codes, d_lens
+    ctx.dfree(d_codes)
+    ctx.dfree(d_lens)
+
+
+def _run_blocks(ctx, data, params, dt, world, ranks, block, gather):
+    codes, lens, d_codes, d_lens = data
+    n, ldc = codes.shape
+    npad = rows_padded(n, world, block)
+    assert npad == L.load().kmg_rows_padded(n, world, block)
+    esz = np.dtype(L.DTYPES[dt]).itemsize
+    d_out = ctx.dmalloc(npad * n * esz)
+    try:
+        ctx.memset(d_out, 0xA5, npad * n * esz)
+        for r in ranks:
+            ctx.gram_blocks(params, d_codes, d_lens, n, ldc, dt, d_out, n, world, r, block, gather)
+        ctx.synchronize()
+        out = np.empty((n, n), dtype=L.DTYPES[dt])
+        ctx.d2h(out, d_out)
+        return out
+    finally:
+        ctx.dfree(d_out)
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("world,block", [(1, 1500), (1, 333), (2, 256), (3, 100), (8, 64)])
+def test_blocks_union_equals_full(ctx, data, case, world, block):
+    params, dt = CASES[case]
+    codes, lens = data[0], data[1]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data, params, dt, world, range(world), block, gather=False)
+    assert np.array_equal(got, full)
+
+
+def test_block_cyclic_ranges_match_library(ctx, data):
+    """The Python layout helper (used by bench.py) and the library agree: rank 1 of 3 writes
+    exactly the rows block_cyclic_ranges lists, nothing else."""
+    params, dt = CASES[0]
+    codes, lens = data[0], data[1]
+    n = codes.shape[0]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data, params, dt, 3, [1], 100, gather=False)
+    mine = np.zeros(n, dtype=bool)
+    for a, b in block_cyclic_ranges(n, 3, 1, 100):
+        mine[a:b] = True
+    assert np.array_equal(got[mine], full[mine])
+    assert np.all(got[~mine].view(np.uint32) == 0xA5A5A5A5)
+
+
+def test_blocks_gather_single_rank_comm(ctx, data):
+    """gather=1 on a 1-rank RCCL communicator: the comm-stream / event ordering path with
+    in-place ncclAllGather per round; the result is the full K on the context stream."""
+    uid = L.Context.unique_id()
+    ctx.comm_init(uid, 1, 0)
+    try:
+        for params, dt in CASES[:2]:
+            full = ctx.gram(params, data[0], data[1], dt)
+            got = _run_blocks(ctx, data, params, dt, 1, [0], 200, gather=True)
+            assert np.array_equal(got, full)
+        with pytest.raises(L.KmgError):  # communicator size must match
+            _run_blocks(ctx, data, CASES[0][0], CASES[0][1], 2, [0], 200, gather=True)
+    finally:
+        ctx.comm_destroy()
+
+
+def test_allgather_rows_validates_splits(ctx):
+    uid = L.Context.unique_id()
+    ctx.comm_init(uid, 1, 0)
+    d = ctx.dmalloc(64 * 64 * 4)
+    try:
+        for bad in ([1, 64], [0, 63], [0, 65]):
+            with pytest.raises(L.KmgError):
+                ctx.allgather_rows(d, 64, 64, L.KMG_I32, bad)
+        with pytest.raises(L.KmgError):
+            ctx.allgather_rows(d, 64, 32, L.KMG_I32, [0, 64])  # ld < n
+        ctx.allgather_rows(d, 64, 64, L.KMG_I32, [0, 64])
+        ctx.synchronize()
+    finally:
+        ctx.dfree(d)
+        ctx.comm_destroy()
+
+
+def test_mismatch_device_rows_narrower_than_window(ctx):
+    """kmg_gram_device with code rows of 100 < the 101 window: EINVAL, no kernel reads past
+    a row."""
+    codes, lens = E.synthetic(16, 100, seed=3)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(16 * 16 * 8)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        for params in (P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1),
+                       P.make(L.KMG_GAPPY, k=1, g=0)):
+            with pytest.raises(L.KmgError) as e:
+                ctx.gram_device(params, d_codes, d_lens, 16, 100, 0, 16, L.KMG_F64, d_out, 16)
+            assert e.value.status == L.KMG_EINVAL
+    finally:
+        for p in (d_out, d_codes, d_lens):
+            ctx.dfree(p)

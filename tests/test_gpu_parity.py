@@ -105,54 +105,34 @@ def test_spectrum_k_range(ctx, k):
     assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, k))
 
 
-def test_spectrum_ragged_and_chunks(ctx, monkeypatch):
+def test_spectrum_ragged_and_chunks(ctx, tune):
     rng = np.random.default_rng(5)
     seqs = ["".join(rng.choice(list("ACGTN"), p=[.24, .24, .24, .24, .04], size=rng.integers(0, 140)))
             for _ in range(700)]
     codes, lens = E.encode(seqs)
     ref = cref.spectrum(codes, lens, 4)
     for chunk in ("24576", "104", "256"):
-        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
+        tune(KMG_SP_CHUNK=chunk, KMG_ALGO=2)
         K = ctx.gram(P.make(L.KMG_SPECTRUM, k=4), codes, lens, L.KMG_I32)
         assert np.array_equal(K.astype(np.int64), ref), chunk
 
 
-@pytest.mark.parametrize("G", ["1", "2", "4"])
-def test_spectrum_lane_groups(ctx, monkeypatch, G):
-    """Every compiled lanes-per-posting-list width of the posting-list spectrum kernel,
-    on ragged + non-ACGT input and at k=8."""
-    monkeypatch.setenv("KMG_SP_G", G)
-    monkeypatch.setenv("KMG_ALGO", "2")
-    rng = np.random.default_rng(6)
-    seqs = ["".join(rng.choice(list("ACGTN"), p=[.24, .24, .24, .24, .04], size=rng.integers(0, 120)))
-            for _ in range(500)]
-    codes, lens = E.encode(seqs)
-    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=4), codes, lens, L.KMG_I32)
-    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 4))
-    codes, lens = E.synthetic(3000, 101, seed=8)
-    codes[7] = 0  # one list of 94 * (rows holding AAAAAAAA) entries
-    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
-    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 8))
-
-
 @pytest.mark.parametrize("v2", ["0", "1"])
-def test_index_builds(ctx, monkeypatch, v2):
+def test_index_builds(ctx, tune, v2):
     """Both posting-index builds (v1: atomics-based MSD partition; v2: per-block local
     sort + per-bucket gather) give bit-identical Grams, over chunkings and block sizes."""
-    monkeypatch.setenv("KMG_IDX_V2", v2)
-    monkeypatch.setenv("KMG_ALGO", "2")
+    tune(KMG_IDX_V2=v2, KMG_ALGO=2)
     codes, lens = E.synthetic(2500, 101, seed=91)
     codes[3] = 0
     ref = cref.spectrum(codes, lens, 8)
     for chunk, seqs_pb in (("24576", "80"), ("700", "7"), ("24576", "1")):
-        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
-        monkeypatch.setenv("KMG_IDX_SEQS", seqs_pb)
+        tune(KMG_SP_CHUNK=chunk, KMG_IDX_SEQS=seqs_pb)
         K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
         assert np.array_equal(K.astype(np.int64), ref), (chunk, seqs_pb)
     c2, l2 = codes[:1200], lens[:1200]
     refm = cref.mismatch_raw(c2, l2, 9, 1)
     for seqs_pb in ("80", "7"):
-        monkeypatch.setenv("KMG_IDX_SEQS", seqs_pb)
+        tune(KMG_IDX_SEQS=seqs_pb)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), c2, l2, L.KMG_I32)
         assert np.array_equal(raw.astype(np.int64), refm), seqs_pb
 
@@ -162,19 +142,6 @@ def test_spectrum_long_sequences_unpacked(ctx):
     codes, lens = E.synthetic(64, 400, seed=9)
     K = ctx.gram(P.make(L.KMG_SPECTRUM, k=5), codes, lens, L.KMG_I32)
     assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 5))
-
-
-@pytest.mark.parametrize("persist", ["1", "2"])
-def test_spectrum_persistent_blocks(ctx, monkeypatch, persist):
-    """KMG_SP_PERSIST: resident blocks loop over (row, chunk) items (several per block)."""
-    monkeypatch.setenv("KMG_SP_PERSIST", persist)
-    codes, lens = E.synthetic(5000, 101, seed=31)
-    for chunk in ("24576", "1000"):
-        monkeypatch.setenv("KMG_SP_CHUNK", chunk)
-        K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
-        for r in (0, 2047, 2048, 4999):
-            assert np.array_equal(K[r].astype(np.int64), cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0]), (chunk, r)
-        assert np.array_equal(K, K.T)
 
 
 def test_mismatch_k9_n20000(ctx):
@@ -202,72 +169,28 @@ def test_mismatch_params(ctx, k, m):
     assert np.array_equal(K, cref.mismatch_rows(codes, lens, k, m))
 
 
-MM_LAUNCH_CONFIGS = [
-    # (KMG_MM_VARIANT, KMG_MM_G, KMG_MM_V, KMG_MM_U, KMG_MM_D): every compiled instance family
-    ("7", "2", None, None, "2"), ("7", "2", None, None, "3"), ("7", "2", None, None, "4"),
-    ("7", "1", None, None, "2"), ("7", "1", None, None, "3"), ("7", "4", None, None, "2"),
-    ("7", "8", None, None, "2"), ("7", "4", None, None, "3"),
-    ("6", "4", "4", "2", None), ("6", "2", "8", "2", None), ("6", "1", "8", "4", None),
-    ("6", "8", "4", "1", None), ("5", "1", None, "24", None), ("5", "2", None, "8", None),
-    ("4", "4", None, "8", None), ("3", "4", None, None, None), ("2", "8", None, None, None),
-]
-
-
-@pytest.mark.parametrize("variant,g,v,u,d", MM_LAUNCH_CONFIGS)
-def test_mismatch_chunked(ctx, monkeypatch, variant, g, v, u, d):
-    codes, lens = E.synthetic(900, 101, seed=11)
-    ref = cref.mismatch_raw(codes, lens, 9, 1)
-    monkeypatch.setenv("KMG_MM_VARIANT", variant)
-    for name, val in (("KMG_MM_G", g), ("KMG_MM_V", v), ("KMG_MM_U", u), ("KMG_MM_D", d)):
-        if val is None:
-            monkeypatch.delenv(name, raising=False)
-        else:
-            monkeypatch.setenv(name, val)
-    for chunk in ("64", "128", "10240"):
-        monkeypatch.setenv("KMG_MM_CHUNK", chunk)
-        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
-                       L.KMG_I32)
-        assert np.array_equal(raw.astype(np.int64), ref), (variant, g, v, u, d, chunk)
-
-
-# (KMG_MM_SLOTV, KMG_MM_D, KMG_MM_TRI): v7 slot kernel, v8 with tested slots (upper
-# triangle + mirror, or full rows), v8 with sentinel slots
-SLOT_KERNELS = [("0", "2", "1"), ("1", "2", "1"), ("1", "3", "1"), ("1", "2", "0"),
-                ("2", "2", "1"), ("2", "3", "1"), ("3", "2", "1"), ("3", "3", "0"),
-                ("4", "2", "0"), ("4", "3", "1")]
-
-
-@pytest.mark.parametrize("slotv,d,tri", SLOT_KERNELS)
 @pytest.mark.parametrize("k", [8, 9, 10, 11, 12])
-def test_mismatch_slots_k_range(ctx, monkeypatch, k, slotv, d, tri):
-    """Slot layout (the default for 8 <= k <= 12) at every compiled k, every slot kernel."""
-    monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
-    monkeypatch.setenv("KMG_MM_SLOTV", slotv)
-    monkeypatch.setenv("KMG_MM_D", d)
-    monkeypatch.setenv("KMG_MM_TRI", tri)
+def test_mismatch_slots_k_range(ctx, tune, k):
+    """Slot layout (the path for 8 <= k <= 12) at every compiled k, raw and normalised,
+    over several column chunkings (slot tables grow with 4^(k-1) per chunk: k >= 10 stays
+    single-chunk here)."""
     codes, lens = E.synthetic(400, 101, seed=50 + k)
-    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
-                   L.KMG_I32)
-    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1))
+    ref = cref.mismatch_raw(codes, lens, k, 1)
+    for chunk in (("64", "300", "20480") if k <= 9 else ("20480",)):
+        tune(KMG_MM_CHUNK=chunk)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), ref), chunk
     Kn = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
                   L.KMG_F64)
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
-    for chunk in (("64", "300") if k <= 9 else ()):  # several column chunks (slot tables
-        # grow with 4^(k-1) per chunk: k >= 10 stays single-chunk here)
-        monkeypatch.setenv("KMG_MM_CHUNK", chunk)
-        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
-                       L.KMG_I32)
-        assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, k, 1)), chunk
 
 
-@pytest.mark.parametrize("slotv", ["0", "1", "2", "3", "4"])
-def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch, slotv):
+def test_mismatch_slots_overflow_and_big_groups(ctx, tune):
     """Slot groups longer than the 60 inline entries (CSR tail) and groups of >= 65535
     entries (16-bit header overflow, CSR only): 720 poly-A rows put 720 * 93 = 66960
     occurrences in the AAAAAAAAA groups of every copy."""
-    monkeypatch.delenv("KMG_MM_VARIANT", raising=False)
-    monkeypatch.setenv("KMG_MM_SLOTV", slotv)
-    monkeypatch.setenv("KMG_MM_CHUNK", "20480")
+    tune(KMG_MM_CHUNK=20480)
     codes, lens = E.synthetic(760, 101, seed=61)
     codes[:720] = 0
     codes[700] = np.tile([0, 1], 51)[:101]
@@ -278,15 +201,6 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, monkeypatch, slotv):
     assert np.array_equal(raw[690:760].astype(np.int64), ref)
     assert np.array_equal(raw[:5].astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1, rows=(0, 5)))
     assert np.array_equal(raw, raw.T)
-
-
-def test_mismatch_unmatched_launch_config_fails_loudly(ctx, monkeypatch):
-    codes, lens = E.synthetic(64, 101, seed=11)
-    monkeypatch.setenv("KMG_MM_VARIANT", "6")
-    monkeypatch.setenv("KMG_MM_G", "3")
-    with pytest.raises(L.KmgError):
-        ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
-                 L.KMG_I32)
 
 
 def test_mismatch_stress_repeats(ctx):
