@@ -98,7 +98,8 @@ enum {
 // kmg_reload_tuning, never per launch.
 struct Tuning {
   int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
-  int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index
+  int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
+  int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
   int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
@@ -128,6 +129,8 @@ void read_tuning(Tuning &t) {
   t.idx_threads = env_or("KMG_IDX_THREADS", d.idx_threads);
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
+  t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
+  if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
 }  // namespace
@@ -141,6 +144,7 @@ struct kmg_ctx {
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
+  DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -387,6 +391,34 @@ int upload_masks(kmg_ctx *c, int k, int m) {
   return KMG_OK;
 }
 
+// Columns per chunk of the pair (drop-two) table: the fewest expected 128-byte lines per
+// row over all chunkings whose LDS accumulator fits (<= 38400 int32 columns) and whose mean
+// group stays <= 190 entries (groups above 255 take the slow wide path).  Lines of a
+// group of n ~ Poisson(mean) entries: ceil((16 + 2n) / 128).
+int pair_chunk(int64_t n, int pmax, int k, int cap) {
+  const double keys = (double)pow4(k - 2);
+  const int64_t max_chunk = std::min<int64_t>(cap > 0 ? cap : 38400, 38400);
+  int64_t best = std::min<int64_t>(n, max_chunk);
+  double best_lines = 1e300;
+  for (int64_t nch = (n + max_chunk - 1) / max_chunk; nch <= (n + max_chunk - 1) / max_chunk + 16; ++nch) {
+    const int64_t ch = (n + nch - 1) / nch;
+    const double mean = (double)ch * pmax / keys;
+    if (mean > 190.0 && nch < (n + 7) / 8) continue;
+    double e = 0.0, pr = std::exp(-mean), cdf = 0.0;  // E[ceil((16 + 2X) / 128)], X ~ Poisson
+    for (int x = 0; x < 2000 && cdf < 1.0 - 1e-12; ++x) {
+      if (x > 0) pr *= mean / x;
+      cdf += pr;
+      e += pr * (x == 0 ? 0.0 : std::ceil((16.0 + 2.0 * x) / 128.0));
+    }
+    const double lines = (double)nch * e;
+    if (lines < best_lines) {
+      best_lines = lines;
+      best = ch;
+    }
+  }
+  return (int)std::max<int64_t>(8, (best + 7) & ~7LL);
+}
+
 // Row ranges of one Gram call: every range [row0, row1) x all n columns is written at
 // `out` (row row0); the index / features / diagonal are built once per call.  `after(q)`
 // runs once range q's Gram launch is enqueued (the multi-GPU path hangs its all-gather of a
@@ -418,7 +450,7 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
                OutSpec o, bool normalize, const AfterRange &after) {
   const int dp = (int)std::max<int64_t>(128, pow4(k));
   KMG_TRY(upload_masks(c, k, m));
-  const int64_t rows_alloc = ((n + 127) & ~127LL) + 128;
+  const int64_t rows_alloc = ((n + 255) & ~255LL) + 256;  // 256-row GEMM tiles, zero pad
   KMG_TRY(c->feat.ensure((size_t)rows_alloc * dp));
   KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
   KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
@@ -461,7 +493,7 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
                          hipMemcpyHostToDevice, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));  // pageable source
   c->masks_k = -1;                           // the neighbour-mask cache no longer holds masks
-  const int64_t rows_alloc = ((n + 127) & ~127LL) + 128;
+  const int64_t rows_alloc = ((n + 255) & ~255LL) + 256;  // 256-row GEMM tiles, zero pad
   KMG_TRY(c->feat.ensure((size_t)rows_alloc * dp));
   KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
   KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)(n > 0 ? n : 1)));
@@ -523,8 +555,15 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
-      const bool use_slots = mm && p->m == 1 && k >= 8 && k <= 12;  // drop-one-letter slots
-      const bool use_index = (exact && k <= 12) || use_slots;
+      // mismatch m = 1: drop-two pair table (auto for k = 10, 11: fewest posting lines per
+      // row) or the drop-one slot table (auto for k = 8, 9 and 12).  At k = 9 the pair kernel
+      // fetches 24% fewer bytes but issues 2x the VALU/SALU work and loses (6.3 vs 4.45 ms,
+      // profiles/r02_mm_pmc.txt); at k = 12 the 66 x 4^10 pair groups cost more to build.
+      const int form = c->tune.mm_form;
+      const bool s1 = mm && p->m == 1;
+      const bool use_pairs = s1 && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
+      const bool use_slots = s1 && !use_pairs && k >= 8 && k <= 12 && form != 2;
+      const bool use_index = (exact && k <= 12) || use_slots || use_pairs;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
@@ -583,6 +622,55 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           return hipSuccess;
         });
       }
+      if (use_pairs) {
+        // exact k-mer index over the mismatch window (kernels.py:171), then the pair table
+        // assembled from it
+        g.copies = 1;
+        g.nkeys = (uint32_t)pow4(k);
+        choose_chunks(g, pair_chunk(n, g.pmax, k, c->tune.mm_chunk));
+        KMG_TRY(build_index(c, g, pkd));
+        PairGeom pg{};
+        pg.k = k;
+        pg.nchunks = g.nchunks;
+        pg.chunk = g.chunk;
+        pg.nkeys2 = (uint32_t)pow4(k - 2);
+        for (int pp = 0; pp < k; ++pp)
+          for (int qq = pp + 1; qq < k; ++qq) pg.pq[pg.npairs++] = (uint16_t)(pp | (qq << 8));
+        const int64_t nrec = pg.nrec();
+        const int64_t nlines = pair_lines_bound(pg, n * g.pmax);
+        if (nlines * 128 >= 0xFFFFFFF0LL)
+          return fail(KMG_EUNSUPPORTED, "pair table too large for 32-bit offsets");
+        KMG_TRY(c->pr_summary.ensure(sizeof(uint32_t) * 8 * (size_t)nrec));
+        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nrec)));
+        KMG_TRY(c->pr_lines.ensure((size_t)nlines * 128));
+        {
+          StageTimer t(c, ST_SLOTS);
+          KMG_HIP(launch_pair_count(pg, c->off.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
+                                    c->pr_rtot.as<uint32_t>(), c->stream));
+          KMG_HIP(launch_scan(c->pr_rtot.as<uint32_t>(), c->pr_rbase.as<uint32_t>(),
+                              c->pr_cursor.as<uint32_t>(), nrec, c->partials.as<uint32_t>(),
+                              c->stream));
+          KMG_HIP(launch_pair_pack(pg, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                   c->pr_rbase.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
+                                   c->pr_lines.as<uint4>(), c->stream));
+        }
+        if (p->normalize) {
+          KMG_TRY(upload_wtab(c, w));
+          KMG_TRY(diag_hamming(c, g, pkd));
+          o.normalize = 1;
+          o.diagv = c->diagv.as<double>();
+          o.dsq = c->dsq.as<double>();
+        }
+        return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          return launch_gram_mismatch1_pairs(pg, g, pkd, c->pr_summary.as<uint32_t>(),
+                                             c->pr_lines.as<uint4>(), nlines,
+                                             c->off.as<uint32_t>(), c->ent.as<uint16_t>(), r0,
+                                             r1, (int)w[0], (int)w[1], (int)w[2], oq, c->stream);
+        });
+      }
       if (exact) {
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
@@ -593,7 +681,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.nkeys = (uint32_t)pow4(k);
         // mean list (4-bin group) length <= 40: inline in one 128-byte line
         const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
-        choose_chunks(g, (int)std::max<int64_t>(8, std::min<int64_t>({(int64_t)c->tune.mm_chunk, cap, 64000})));
+        const int64_t lim = c->tune.mm_chunk > 0 ? c->tune.mm_chunk : 20480;
+        choose_chunks(g, (int)std::max<int64_t>(8, std::min<int64_t>({lim, cap, 64000})));
       }
       KMG_TRY(build_index(c, g, pkd));
       if (use_slots) {
@@ -754,6 +843,7 @@ int kmg_destroy(kmg_ctx *c) {
   DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
+                    &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info};
   for (DevBuf *b : bufs) b->release();

@@ -12,9 +12,12 @@
 // sequence has at most 127 windows (host check), so F*F^T accumulated in int32 is exact.
 // Large k (sparse F, 4^k >> windows) goes through the posting-list kernels instead.
 //
-// Layout in HBM: F int8 [rows_alloc][dp], dp = 4^k rounded up to 128, rows_alloc >= n +
-// 128 with the padding rows zero, so tile loads never need bounds checks.
+// Layout in HBM: F int8 [rows_alloc][dp], dp = 4^k rounded up to 128, rows_alloc >= n
+// rounded up to 256, + 256, with the padding rows zero, so tile loads never need bounds
+// checks.
 #include "kmg_internal.h"
+
+#include <type_traits>
 
 namespace kmg {
 
@@ -87,142 +90,210 @@ __global__ __launch_bounds__(256) void dense_feat_kernel(
 }
 
 // ------------------------------------------------------------------ GEMM
-// K[r][c] = sum_b F[r][b] F[c][b] over a 128 x 128 output tile per workgroup (4 waves,
-// 2 x 2 of them, 64 x 64 each = 2 x 2 v_mfma_i32_32x32x32_i8 tiles).  The reduction
-// runs over 128-byte stages of F staged in LDS (double buffered, XOR-swizzled 16-byte
-// chunks so the fragment reads of 32 consecutive rows hit distinct banks).
+// K[r][c] = sum_b F[r][b] F[c][b] over a 256 x 256 output tile per workgroup: 8 waves in a
+// 2 x 4 grid, each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles (128 accumulator
+// registers).  The reduction runs over 64-byte stages of F staged in LDS (double
+// buffered; the 16-byte chunk of row r sits at chunk ^ ((r >> 2) & 3), so the fragment
+// reads of 16 consecutive rows hit 16 distinct bank quads).
 //
 // Both operands are rows of F, so A and B fragments are loaded by the same code:
 // whatever order the instruction sums its 32 k-values in, A and B use the same lane/
 // element -> k map, and the tile is the full dot product.  Output map (gfx950, every
 // dtype): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5).
-constexpr int DT_BM = 128;
-constexpr int DT_BK = 128;                       // bytes of F per stage
-constexpr int DT_STAGE = 2 * DT_BM * DT_BK;      // A + B bytes per stage
+//
+// SYM (full square K): only tiles tm <= tn are computed (half the MFMA work and half the
+// F panel traffic); an off-diagonal tile is written twice, directly and transposed (K is
+// symmetric and the fused normalisation K_ij / (d_i * d_j) is too, bit for bit).
+// Epilogue: each wave stages one 32 x 32 sub-tile at a time in LDS and writes rows (and,
+// for SYM, columns) of it with 16-byte non-temporal stores.
+constexpr int DT_BM = 256;
+constexpr int DT_BK = 64;                         // bytes of F per stage
+constexpr int DT_STAGE = 2 * DT_BM * DT_BK;       // A + B bytes per stage (32 KB)
+constexpr int DT_EPI = 9 * 1024;                  // LDS bytes per wave for the epilogue
+constexpr int DT_LDS = 8 * DT_EPI > 2 * DT_STAGE ? 8 * DT_EPI : 2 * DT_STAGE;
 
-__device__ __forceinline__ int swz(int row, int c16) { return row * DT_BK + ((c16 ^ (row & 7)) << 4); }
+__device__ __forceinline__ int swz(int row, int c16) { return row * DT_BK + ((c16 ^ ((row >> 2) & 3)) << 4); }
 
-template <int DT>
-__device__ __forceinline__ void dense_store(const OutSpec &o, bool norm, int64_t row0, int64_t gr,
-                                            int64_t gc, int v) {
-  if constexpr (DT == KMG_I32) {
-    __builtin_nontemporal_store(v, (int32_t *)o.out + (gr - row0) * o.ld + gc);
-  } else {
-    double r = (double)v;
-    if (norm) r = (gr == gc) ? 1.0 : r / (o.dsq[gr] * o.dsq[gc]);
-    if constexpr (DT == KMG_F64)
-      __builtin_nontemporal_store(r, (double *)o.out + (gr - row0) * o.ld + gc);
-    else
-      __builtin_nontemporal_store((float)r, (float *)o.out + (gr - row0) * o.ld + gc);
-  }
+template <typename T>
+__device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
+  typedef int v4i_t __attribute__((ext_vector_type(4)));
+  v4i_t x;
+  __builtin_memcpy(&x, v, 16);
+  __builtin_nontemporal_store(x, (v4i_t *)p);
 }
 
-// Tile order: blocks are dispatched round-robin over the 8 XCDs, so block b is remapped
-// to logical tile (b % 8) * per_xcd + b / 8 — each XCD walks a contiguous run of
-// logical tiles — and logical tiles run down GROUP tile-rows before moving one
-// tile-column right, so the workgroups resident on one XCD share a few F panels in its L2.
-template <int DT>
-__global__ __launch_bounds__(256, 2) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
+template <int DT, bool SYM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
                                                             int64_t n, int64_t row0, int64_t rows,
-                                                            int tiles_m, int tiles_n, OutSpec o) {
+                                                            int tiles_m, int tiles_n, int64_t ntiles,
+                                                            OutSpec o) {
+  using T = typename std::conditional<DT == KMG_F64, double,
+                                      typename std::conditional<DT == KMG_F32, float, int32_t>::type>::type;
   extern __shared__ __align__(16) uint8_t lds[];
-  constexpr int GROUP = 8;
-  const int total = tiles_m * tiles_n;
-  const int per_xcd = (int)((gridDim.x + 7) >> 3);
-  const int logical = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-  if (logical >= total) return;
-  const int band = logical / (GROUP * tiles_n);
-  const int in_band = logical - band * GROUP * tiles_n;
-  const int band_rows = min(GROUP, tiles_m - band * GROUP);
-  const int tm = band * GROUP + in_band % band_rows;
-  const int tn = in_band / band_rows;
+  const int64_t per_xcd = ((int64_t)gridDim.x + 7) >> 3;
+  const int64_t logical = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (logical >= ntiles) return;
+  int tm, tn;
+  if constexpr (SYM) {  // row-band-major over tm <= tn: band tm holds tiles_n - tm tiles
+    const double Tn = (double)tiles_n;
+    int64_t t = (int64_t)((2.0 * Tn + 1.0 - sqrt((2.0 * Tn + 1.0) * (2.0 * Tn + 1.0) - 8.0 * (double)logical)) * 0.5);
+    auto cum = [&](int64_t b) { return b * tiles_n - b * (b - 1) / 2; };
+    while (t > 0 && cum(t) > logical) --t;
+    while (cum(t + 1) <= logical) ++t;
+    tm = (int)t;
+    tn = (int)(tm + (logical - cum(t)));
+  } else {
+    tm = (int)(logical / tiles_n);
+    tn = (int)(logical - (int64_t)tm * tiles_n);
+  }
   const int64_t rbase = row0 + (int64_t)tm * DT_BM;
   const int64_t cbase = (int64_t)tn * DT_BM;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave >> 2, wn = wave & 3;
 
-  // global -> register staging: 4 x 16 B of A and 4 x 16 B of B per thread per stage
-  const int8_t *gA = F + rbase * (int64_t)dp;
-  const int8_t *gB = F + cbase * (int64_t)dp;
-  uint4 ra[4], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tid + 256 * q;
-      const int r = c >> 3, c16 = c & 7;
-      ra[q] = *(const uint4 *)(gA + (int64_t)r * dp + k0 + c16 * 16);
-      rb[q] = *(const uint4 *)(gB + (int64_t)r * dp + k0 + c16 * 16);
-    }
-  };
-  auto lstore = [&](int buf) {
-    uint8_t *sA = lds + buf * DT_STAGE;
-    uint8_t *sB = sA + DT_BM * DT_BK;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tid + 256 * q;
-      const int r = c >> 3, c16 = c & 7;
-      *(uint4 *)(sA + swz(r, c16)) = ra[q];
-      *(uint4 *)(sB + swz(r, c16)) = rb[q];
-    }
-  };
+  // global -> register staging: 2 x 16 B of A and 2 x 16 B of B per thread per stage
+  const int lr = tid >> 2, lc = tid & 3;
+  const int8_t *gA0 = F + (rbase + lr) * (int64_t)dp + lc * 16;
+  const int8_t *gA1 = gA0 + 128 * (int64_t)dp;
+  const int8_t *gB0 = F + (cbase + lr) * (int64_t)dp + lc * 16;
+  const int8_t *gB1 = gB0 + 128 * (int64_t)dp;
+  const int so0 = swz(lr, lc), so1 = swz(lr + 128, lc);
 
-  v16i acc[2][2];
+  v16i acc[4][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (v16i){};
 
   const int nst = dp / DT_BK;
-  gload(0);
-  lstore(0);
+  uint4 ra0 = *(const uint4 *)gA0, ra1 = *(const uint4 *)gA1;
+  uint4 rb0 = *(const uint4 *)gB0, rb1 = *(const uint4 *)gB1;
+  {
+    uint8_t *sA = lds, *sB = lds + DT_BM * DT_BK;
+    *(uint4 *)(sA + so0) = ra0;
+    *(uint4 *)(sA + so1) = ra1;
+    *(uint4 *)(sB + so0) = rb0;
+    *(uint4 *)(sB + so1) = rb1;
+  }
   __syncthreads();
   const int fr = lane & 31, fh = lane >> 5;
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nst) gload((st + 1) * DT_BK);
+    const bool more = st + 1 < nst;
+    if (more) {
+      const int k0 = (st + 1) * DT_BK;
+      ra0 = *(const uint4 *)(gA0 + k0);
+      ra1 = *(const uint4 *)(gA1 + k0);
+      rb0 = *(const uint4 *)(gB0 + k0);
+      rb1 = *(const uint4 *)(gB1 + k0);
+    }
     const uint8_t *sA = lds + buf * DT_STAGE;
     const uint8_t *sB = sA + DT_BM * DT_BK;
 #pragma unroll
     for (int s = 0; s < DT_BK / 32; ++s) {
       const int c16 = 2 * s + fh;
-      v4i a[2], b[2];
+      v4i a[4], b[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = *(const v4i *)(sA + swz(wm * 64 + t * 32 + fr, c16));
-        b[t] = *(const v4i *)(sB + swz(wn * 64 + t * 32 + fr, c16));
-      }
+      for (int x = 0; x < 4; ++x) a[x] = *(const v4i *)(sA + swz(wm * 128 + x * 32 + fr, c16));
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int y = 0; y < 2; ++y) b[y] = *(const v4i *)(sB + swz(wn * 64 + y * 32 + fr, c16));
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
           acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[y], acc[x][y], 0, 0, 0);
     }
-    if (st + 1 < nst) {
-      lstore(buf ^ 1);
+    if (more) {
+      uint8_t *dA = lds + (buf ^ 1) * DT_STAGE, *dB = dA + DT_BM * DT_BK;
+      *(uint4 *)(dA + so0) = ra0;
+      *(uint4 *)(dA + so1) = ra1;
+      *(uint4 *)(dB + so0) = rb0;
+      *(uint4 *)(dB + so1) = rb1;
       __syncthreads();
     }
   }
+  __syncthreads();  // staging buffers are reused by the epilogue
 
   const bool norm = DT != KMG_I32 && o.normalize && o.diagv[0] != 1.0;
   const int64_t rend = row0 + rows;
+  constexpr int PITCH = sizeof(T) == 8 ? 34 : 36;  // elements per LDS tile row (16-B aligned)
+  constexpr int V = 16 / (int)sizeof(T);                                       // per 16 B
+  T *tile = (T *)(lds + wave * DT_EPI);
+  const bool mirror = SYM && tm != tn;
+  const bool vec_ok = ((o.ld * (int64_t)sizeof(T)) & 15) == 0 && (((uintptr_t)o.out) & 15) == 0;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < 4; ++x) {
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
-      const int64_t gc = cbase + wn * 64 + y * 32 + fr;
-      if (gc >= n) continue;
+      const int64_t gr0 = rbase + wm * 128 + x * 32, gc0 = cbase + wn * 64 + y * 32;
+      if (gr0 >= rend || gc0 >= n) continue;  // wave-uniform
+      const int64_t gc = gc0 + fr;
+      const double dc = (norm && gc < n) ? o.dsq[gc] : 1.0;
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const int64_t gr = rbase + wm * 64 + x * 32 + (g & 3) + 8 * (g >> 2) + 4 * fh;
-        if (gr < rend) dense_store<DT>(o, norm, row0, gr, gc, acc[x][y][g]);
+        const int r = (g & 3) + 8 * (g >> 2) + 4 * fh;
+        const int64_t gr = gr0 + r;
+        const int v = acc[x][y][g];
+        T val;
+        if constexpr (DT == KMG_I32) {
+          val = v;
+        } else {
+          double d = (double)v;
+          if (norm) d = (gr == gc) ? 1.0 : (gr < rend && gc < n ? d / (o.dsq[gr] * dc) : 0.0);
+          val = (T)d;
+        }
+        tile[r * PITCH + fr] = val;
       }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
+      __builtin_amdgcn_wave_barrier();
+      // rows of the sub-tile: 32 rows x (32 / V) chunks of 16 B
+      constexpr int CPR = 32 / V;
+#pragma unroll
+      for (int it = 0; it < (32 * CPR) / 64; ++it) {
+        const int ch = lane + 64 * it;
+        const int r = ch / CPR, c4 = (ch - r * CPR) * V;
+        const int64_t gr = gr0 + r, gc = gc0 + c4;
+        if (gr >= rend) continue;
+        T v[V];
+#pragma unroll
+        for (int q = 0; q < V; ++q) v[q] = tile[r * PITCH + c4 + q];
+        T *dst = (T *)o.out + (gr - row0) * o.ld + gc;
+        if (vec_ok && gc + V <= n) {
+          store16(dst, v);
+        } else {
+#pragma unroll
+          for (int q = 0; q < V; ++q)
+            if (gc + q < n) dst[q] = v[q];
+        }
+      }
+      if (mirror) {  // K[gc][gr] = K[gr][gc]: output row c of the sub-tile is column c
+#pragma unroll
+        for (int it = 0; it < (32 * CPR) / 64; ++it) {
+          const int ch = lane + 64 * it;
+          const int c = ch / CPR, r4 = (ch - c * CPR) * V;
+          const int64_t orow = gc0 + c, ocol = gr0 + r4;
+          if (orow >= n) continue;
+          T v[V];
+#pragma unroll
+          for (int q = 0; q < V; ++q) v[q] = tile[(r4 + q) * PITCH + c];
+          T *dst = (T *)o.out + orow * o.ld + ocol;
+          if (vec_ok && ocol + V <= rend) {
+            store16(dst, v);
+          } else {
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+              if (ocol + q < rend) dst[q] = v[q];
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();  // the next sub-tile overwrites this wave's region
     }
+  }
 }
-
-size_t dense_gram_lds_bytes() { return 2 * DT_STAGE; }
 
 hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t n,
                                  int k, int window, int dp, const uint32_t *masks, int nmask,
@@ -301,26 +372,28 @@ hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, i
   const int64_t rows = row1 - row0;
   if (rows <= 0 || n <= 0) return hipSuccess;
   if (dp & (DT_BK - 1)) return hipErrorInvalidValue;
+  const bool sym = row0 == 0 && rows == n;
   const int tiles_m = (int)((rows + DT_BM - 1) / DT_BM);
   const int tiles_n = (int)((n + DT_BM - 1) / DT_BM);
-  const int64_t total = (int64_t)tiles_m * tiles_n;
+  const int64_t total = sym ? (int64_t)tiles_n * (tiles_n + 1) / 2 : (int64_t)tiles_m * tiles_n;
   if (total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((total + 7) & ~7LL);
-  const size_t lds = dense_gram_lds_bytes();
+  const size_t lds = DT_LDS;
+#define KMG_DENSE(DTV, SY)                                                                       \
+  hipLaunchKernelGGL((gram_dense_kernel<DTV, SY>), dim3(grid), dim3(512), lds, s, F, dp, n, row0, \
+                     rows, tiles_m, tiles_n, total, o)
   switch (o.dtype) {
     case KMG_I32:
-      hipLaunchKernelGGL(gram_dense_kernel<KMG_I32>, dim3(grid), dim3(256), lds, s, F, dp, n, row0,
-                         rows, tiles_m, tiles_n, o);
+      if (sym) KMG_DENSE(KMG_I32, true); else KMG_DENSE(KMG_I32, false);
       break;
     case KMG_F32:
-      hipLaunchKernelGGL(gram_dense_kernel<KMG_F32>, dim3(grid), dim3(256), lds, s, F, dp, n, row0,
-                         rows, tiles_m, tiles_n, o);
+      if (sym) KMG_DENSE(KMG_F32, true); else KMG_DENSE(KMG_F32, false);
       break;
     default:
-      hipLaunchKernelGGL(gram_dense_kernel<KMG_F64>, dim3(grid), dim3(256), lds, s, F, dp, n, row0,
-                         rows, tiles_m, tiles_n, o);
+      if (sym) KMG_DENSE(KMG_F64, true); else KMG_DENSE(KMG_F64, false);
       break;
   }
+#undef KMG_DENSE
   return hipGetLastError();
 }
 

@@ -351,6 +351,273 @@ __global__ __launch_bounds__(1024) void gram_mm1_kernel(IndexGeom g, Packed pk,
   }
 }
 
+// ------------------------------------------------------------------ mismatch m=1, pair table
+// Drop-two-letters formulation (PairGeom, kmg_internal.h).  For a row k-mer u and a pair
+// p < q, group key_pq(u) holds every occurrence z that agrees with u outside {p, q}, in 16
+// sub-bins (z_p, z_q), z_p-major.  Weights, an inclusion-exclusion over the pairs that
+// leaves every group but k-1 of the 36 with ONE interval test per entry:
+//   every pair: entries with z_p != u_p (all but the contiguous row u_p)  -> w2
+//     this counts each Hamming-2 neighbour at {p, q} once, and each Hamming-1 neighbour
+//     at r (k-1-r) times (the pairs (r, q > r)), Hamming 0 never;
+//   pairs (0, r), r >= 1, additionally: row u_0 (z_0 = u_0: Hamming 1 at r, or 0):
+//     Hamming 1 at r -> c_r = w1 - (k-1-r) w2, the exact bin (u_0, u_r) -> w0 for r = 1
+//     only; and for r = 1 the column bins (z_0 != u_0, z_1 = u_1) = Hamming 1 at 0 get
+//     c_0 = w1 - (k-1) w2 on top of w2.
+// Net: every Hamming <= 2 neighbour gets exactly w[ham] (the closed form of
+// <Phi_x, Phi_y>, kernels.py:161-175, 211-215).  Per row: k(k-1)/2 lists per window (36
+// at k = 9, against 117 one-line lists of the drop-one table), each a few whole lines.
+// Eight lanes per list; per list (pipelined): a 32-byte summary record (L2) gives the
+// group's first line and line count nl (DPP sums over the 8 lanes), then lane gl loads the
+// group header and its pieces [gl*nl, gl*nl + nl) with buffer loads (pieces past nl fall
+// outside the buffer: no traffic), builds 64-bit masks of its entries from the 16
+// bin-end bytes and adds the weights with LDS atomics.
+__device__ __forceinline__ uint64_t span_mask(int a, int b) {  // bits [a, b) of 0..63
+  const int lo = min(max(a, 0), 64), hi = min(max(b, 0), 64);
+  const uint64_t mh = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  const uint64_t ml = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+  return mh & ~ml;
+}
+__device__ __forceinline__ uint32_t nibble_sum(uint32_t x) {
+  const uint32_t y = (x & 0x0F0F0F0Fu) + ((x >> 4) & 0x0F0F0F0Fu);
+  return (y * 0x01010101u) >> 24;
+}
+// sum over each aligned group of 8 lanes, result in all 8 (DPP: half-row mirror, then the
+// two quad swaps)
+__device__ __forceinline__ uint32_t sum8(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  return v;
+}
+// start / end of sub-bin b from the header dwords (bin ends as bytes, e[15] = n)
+__device__ __forceinline__ int bin_end(const uint32_t (&h)[4], int b) {
+  const int q = b >> 2;  // select, not an indexed load: keeps h in registers
+  const uint32_t w = q == 0 ? h[0] : q == 1 ? h[1] : q == 2 ? h[2] : h[3];
+  return (int)((w >> (8 * (b & 3))) & 0xFFu);
+}
+__device__ __forceinline__ int bin_start(const uint32_t (&h)[4], int b) {
+  return b == 0 ? 0 : bin_end(h, b - 1);
+}
+
+template <int K, int D>
+__global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g, Packed pk,
+                                                        const uint32_t *__restrict__ summary,
+                                                        const uint4 *__restrict__ lines,
+                                                        uint32_t line_bytes,
+                                                        const uint32_t *__restrict__ xoff,
+                                                        const uint16_t *__restrict__ xent,
+                                                        int64_t row0, int64_t rows, int w0, int w1,
+                                                        int w2, OutSpec o) {
+  constexpr int G = 8, MAXP = 5;
+  constexpr int NP = K * (K - 1) / 2;
+  constexpr uint32_t NK2 = 1u << (2 * (K - 2));
+  // one dynamic LDS block, accumulator first: col_addr_sdwa needs acc at LDS offset 0, so
+  // this kernel declares no static __shared__ variable
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int c = (int)(blockIdx.x / rows);
+  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  const int64_t i = row0 + il;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;
+  uint32_t *rowk = smem + accw;  // [P] row k-mers (KMG_INVALID: skipped)
+  uint32_t *srec = rowk + P;     // packed row record
+  uint32_t *spq = srec + pk.ldp; // [NP] p | q << 8 of every pair
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  stage_record(pk, i, srec);
+  if (threadIdx.x < NP) spq[threadIdx.x] = pg.pq[threadIdx.x];
+  __syncthreads();
+  for (int a = threadIdx.x; a < P; a += blockDim.x) rowk[a] = pk_window(srec, pk.cw, a, K);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void *)lines, (short)0, (int)line_bytes, 0x00020000);
+  const int ngrp = blockDim.x / G, grp = threadIdx.x / G, gl = threadIdx.x % G;
+  const int total = NP * P;
+  const uint32_t chunk_base = (uint32_t)c * NK2;
+  const uint32_t pair_stride = (uint32_t)g.nchunks * NK2;
+  const int c0 = w1 - (K - 1) * w2;  // Hamming 1 at 0, on top of the w2 it got K-1 times
+
+  // the lists of this lane group: L = grp + t * ngrp, pair-major (pi, a) = divmod(L, P),
+  // walked incrementally (no division per list)
+  int nx_pi = grp / P, nx_a = grp - (grp / P) * P, nx_L = grp;
+  // describe the next list of the stream and advance it; meta = u_p | u_q << 2 |
+  // valid << 4 | special (p == 0) << 5 | q << 8
+  auto describe_next = [&](uint32_t &gidx, uint32_t &meta) {
+    const bool in = nx_L < total;
+    const uint32_t pq = spq[in ? nx_pi : 0];
+    const int p = pq & 0xFF, q = pq >> 8;
+    const uint32_t u = rowk[in ? nx_a : 0];
+    const bool valid = in && u != KMG_INVALID;
+    const uint32_t uu = valid ? u : 0u;
+    gidx = (uint32_t)(in ? nx_pi : 0) * pair_stride + chunk_base + pair_key(uu, K, p, q);
+    meta = ((uu >> (2 * (K - 1 - p))) & 3u) | (((uu >> (2 * (K - 1 - q))) & 3u) << 2) |
+           ((valid ? 1u : 0u) << 4) | ((p == 0 ? 1u : 0u) << 5) | ((uint32_t)q << 8);
+    nx_L += ngrp;
+    nx_a += ngrp;
+    while (nx_a >= P) {
+      nx_a -= P;
+      ++nx_pi;
+    }
+  };
+  // summary dword gl of the group's record
+  auto load_summary = [&](uint32_t gidx) -> uint32_t { return summary[(size_t)(gidx >> 5) * 8 + gl]; };
+  // base line and line count of the group from the 8 lanes' summary dwords
+  auto decode = [&](uint32_t sw, uint32_t gidx, uint32_t meta, uint32_t &base, uint32_t &nl) {
+    const int r = (int)(gidx & 31u);
+    const int below = r - 8 * (gl - 1);  // lanes 1..4: nibbles of this word before group r
+    const bool nib = gl >= 1 && gl <= 4;
+    const uint32_t m = below >= 8 ? 0xFFFFFFFFu : (below <= 0 ? 0u : ((1u << (4 * below)) - 1u));
+    const uint32_t part = gl == 0 ? sw : (nib ? nibble_sum(sw & m) : 0u);
+    const uint32_t own = (nib && below >= 0 && below < 8) ? (sw >> (4 * below)) & 15u : 0u;
+    base = sum8(part);
+    nl = (meta & 16u) ? sum8(own) : 0u;
+  };
+  // header (piece 0) and this lane's pieces [gl * nl, gl * nl + nl)
+  auto load_lines = [&](uint32_t base, uint32_t nl, uint4 &hdr, uint4(&d)[MAXP]) {
+    const uint32_t first = (uint32_t)gl * nl;
+    hdr = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, nl ? base * 128u : 0xFFFFFFF0u, 0, 0));
+#pragma unroll
+    for (int s = 0; s < MAXP; ++s) {
+      const uint32_t off = (uint32_t)s < nl ? (base * 128u + (first + (uint32_t)s) * 16u) : 0xFFFFFFF0u;
+      d[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, off, 0, 0));
+    }
+  };
+  // weight of sub-bin (zp, zq) for the list (inclusion-exclusion above)
+  auto bin_weight = [&](uint32_t meta, uint32_t zp, uint32_t zq) -> int {
+    if (!(meta & 16u)) return 0;
+    const uint32_t up = meta & 3u, uq = (meta >> 2) & 3u;
+    if (!(meta & 32u)) return zp != up ? w2 : 0;
+    const int r = (int)(meta >> 8);
+    if (zp != up) return w2 + ((r == 1 && zq == uq) ? c0 : 0);
+    return zq == uq ? (r == 1 ? w0 : 0) : w1 - (K - 1 - r) * w2;
+  };
+  // wide group (> 255 entries): every bin straight from the exact index
+  auto wide = [&](uint32_t gidx, uint32_t meta) {
+    const uint32_t key = gidx & (NK2 - 1u);
+    const int pi = (int)(gidx / pair_stride);
+    const int p = spq[pi] & 0xFF, q = spq[pi] >> 8;
+    const uint32_t *xo = xoff + (size_t)c * ((size_t)NK2 << 4);
+    for (uint32_t b = 0; b < 16; ++b) {
+      const int w = bin_weight(meta, b >> 2, b & 3u);
+      if (!w) continue;
+      const uint32_t z = pair_insert(key, K, p, q, b >> 2, b & 3u);
+      const uint32_t e1 = xo[z + 1];
+      for (uint32_t e = xo[z] + (uint32_t)gl; e < e1; e += G) atomicAdd(&acc[xent[e]], w);
+    }
+  };
+  auto add = [&](uint32_t ad, int w) {
+    __hip_atomic_fetch_add((__attribute__((address_space(3))) int32_t *)(uintptr_t)ad, w,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto process = [&](const uint4 &hdr, const uint4(&d)[MAXP], uint32_t nl, uint32_t gidx,
+                     uint32_t meta) {
+    if (nl == 0) return;
+    const uint32_t hd[4] = {hdr.x, hdr.y, hdr.z, hdr.w};
+    if ((hdr.w >> 16) == 0x00FFu) {  // byte 14 = 0xFF, byte 15 = 0: wide marker
+      wide(gidx, meta);
+      return;
+    }
+    const int up = (int)(meta & 3u), n = (int)(hdr.w >> 24);
+    // this lane's entries: piece gl*nl holds entries 8 (gl*nl) - 8 ..; valid = [0, n)
+    const int t0 = 8 * gl * (int)nl - 8;
+    const uint64_t vm = span_mask(-t0, min(n - t0, 8 * (int)nl));
+    const uint64_t rm = span_mask(bin_start(hd, 4 * up) - t0, bin_end(hd, 4 * up + 3) - t0);
+    if (!__any(meta & 32u)) {  // no pair (0, r) list in this wave: one interval per entry
+      const uint64_t act = vm & ~rm;
+#pragma unroll
+      for (int s = 0; s < MAXP; ++s) {
+        if (!__any((uint32_t)s < nl)) break;
+        const uint32_t m8 = (uint32_t)(act >> (8 * s)) & 0xFFu;
+        const uint32_t wd[4] = {d[s].x, d[s].y, d[s].z, d[s].w};
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          if (m8 & (1u << v))
+            add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w2);
+      }
+      return;
+    }
+    // general form (pairs (0, r) in this wave): per-entry weight from row / bin / column
+    const int uq = (int)((meta >> 2) & 3u), r = (int)(meta >> 8);
+    const bool special = meta & 32u;
+    const int cr = w1 - (K - 1 - r) * w2;
+    const int wrow = special ? cr : 0, wex = (special && r == 1) ? w0 : 0;
+    const int wcol = (special && r == 1) ? w2 + c0 : w2;
+    const uint64_t bm = special ? span_mask(bin_start(hd, 4 * up + uq) - t0, bin_end(hd, 4 * up + uq) - t0) : 0ull;
+    uint64_t cm = 0;
+    if (special && r == 1) {
+#pragma unroll
+      for (int zp = 0; zp < 4; ++zp)
+        cm |= span_mask(bin_start(hd, 4 * zp + uq) - t0, bin_end(hd, 4 * zp + uq) - t0);
+    }
+#pragma unroll
+    for (int s = 0; s < MAXP; ++s) {
+      if (!__any((uint32_t)s < nl)) break;
+      const uint32_t wd[4] = {d[s].x, d[s].y, d[s].z, d[s].w};
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const int j = 8 * s + v;
+        if ((vm >> j) & 1ull) {
+          const bool inr = (rm >> j) & 1ull;
+          const int w = inr ? (((bm >> j) & 1ull) ? wex : wrow) : (((cm >> j) & 1ull) ? wcol : w2);
+          if (w) add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w);
+        }
+      }
+    }
+  };
+
+  // ring of D lists per lane group, unrolled so no loaded register is ever copied: slot r
+  // holds the lines of its current list (loaded one round ago) and the summary of its next
+  // list (loaded one round ago); per round and slot: atomics of the current list, decode
+  // of the next list's summary + its line loads, then the summary load of the list after.
+  uint4 dat[D][MAXP], hdr[D];
+  uint32_t nl[D], gid[D], met[D], gidn[D], metn[D], swn[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    describe_next(gid[r], met[r]);
+    swn[r] = load_summary(gid[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    uint32_t base;
+    decode(swn[r], gid[r], met[r], base, nl[r]);
+    load_lines(base, nl[r], hdr[r], dat[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    describe_next(gidn[r], metn[r]);
+    swn[r] = load_summary(gidn[r]);
+  }
+  for (int L = grp; L < total; L += D * ngrp) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      process(hdr[r], dat[r], nl[r], gid[r], met[r]);
+      uint32_t base;
+      decode(swn[r], gidn[r], metn[r], base, nl[r]);
+      gid[r] = gidn[r];
+      met[r] = metn[r];
+      load_lines(base, nl[r], hdr[r], dat[r]);
+      describe_next(gidn[r], metn[r]);
+      swn[r] = load_summary(gidn[r]);
+    }
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
+    const int4 w = *(const int4 *)&acc[qq];
+    if (o.dtype == KMG_F64)
+      emit4<KMG_F64, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else if (o.dtype == KMG_F32)
+      emit4<KMG_F32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+    else
+      emit4<KMG_I32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
+  }
+}
+
 // ------------------------------------------------------------------ Hamming forms
 __device__ __forceinline__ int ham2bit(uint32_t a, uint32_t b, uint32_t mask55) {
   const uint32_t x = a ^ b;
@@ -530,6 +797,33 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, con
     break;
     KMG_MM(8) KMG_MM(9) KMG_MM(10) KMG_MM(11) KMG_MM(12)
 #undef KMG_MM
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, const Packed &pk,
+                                       const uint32_t *summary, const uint4 *lines,
+                                       int64_t nlines, const uint32_t *xoff, const uint16_t *xent,
+                                       int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                       const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || g.n == 0) return hipSuccess;
+  if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
+  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (nlines * 128 >= 0xFFFFFFF0LL) return hipErrorInvalidValue;  // 32-bit buffer offsets
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax + pk.ldp + KMG_PAIRS_MAX) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(rows * g.nchunks));
+  const uint32_t lb = (uint32_t)(nlines * 128);
+  switch (pg.k) {
+#define KMG_MM2(KK)                                                                               \
+  case KK:                                                                                        \
+    hipLaunchKernelGGL((gram_mm2_kernel<KK, 2>), grid, dim3(1024), lds, s, pg, g, pk, summary, lines, \
+                       lb, xoff, xent, row0, rows, w0, w1, w2, o);                                \
+    break;
+    KMG_MM2(3) KMG_MM2(4) KMG_MM2(5) KMG_MM2(6) KMG_MM2(7) KMG_MM2(8) KMG_MM2(9) KMG_MM2(10)
+    KMG_MM2(11) KMG_MM2(12)
+#undef KMG_MM2
   }
   return hipGetLastError();
 }

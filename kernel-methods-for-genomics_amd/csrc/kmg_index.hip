@@ -355,6 +355,136 @@ hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint1
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ pair (drop-two) table
+__device__ __forceinline__ void pair_decode(const PairGeom &pg, int64_t g, int &p, int &q,
+                                            int &c, uint32_t &key) {
+  key = (uint32_t)(g % pg.nkeys2);
+  const int64_t pc = g / pg.nkeys2;  // pair * nchunks + chunk
+  c = (int)(pc % pg.nchunks);
+  const int pi = (int)(pc / pg.nchunks);
+  p = pg.pq[pi] & 0xFF;
+  q = pg.pq[pi] >> 8;
+}
+
+__device__ __forceinline__ uint32_t pair_lines(uint32_t n) {
+  return n == 0 ? 0u : (n > 255u ? 1u : (16u + 2u * n + 127u) / 128u);
+}
+
+// one thread per 8 groups (one nibble word of a summary record); 4 threads per record
+__global__ __launch_bounds__(256) void pair_count_kernel(PairGeom pg,
+                                                         const uint32_t *__restrict__ xoff,
+                                                         uint32_t *__restrict__ summary,
+                                                         uint32_t *__restrict__ rtot) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrec = pg.nrec();
+  const bool live = t < nrec * 4;
+  uint32_t word = 0, tot = 0;
+  if (live) {
+    const int64_t g0 = (t >> 2) * 32 + (t & 3) * 8;
+    for (int r = 0; r < 8; ++r) {
+      const int64_t g = g0 + r;
+      if (g >= pg.ngroups()) break;
+      int p, q, c;
+      uint32_t key;
+      pair_decode(pg, g, p, q, c, key);
+      const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
+      uint32_t n = 0;
+      for (uint32_t b = 0; b < 16; ++b) {
+        const uint32_t z = pair_insert(key, pg.k, p, q, b >> 2, b & 3u);
+        n += xo[z + 1] - xo[z];
+      }
+      const uint32_t nl = pair_lines(n);
+      word |= nl << (4 * r);
+      tot += nl;
+    }
+    summary[(t >> 2) * 8 + 1 + (t & 3)] = word;
+  }
+  // record total over its 4 threads (adjacent lanes)
+  tot += __shfl_xor(tot, 1, 64);
+  tot += __shfl_xor(tot, 2, 64);
+  if (live && (t & 3) == 0) rtot[t >> 2] = tot;
+}
+
+// 16 lanes per group (lane b = sub-bin (z_p, z_q) = (b >> 2, b & 3)), 16 groups per block:
+// the group's lines are assembled in LDS (header bytes, then every bin's entries copied
+// from the exact index) and written out with 16-byte stores.
+constexpr int PAIR_PACK_GROUPS = 16;
+constexpr int PAIR_MAX_LINES = 5;  // n <= 255: (16 + 510) / 128 -> 5 lines
+__global__ __launch_bounds__(256) void pair_pack_kernel(PairGeom pg,
+                                                        const uint32_t *__restrict__ xoff,
+                                                        const uint16_t *__restrict__ xent,
+                                                        const uint32_t *__restrict__ rbase,
+                                                        uint32_t *__restrict__ summary,
+                                                        uint4 *__restrict__ lines) {
+  __shared__ __align__(16) uint32_t img[PAIR_PACK_GROUPS][PAIR_MAX_LINES * 32];
+  const int lg = threadIdx.x >> 4, b = threadIdx.x & 15;
+  const int64_t g = (int64_t)blockIdx.x * PAIR_PACK_GROUPS + lg;
+  const bool live = g < pg.ngroups();
+  // record base -> summary w0 (first lane of each record's first group)
+  if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5];
+  for (int w = b; w < PAIR_MAX_LINES * 32; w += 16) img[lg][w] = 0;
+  uint32_t s0 = 0, cnt = 0, key = 0;
+  int p = 0, q = 1, c = 0;
+  if (live) {
+    pair_decode(pg, g, p, q, c, key);
+    const uint32_t z = pair_insert(key, pg.k, p, q, (uint32_t)b >> 2, (uint32_t)b & 3u);
+    const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
+    s0 = xo[z];
+    cnt = xo[z + 1] - s0;
+  }
+  // inclusive scan of the 16 bin counts
+  uint32_t end = cnt;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const uint32_t v = __shfl_up(end, d, 16);
+    if (b >= d) end += v;
+  }
+  const uint32_t n = __shfl(end, 15, 16);
+  // base line of this group: record base + line counts of the record's earlier groups
+  uint32_t base = 0;
+  if (live) {
+    const int64_t rec = g >> 5;
+    const int r = (int)(g & 31);
+    base = rbase[rec];
+    for (int j = 0; j < r; ++j) base += (summary[rec * 8 + 1 + (j >> 3)] >> (4 * (j & 7))) & 15u;
+  }
+  __syncthreads();
+  const uint32_t nl = pair_lines(n);
+  uint8_t *im = (uint8_t *)img[lg];
+  if (live && n > 0) {
+    if (n > 255u) {  // wide marker: byte 14 = 0xFF, byte 15 = 0
+      if (b == 14) im[14] = 0xFF;
+    } else {
+      im[b] = (uint8_t)end;
+      uint16_t *dst = (uint16_t *)(im + 16) + (end - cnt);
+      for (uint32_t e = 0; e < cnt; ++e) dst[e] = xent[s0 + e];
+    }
+  }
+  __syncthreads();
+  if (live)
+    for (uint32_t w = b; w < nl * 8; w += 16)
+      lines[(size_t)base * 8 + w] = ((const uint4 *)img[lg])[w];
+}
+
+hipError_t launch_pair_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
+                             uint32_t *rtot, hipStream_t s) {
+  const int64_t threads = pg.nrec() * 4;
+  if (threads == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_count_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     pg, xoff, summary, rtot);
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
+                            const uint32_t *rbase, uint32_t *summary, uint4 *lines,
+                            hipStream_t s) {
+  const int64_t blocks = (pg.ngroups() + PAIR_PACK_GROUPS - 1) / PAIR_PACK_GROUPS;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent,
+                     rbase, summary, lines);
+  return hipGetLastError();
+}
+
 // plain k-mer extraction (Hamming formulation)
 __global__ __launch_bounds__(256) void extract_kernel(IndexGeom g, Packed pk,
                                                       uint32_t *__restrict__ kmers) {

@@ -101,6 +101,62 @@ hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const
 hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint16_t *ent,
                             uint4 *slots, hipStream_t s);
 
+// ---------------------------------------------------------------- pair (drop-two) table
+// Mismatch (k, 1) through the drop-two-letters index: for every pair of positions
+// p < q (npairs = k(k-1)/2, enumerated (0,1), (0,2), ..., (k-2,k-1)) and every k-mer z,
+// key_pq(z) = z with letters p and q removed (k-2 letters).  Group (pair, chunk, key) holds
+// every occurrence z with that key, sorted into 16 sub-bins by (z_p, z_q).
+// Storage: each group is nl whole 128-byte lines at line index base(g) of `lines`:
+//   16-byte header = bin ends e[0..15] as bytes (e[15] = n), then n uint16 columns;
+//   nl = ceil((16 + 2n) / 128); n = 0 -> nl = 0 (no lines);
+//   n > 255 -> "wide": one marker line (byte 14 = 0xFF, byte 15 = 0) and the entries are
+//   read from the exact k-mer index (xoff / xent) in a slow path.
+// Summary (L2-resident, 1 byte per group): per 32 groups a 32-byte record
+//   w0 = base line of the record's first group, w1..w4 = nl of the 32 groups, 4 bits each.
+#define KMG_PAIRS_MAX 66
+struct PairGeom {
+  int k;
+  int npairs;
+  int nchunks;
+  int chunk;
+  uint32_t nkeys2;                 // 4^(k-2)
+  uint16_t pq[KMG_PAIRS_MAX];      // p | q << 8
+  __host__ __device__ int64_t ngroups() const { return (int64_t)npairs * nchunks * nkeys2; }
+  __host__ __device__ int64_t nrec() const { return (ngroups() + 31) / 32; }
+};
+// z with letters zp at p and zq at q inserted into the (k-2)-letter key (p < q)
+__host__ __device__ __forceinline__ uint32_t pair_insert(uint32_t key, int k, int p, int q,
+                                                         uint32_t zp, uint32_t zq) {
+  const int lo = 2 * (k - 1 - q), mid = 2 * (q - p - 1);
+  const uint32_t bottom = key & ((1u << lo) - 1u);
+  const uint32_t middle = (key >> lo) & ((1u << mid) - 1u);
+  const uint32_t top = (uint32_t)((uint64_t)key >> (lo + mid));
+  return (((((top << 2) | zp) << mid | middle) << 2 | zq) << lo) | bottom;
+}
+// (k-2)-letter key of k-mer u for the pair p < q
+__host__ __device__ __forceinline__ uint32_t pair_key(uint32_t u, int k, int p, int q) {
+  const int lo = 2 * (k - 1 - q), mid = 2 * (q - p - 1);
+  const uint32_t bottom = u & ((1u << lo) - 1u);
+  const uint32_t middle = (u >> (lo + 2)) & ((1u << mid) - 1u);
+  const uint32_t top = (uint32_t)((uint64_t)u >> (2 * (k - p)));
+  return (((top << mid) | middle) << lo) | bottom;
+}
+// from the exact index (xoff over [chunk][4^k]): per-group line counts into summary
+// w1..w4 and per-record line totals rtot[nrec]
+hipError_t launch_pair_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
+                             uint32_t *rtot, hipStream_t s);
+// after the exclusive scan of rtot into rbase: summary w0 = rbase, then the lines
+hipError_t launch_pair_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
+                            const uint32_t *rbase, uint32_t *summary, uint4 *lines,
+                            hipStream_t s);
+// upper bound of the line count (no device round trip before allocating): a non-empty
+// group holds >= 1 of the npairs * occurrences entries and takes <= 1 + (16 + 2n) / 128 lines
+inline int64_t pair_lines_bound(const PairGeom &pg, int64_t occurrences) {
+  const int64_t entries = (int64_t)pg.npairs * occurrences;
+  const int64_t nonempty = pg.ngroups() < entries ? pg.ngroups() : entries;
+  return nonempty + nonempty / 8 + 2 * entries / 128 + 64;
+}
+
 // ---------------------------------------------------------------- Gram kernels
 struct OutSpec {
   void *out;         // points at row row0
@@ -119,6 +175,12 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, con
                                        const uint32_t *off, const uint16_t *ent, int64_t row0,
                                        int64_t row1, int w0, int w1, int w2, const OutSpec &o,
                                        hipStream_t s);
+// mismatch (k,1), 3 <= k <= 12, on the pair (drop-two) table; xoff / xent = exact index
+hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, const Packed &pk,
+                                       const uint32_t *summary, const uint4 *lines,
+                                       int64_t nlines, const uint32_t *xoff, const uint16_t *xent,
+                                       int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                       const OutSpec &o, hipStream_t s);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -171,11 +171,12 @@ def test_mismatch_params(ctx, k, m):
 
 @pytest.mark.parametrize("k", [8, 9, 10, 11, 12])
 def test_mismatch_slots_k_range(ctx, tune, k):
-    """Slot layout (the path for 8 <= k <= 12) at every compiled k, raw and normalised,
-    over several column chunkings (slot tables grow with 4^(k-1) per chunk: k >= 10 stays
-    single-chunk here)."""
+    """Drop-one slot layout (default for k = 8, forced for 9..12) at every compiled k, raw
+    and normalised, over several column chunkings (slot tables grow with 4^(k-1) per
+    chunk: k >= 10 stays single-chunk here)."""
     codes, lens = E.synthetic(400, 101, seed=50 + k)
     ref = cref.mismatch_raw(codes, lens, k, 1)
+    tune(KMG_MM_FORM=1)
     for chunk in (("64", "300", "20480") if k <= 9 else ("20480",)):
         tune(KMG_MM_CHUNK=chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
@@ -186,11 +187,30 @@ def test_mismatch_slots_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-def test_mismatch_slots_overflow_and_big_groups(ctx, tune):
-    """Slot groups longer than the 60 inline entries (CSR tail) and groups of >= 65535
-    entries (16-bit header overflow, CSR only): 720 poly-A rows put 720 * 93 = 66960
-    occurrences in the AAAAAAAAA groups of every copy."""
-    tune(KMG_MM_CHUNK=20480)
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+def test_mismatch_pairs_k_range(ctx, tune, k):
+    """Drop-two pair table (default for 9 <= k <= 12, forced below) at every compiled k,
+    raw and normalised, over several column chunkings (chunk = columns per group table)."""
+    codes, lens = E.synthetic(500, 101, seed=80 + k)
+    ref = cref.mismatch_raw(codes, lens, k, 1)
+    tune(KMG_MM_FORM=2)
+    for chunk in (("40", "168", "20480") if k <= 9 else ("168", "20480") if k == 10 else ("20480",)):
+        tune(KMG_MM_CHUNK=chunk)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), ref), chunk
+    Kn = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
+                  L.KMG_F64)
+    assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
+
+
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
+    """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
+    >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
+    entries (wide marker, read from the exact index).  720 poly-A rows put 720 * 93 = 66960
+    occurrences in the AAAAAAAAA groups of every copy / pair."""
+    tune(KMG_MM_CHUNK=20480, KMG_MM_FORM=form)
     codes, lens = E.synthetic(760, 101, seed=61)
     codes[:720] = 0
     codes[700] = np.tile([0, 1], 51)[:101]
@@ -203,7 +223,9 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune):
     assert np.array_equal(raw, raw.T)
 
 
-def test_mismatch_stress_repeats(ctx):
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_mismatch_stress_repeats(ctx, tune, form):
+    tune(KMG_MM_FORM=form)
     codes, lens = E.synthetic(40, 101, seed=12)
     codes[3] = 0
     codes[4] = np.tile([0, 1], 51)[:101]
