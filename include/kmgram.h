@@ -80,7 +80,9 @@ typedef struct kmg_params {
   int32_t normalize; /* 1: fused normalize_K epilogue (kernels.py:398-415) */
   int32_t smith;     /* LA: 1 = Smith_Waterman max form */
   int32_t la_mode;   /* LA: KMG_LA_REFERENCE / KMG_LA_INTENDED; GP: KMG_MODE_* */
-  int32_t reserved[6];
+  int32_t span;      /* WD/WDS: summation length L of get_WD_d / get_WDShifts_d (kernels.py:64,
+                        115); 0 = len(x) of the smaller-index row, as get_*_K pass it */
+  int32_t reserved[5];
   double lambda;     /* SS lambda */
   double lambda2;    /* SS lambda**2 exactly as the host language computes it */
   double la_e, la_d, la_beta; /* LA gap open / extend / beta */

@@ -713,13 +713,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (p->kind == KMG_WDS && (p->S < 0 || p->S > 15))
         return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
+      if (p->span < 0) return fail(KMG_EINVAL, "span < 0");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
       bool unsupported = false;
       const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         hipError_t e = p->kind == KMG_WD
-                           ? launch_gram_wd(q, r0, r1, p->d, p->coef_a, oq, c->stream)
-                           : launch_gram_wds(q, r0, r1, p->d, p->S, p->coef_a, p->coef_b, oq,
-                                             c->stream);
+                           ? launch_gram_wd(q, r0, r1, p->d, p->span, p->coef_a, oq, c->stream)
+                           : launch_gram_wds(q, r0, r1, p->d, p->S, p->span, p->coef_a,
+                                             p->coef_b, oq, c->stream);
         if (e == hipErrorNotSupported) {
           unsupported = true;
           return hipSuccess;

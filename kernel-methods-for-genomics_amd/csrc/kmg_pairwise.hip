@@ -124,7 +124,7 @@ __device__ __forceinline__ void store_f(const OutSpec &o, int64_t il, int64_t j,
 // L-1+(1-d)/3 (kernels.py:96).  Tile: 16 rows x 64 columns, 256 threads.
 template <int NW>
 __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, int64_t row1, int d,
-                                                      Coef cf, OutSpec o) {
+                                                      int span, Coef cf, OutSpec o) {
   constexpr int WS = SeqTile<NW>::WORDS;
   __shared__ uint32_t srow[16][WS];
   __shared__ uint32_t scol[64][WS];
@@ -149,6 +149,7 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
       const uint32_t *ys = rowx ? scol[lane] : srow[r];
       const int Lx = q.lens[rowx ? i : j], Ly = q.lens[rowx ? j : i];
       uint64_t M[NW], A[NW], Ms[NW], V[NW];
+      const int Lr = span > 0 ? span : Lx;  // summation length L (get_WD_d's argument)
       match_mask<NW>(xs, Lx, 0, ys, Ly, 0, M);
 #pragma unroll
       for (int w = 0; w < NW; ++w) { A[w] = M[w]; Ms[w] = M[w]; }
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
             A[w] &= Ms[w];
           }
         }
-        range_mask<NW>(V, 1, Lx - k + 1);
+        range_mask<NW>(V, 1, Lr - k + 1);
         const int c = popc_and<NW>(A, V);
         val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], (double)c));
       }
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
 // (kernels.py:115-135).  Zero terms are skipped: adding +0.0 never changes an fp64 sum.
 template <int NW, int SMAX>
 __global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, int64_t row1, int d,
-                                                       int S, Coef cf, OutSpec o) {
+                                                       int S, int span, Coef cf, OutSpec o) {
   constexpr int WS = SeqTile<NW>::WORDS;
   __shared__ uint32_t srow[16][WS];
   __shared__ uint32_t scol[64][WS];
@@ -197,12 +198,22 @@ __global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, 
     const uint32_t *xs = rowx ? srow[r] : scol[lane];
     const uint32_t *ys = rowx ? scol[lane] : srow[r];
     const int Lx = q.lens[rowx ? i : j], Ly = q.lens[rowx ? j : i];
+    const int Lr = span > 0 ? span : Lx;  // summation length L (get_WDShifts_d's argument)
     uint64_t M1[SMAX + 1][NW], M2[SMAX + 1][NW], W1[SMAX + 1][NW], W2[SMAX + 1][NW];
 #pragma unroll
     for (int s = 0; s <= SMAX; ++s) {
       if (s <= S) {
         match_mask<NW>(xs, Lx, s, ys, Ly, 0, M1[s]);  // x_{i+s} == y_i
         match_mask<NW>(xs, Lx, 0, ys, Ly, s, M2[s]);  // x_i == y_{i+s}
+        if (s > 0 && Lx - s == Ly) {
+          // ragged rows: x[i+s:i+s+k] and y[i:i+k] are clipped to the SAME length Ly - i
+          // near the end, and Python compares the clipped slices (kernels.py:133): a
+          // suffix match counts.  Positions past the end of y match vacuously.
+          uint64_t tail[NW];
+          range_mask<NW>(tail, Ly, 64 * NW);
+#pragma unroll
+          for (int w = 0; w < NW; ++w) M1[s][w] |= tail[w];
+        }
       } else {
 #pragma unroll
         for (int w = 0; w < NW; ++w) { M1[s][w] = 0; M2[s][w] = 0; }
@@ -223,7 +234,7 @@ __global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, 
         }
       }
       uint64_t V[NW];
-      range_mask<NW>(V, 1, Lx - k + 1);
+      range_mask<NW>(V, 1, Lr - k + 1);
       uint64_t any[NW];
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, 
           const int ii = 64 * w + b;
 #pragma unroll
           for (int s = 0; s <= SMAX; ++s) {
-            if (s <= S && s + ii < Lx) {
+            if (s <= S && s + ii < Lr) {
               const int m = (int)((W1[s][w] >> b) & 1ull) + (int)((W2[s][w] >> b) & 1ull);
               if (m) cst = __dadd_rn(cst, __dmul_rn(cf.b[s], (double)m));
             }
@@ -472,8 +483,8 @@ static Coef make_coef(const double *a, const double *b) {
   return c;
 }
 
-hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, const double *beta,
-                          const OutSpec &o, hipStream_t s) {
+hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, int span,
+                          const double *beta, const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   int nw;
@@ -481,13 +492,13 @@ hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, c
   const Coef cf = make_coef(beta, nullptr);
   const dim3 grid((unsigned)((q.n + 63) / 64), (unsigned)((rows + 15) / 16));
   if (nw == 2)
-    hipLaunchKernelGGL((gram_wd_kernel<2>), grid, dim3(256), 0, s, q, row0, row1, d, cf, o);
+    hipLaunchKernelGGL((gram_wd_kernel<2>), grid, dim3(256), 0, s, q, row0, row1, d, span, cf, o);
   else
-    hipLaunchKernelGGL((gram_wd_kernel<4>), grid, dim3(256), 0, s, q, row0, row1, d, cf, o);
+    hipLaunchKernelGGL((gram_wd_kernel<4>), grid, dim3(256), 0, s, q, row0, row1, d, span, cf, o);
   return hipGetLastError();
 }
 
-hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S,
+hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S, int span,
                            const double *beta, const double *delta, const OutSpec &o,
                            hipStream_t s) {
   const int64_t rows = row1 - row0;
@@ -497,7 +508,7 @@ hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, 
   const Coef cf = make_coef(beta, delta);
   const dim3 grid((unsigned)((q.n + 63) / 64), (unsigned)((rows + 15) / 16));
 #define KMG_WDS(NW_, SM_) \
-  hipLaunchKernelGGL((gram_wds_kernel<NW_, SM_>), grid, dim3(256), 0, s, q, row0, row1, d, S, cf, o)
+  hipLaunchKernelGGL((gram_wds_kernel<NW_, SM_>), grid, dim3(256), 0, s, q, row0, row1, d, S, span, cf, o)
   if (nw == 2) {
     if (S <= 1) KMG_WDS(2, 1);
     else if (S <= 3) KMG_WDS(2, 3);

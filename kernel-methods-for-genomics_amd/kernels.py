@@ -105,17 +105,13 @@ def _pair(fn, x, y):
 
 
 def get_WD_d(x, y, d, L):
-    """WD value of one pair (kernels.py:64-81); L must be len(x) as in get_WD_K."""
-    if L != len(x):
-        raise NotImplementedError("get_WD_d with L != len(x)")
-    return _pair(lambda s: _eng().wd(s, d), x, y)
+    """WD value of one pair (kernels.py:64-81), any L (slices clip as Python's do)."""
+    return _eng().wd_pair(x, y, d, L)
 
 
 def get_WDShifts_d(x, y, d, S, L):
-    """WDS value of one pair (kernels.py:115-135); L must be len(x)."""
-    if L != len(x):
-        raise NotImplementedError("get_WDShifts_d with L != len(x)")
-    return _pair(lambda s: _eng().wds(s, d, S), x, y)
+    """WDS value of one pair (kernels.py:115-135), any L."""
+    return _eng().wds_pair(x, y, d, S, L)
 
 
 def K_k(lbda, k, x, y):

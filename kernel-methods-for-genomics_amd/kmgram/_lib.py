@@ -41,7 +41,7 @@ class KmgParams(ctypes.Structure):
         ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("m", ctypes.c_int32),
         ("d", ctypes.c_int32), ("S", ctypes.c_int32), ("g", ctypes.c_int32),
         ("window", ctypes.c_int32), ("normalize", ctypes.c_int32), ("smith", ctypes.c_int32),
-        ("la_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6),
+        ("la_mode", ctypes.c_int32), ("span", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
         ("lambda_", ctypes.c_double), ("lambda2", ctypes.c_double),
         ("la_e", ctypes.c_double), ("la_d", ctypes.c_double), ("la_beta", ctypes.c_double),
         ("coef_a", ctypes.c_double * KMG_MAX_COEF), ("coef_b", ctypes.c_double * KMG_MAX_COEF),

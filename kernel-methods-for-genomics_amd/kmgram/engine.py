@@ -80,11 +80,49 @@ class GramEngine:
         return self._run(P.make(L.KMG_WD, d=int(d)), seqs)
 
     def wds(self, seqs, d, S):
-        """get_WDShifts_K (kernels.py:138-155)."""
-        seqs = list(seqs)
-        if len({len(s) for s in seqs}) > 1:
-            raise NotImplementedError("WDS on sequences of different lengths is not supported")
+        """get_WDShifts_K (kernels.py:138-155); rows of any lengths (the clipped-slice
+        suffix matches of kernels.py:133 are counted on the device)."""
         return self._run(P.make(L.KMG_WDS, d=int(d), S=int(S)), seqs)
+
+    @staticmethod
+    def _pair_codes(x, y, length):
+        """x and y cut or padded to ``length`` symbols with a code neither uses.  Slices of
+        the padded strings that end inside them compare exactly like the reference's
+        clipped slices: two clipped slices are equal iff they have the same length and
+        symbols, and the padded ones iff they hold the same symbols and pad positions."""
+        codes, lens = E.encode([x, y])
+        used = set(np.unique(codes[0, :lens[0]]).tolist()) | set(np.unique(codes[1, :lens[1]]).tolist())
+        pad = next((c for c in range(4, 255) if c not in used), None)
+        if pad is None:
+            raise ValueError("no free symbol code to pad the pair with")
+        ldc = max(4, -(-length // 4) * 4)
+        out = np.full((2, ldc), 255, dtype=np.uint8)
+        for r in range(2):
+            m = min(int(lens[r]), length)
+            out[r, :m] = codes[r, :m]
+            out[r, m:length] = pad
+        return out, np.full(2, length, dtype=np.int32)
+
+    def _pair_value(self, params, codes, lens):
+        return float(self.ctx.gram(params, codes, lens, L.KMG_F64)[0, 1])
+
+    def wd_pair(self, x, y, d, span):
+        """get_WD_d(x, y, d, L=span) (kernels.py:64-81) for any L: windows end at or before
+        L, so x and y padded to L symbols give every clipped comparison."""
+        span = int(span)
+        if span <= 1:
+            return 0.0  # range(1, L - k + 1) is empty for every k
+        codes, lens = self._pair_codes(x, y, span)
+        return self._pair_value(P.make(L.KMG_WD, d=int(d), span=span), codes, lens)
+
+    def wds_pair(self, x, y, d, S, span):
+        """get_WDShifts_d(x, y, d, S, L=span) (kernels.py:115-135) for any L: windows end
+        at or before L + S, so the pair is padded to L + S symbols and the sums run to L."""
+        span, S = int(span), int(S)
+        if span <= 1:
+            return 0.0
+        codes, lens = self._pair_codes(x, y, span + S)
+        return self._pair_value(P.make(L.KMG_WDS, d=int(d), S=S, span=span), codes, lens)
 
     def substring(self, seqs, lbda, k):
         """get_string_K (kernels.py:367-382)."""

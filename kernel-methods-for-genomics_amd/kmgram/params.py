@@ -40,7 +40,7 @@ def make(kind, **kw):
     """Fill a KmgParams struct."""
     p = L.KmgParams()
     p.kind = kind
-    for name in ("k", "m", "d", "S", "g", "window", "normalize", "smith", "la_mode"):
+    for name in ("k", "m", "d", "S", "g", "window", "normalize", "smith", "la_mode", "span"):
         if name in kw:
             setattr(p, name, int(kw[name]))
     if "lbda" in kw:

@@ -184,6 +184,32 @@ def wds(codes, lens, d, S):
     return K
 
 
+def wd_pair(x, y, d, L):
+    """get_WD_d(x, y, d, L) (kernels.py:64-81) for any L: the slices clip at the end of
+    each string and are compared as strings (x, y: str)."""
+    c_t = 0
+    for k in range(1, d + 1):
+        c_st = 0
+        for l in range(1, L - k + 1):
+            c_st += (x[l:l + k] == y[l:l + k])
+        c_t += (2 * (d - k + 1) / d / (d + 1)) * c_st
+    return c_t
+
+
+def wds_pair(x, y, d, S, L):
+    """get_WDShifts_d(x, y, d, S, L) (kernels.py:115-135) for any L (x, y: str)."""
+    c_t = 0
+    for k in range(1, d + 1):
+        c_st = 0
+        for i in range(1, L - k + 1):
+            for s in range(0, S + 1):
+                if s + i < L:
+                    c_st += (1 / 2 / (s + 1)) * ((x[i + s:i + s + k] == y[i:i + k]) +
+                                                 (x[i:i + k] == y[i + s:i + s + k]))
+        c_t += (2 * (d - k + 1) / d / (d + 1)) * c_st
+    return c_t
+
+
 # --------------------------------------------------------------------- substring
 def ss_pair(x, y, lbda, k):
     """K_k(lbda, k, x, y) (kernels.py:344-364) by bottom-up DP over B_t (kernels.py:322-342)

@@ -61,6 +61,8 @@ def job(spec):
         try:
             if fn == "select_method":
                 K = km.select_method(X, kwargs["method"])
+            elif fn in ("get_WD_d", "get_WDShifts_d"):  # one pair: (x, y, ..., L)
+                K = np.array([getattr(km, fn)(seqs[0], seqs[1], **kwargs)], dtype=np.float64)
             else:
                 K = getattr(km, fn)(X, **kwargs)
             out["K"] = np.asarray(K)
@@ -105,6 +107,25 @@ def main():
     for d, S in ((1, 0), (3, 1), (5, 3), (10, 5)):
         jobs.append((f"WDS_d{d}_s{S}_xtr0_n24", "get_WDShifts_K", {"d": d, "S": S}, seqs[:24]))
     jobs.append(("WDS_d5_s3_stress", "get_WDShifts_K", {"d": 5, "S": 3}, stress))
+    # ragged WD / WDS: rows whose lengths differ by 1..S (the clipped-slice suffix matches of
+    # kernels.py:133), a row that is another minus its first s symbols, and the empty row
+    base = seqs[7][:60]
+    wragged = [base, base[2:], seqs[8][:59], base[1:], seqs[9][:57], base[3:] + "A", base[:58],
+               seqs[10][:61], base[4:], "ACGTA", "", base[:57], "NACGT" * 11, base[3:]]
+    jobs.append(("WD_d5_ragged", "get_WD_K", {"d": 5}, wragged))
+    jobs.append(("WD_d1_ragged", "get_WD_K", {"d": 1}, wragged))
+    for d, S in ((1, 1), (3, 2), (5, 3), (4, 7)):
+        jobs.append((f"WDS_d{d}_s{S}_ragged", "get_WDShifts_K", {"d": d, "S": S}, wragged))
+    # pair helpers with L != len(x) (kernels.py:64-81, 115-135)
+    pairs = [(base, base[2:]), (base[2:], base), (seqs[11][:50], seqs[12][:50]),
+             (base, base), ("ACGTACGT", "ACGTAC"), (seqs[13][:40], seqs[13][:40] + "AC")]
+    for pi, (x, y) in enumerate(pairs):
+        for L in sorted({1, 3, len(x) - 7, len(x) - 1, len(x), len(x) + 1, len(x) + 5,
+                         len(y) + 2, len(x) + 12}):
+            if L < 0:
+                continue
+            jobs.append((f"WDd_p{pi}_L{L}", "get_WD_d", {"d": 4, "L": L}, [x, y]))
+            jobs.append((f"WDSd_p{pi}_L{L}", "get_WDShifts_d", {"d": 4, "S": 3, "L": L}, [x, y]))
     for lb, k in ((0.5, 3), (1.0, 3), (0.7, 5), (0.3, 2), (0.5, 1)):
         jobs.append((f"SS_l{lb}_k{k}_xtr0_n10", "get_string_K", {"lbda": lb, "k": k}, seqs[:10]))
     jobs.append(("SS_l0.5_k3_short", "get_string_K", {"lbda": 0.5, "k": 3},

@@ -33,6 +33,12 @@ def test_all_goldens_through_dropin(golden):
         if name == "SP_k6_xtr0_full":
             continue
         e = golden.entry(name)
+        if e["fn"] in ("get_WD_d", "get_WDShifts_d"):  # one pair, any L
+            x, y = golden.seqs(name)
+            v = getattr(kernels, e["fn"])(x, y, **e["kwargs"])
+            assert v == golden.K(name)[0], name
+            checked += 1
+            continue
         X = _X(golden.seqs(name))
         fn = fn_map[e["fn"]]
         if e["error"]:
@@ -46,7 +52,7 @@ def test_all_goldens_through_dropin(golden):
             assert np.array_equal(K, ref), name
             assert sha256_f64(K) == e["sha256_f64"], name
         checked += 1
-    assert checked >= 50
+    assert checked >= 150
 
 
 def test_config1_spectrum_k6_xtr0_sha(golden):
@@ -258,6 +264,41 @@ def test_wd_ragged(ctx):
     codes, lens = E.encode(seqs)
     K = ctx.gram(P.make(L.KMG_WD, d=6), codes, lens, L.KMG_F64)
     assert np.array_equal(K, cref.wd(codes, lens, 6))
+
+
+def _ragged_family(rng, n, base_len=120, S=7):
+    """Rows cut from a few parents with length differences 0..S+1 and shifted copies (a row
+    equal to another minus its first s symbols): the clipped-slice suffix matches of
+    kernels.py:133 occur in many pairs."""
+    parents = ["".join(rng.choice(list("ACGT"), size=base_len + S + 2)) for _ in range(4)]
+    out = []
+    for _ in range(n):
+        p = parents[rng.integers(0, 4)]
+        a = int(rng.integers(0, S + 2))
+        b = base_len - int(rng.integers(0, S + 2))
+        out.append(p[a:b] if rng.random() < 0.8 else p[a:b][:-3] + "NNA")
+    return out
+
+
+@pytest.mark.parametrize("d,S", [(1, 1), (3, 2), (5, 3), (8, 7), (4, 12)])
+def test_wds_ragged(ctx, d, S):
+    rng = np.random.default_rng(100 + S)
+    seqs = _ragged_family(rng, 96, S=S)
+    codes, lens = E.encode(seqs)
+    K = ctx.gram(P.make(L.KMG_WDS, d=d, S=S), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.wds(codes, lens, d, S))
+
+
+def test_wd_wds_pair_any_L(engine):
+    """get_WD_d / get_WDShifts_d for L below, at and above the lengths (padded pair on the
+    device) against the oracle's literal loops."""
+    rng = np.random.default_rng(9)
+    seqs = _ragged_family(rng, 12, base_len=50, S=3)
+    for t in range(0, 12, 2):
+        x, y = seqs[t], seqs[t + 1]
+        for span in (0, 1, 2, 5, len(x) - 3, len(x), len(y), len(x) + 4, max(len(x), len(y)) + 9):
+            assert engine.wd_pair(x, y, 5, span) == cpu_ref.wd_pair(x, y, 5, span)
+            assert engine.wds_pair(x, y, 4, 3, span) == cpu_ref.wds_pair(x, y, 4, 3, span)
 
 
 @pytest.mark.parametrize("d,S", [(1, 0), (3, 1), (5, 3), (10, 5), (8, 7), (4, 12)])

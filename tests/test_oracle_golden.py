@@ -105,6 +105,37 @@ def test_wds_stress(golden):
     assert np.array_equal(cref.wds(codes, lens, 5, 3), golden.K("WDS_d5_s3_stress"))
 
 
+@pytest.mark.parametrize("name", ["WD_d5_ragged", "WD_d1_ragged", "WDS_d1_s1_ragged",
+                                  "WDS_d3_s2_ragged", "WDS_d5_s3_ragged", "WDS_d4_s7_ragged"])
+def test_wd_wds_ragged(golden, name):
+    """Rows of different lengths: slices clip and compare as strings (kernels.py:79,133)."""
+    e = golden.entry(name)
+    codes, lens = _enc(golden, name)
+    ref = golden.K(name)
+    kw = e["kwargs"]
+    if name.startswith("WDS"):
+        assert np.array_equal(cref.wds(codes, lens, kw["d"], kw["S"]), ref)
+        assert np.array_equal(cpu_ref.wds(codes[:6], lens[:6], kw["d"], kw["S"]), ref[:6, :6])
+    else:
+        assert np.array_equal(cref.wd(codes, lens, kw["d"]), ref)
+        assert np.array_equal(cpu_ref.wd(codes[:6], lens[:6], kw["d"]), ref[:6, :6])
+
+
+def test_wd_pair_any_L(golden):
+    """get_WD_d / get_WDShifts_d with L != len(x) (kernels.py:64-81, 115-135)."""
+    names = golden.names("WDd_p") + golden.names("WDSd_p")
+    assert len(names) >= 40
+    for name in names:
+        e = golden.entry(name)
+        x, y = golden.seqs(name)
+        kw = e["kwargs"]
+        if name.startswith("WDSd"):
+            v = cpu_ref.wds_pair(x, y, kw["d"], kw["S"], kw["L"])
+        else:
+            v = cpu_ref.wd_pair(x, y, kw["d"], kw["L"])
+        assert v == golden.K(name)[0], name
+
+
 @pytest.mark.parametrize("lb,k", [(0.5, 3), (1.0, 3), (0.7, 5), (0.3, 2), (0.5, 1)])
 def test_substring(golden, lb, k):
     name = f"SS_l{lb}_k{k}_xtr0_n10"
