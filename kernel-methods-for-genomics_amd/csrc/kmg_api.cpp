@@ -100,6 +100,7 @@ struct Tuning {
   int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
   int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
   int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table
+  int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
   int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
@@ -130,6 +131,7 @@ void read_tuning(Tuning &t) {
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
+  t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -715,10 +717,23 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
       if (p->span < 0) return fail(KMG_EINVAL, "span < 0");
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+      Packed pkd{nullptr, 0, 0};
+      const bool packed_wd = p->kind == KMG_WD && c->tune.wd_form == 0 && maxlen <= 256 &&
+                             p->span <= 256;
+      if (packed_wd) {  // 2-bit records: 7 words a pair at L = 101 (kmg_pairwise.hip)
+        const int cw = packed_cw(ldc), mw = packed_mw(ldc);
+        KMG_TRY(c->packed.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(1, n) * (cw + mw)));
+        pkd = Packed{c->packed.as<uint32_t>(), (int64_t)(cw + mw), cw};
+        StageTimer t(c, ST_PACK);
+        KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, 0, c->packed.as<uint32_t>(), c->stream));
+      }
       bool unsupported = false;
       const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         hipError_t e = p->kind == KMG_WD
-                           ? launch_gram_wd(q, r0, r1, p->d, p->span, p->coef_a, oq, c->stream)
+                           ? (packed_wd ? launch_gram_wd_packed(q, pkd, r0, r1, p->d, p->span,
+                                                                p->coef_a, oq, c->stream)
+                                        : launch_gram_wd(q, r0, r1, p->d, p->span, p->coef_a, oq,
+                                                         c->stream))
                            : launch_gram_wds(q, r0, r1, p->d, p->S, p->span, p->coef_a,
                                              p->coef_b, oq, c->stream);
         if (e == hipErrorNotSupported) {

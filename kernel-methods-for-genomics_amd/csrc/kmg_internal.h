@@ -196,6 +196,9 @@ struct SeqSpec {
 };
 hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, int span,
                           const double *beta, const OutSpec &o, hipStream_t s);
+hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row0, int64_t row1,
+                                 int d, int span, const double *beta, const OutSpec &o,
+                                 hipStream_t s);
 hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S, int span,
                            const double *beta, const double *delta, const OutSpec &o,
                            hipStream_t s);

@@ -173,6 +173,149 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
   }
 }
 
+// WD on the 2-bit packed records (Packed, kmg_internal.h).  Symbol q of code word w sits
+// at bits [30-2q, 31-2q]; with v = x_w ^ y_w, bit 31-2q of v | v << 1 is set iff the
+// symbols differ, so the match mask of a pair is M_w = keep_w & ~(v | v << 1), 2 bits a
+// position and position l+1 two bits below l.  keep_w holds the positions [1, min(Lx, Ly,
+// L)) (kernels.py:78: l >= 1; a slice clipped by either end never equals a full one, and
+// the range is symmetric in i, j).  Then A_1 = M, A_k = A_{k-1} & (A_{k-1} << 2) (one
+// funnel shift a word) and c_k = popc(A_k) = #{l in [1, L-k] : x[l:l+k] == y[l:l+k]}
+// (kernels.py:64-81); val accumulates beta_k * c_k in k order.  The k loop ends when no
+// lane of the wave has a run left: a skipped beta_k * 0 adds +0.0 (no rounding change).
+// A pair holding a non-ACGT symbol (mask bit below len) is compared byte by byte from the
+// codes (rare; exact for any alphabet).  Tile: 64 columns (one per lane, record in VGPRs)
+// x 64 rows (16 per wave, records read wave-uniform through the scalar cache).  MIRROR
+// (full square K): only tiles J >= I run; an off-diagonal tile also writes its transpose
+// from an LDS copy, 64 coalesced 512-B rows.
+__device__ __forceinline__ uint32_t wd_keep(int lim, int w) {
+  const int nv = min(max(lim - 16 * w, 0), 16);
+  return nv == 0 ? 0u : (0xAAAAAAAAu & (0xFFFFFFFFu << (32 - 2 * nv)));
+}
+
+__device__ __forceinline__ bool wd_has_other(const uint32_t *rec, int cw, int len) {
+  bool bad = false;
+  for (int w = 0; 32 * w < len; ++w) {
+    const int nv = min(len - 32 * w, 32);
+    const uint32_t below = nv >= 32 ? 0xFFFFFFFFu : ((1u << nv) - 1u);
+    bad |= (rec[cw + w] & below) != 0u;
+  }
+  return bad;
+}
+
+template <int NC>
+__device__ __forceinline__ void wd_mask_bytes(const SeqSpec &q, int64_t a, int64_t b, int lim,
+                                              uint32_t (&M)[NC]) {
+  const uint8_t *xa = q.codes + a * q.ldc, *yb = q.codes + b * q.ldc;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) {
+    uint32_t m = 0;
+    for (int t = 0; t < 16; ++t) {
+      const int pos = 16 * w + t;
+      if (pos >= 1 && pos < lim && xa[pos] == yb[pos]) m |= 1u << (31 - 2 * t);
+    }
+    M[w] = m;
+  }
+}
+
+template <int NC, bool MIRROR>
+__global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int64_t row0,
+                                                       int64_t row1, int d, int span, Coef cf,
+                                                       OutSpec o) {
+  constexpr int RB = 64;
+  constexpr int SW = NC | 1;  // odd word stride: the column reads are bank-conflict free
+  __shared__ double tile[MIRROR ? RB : 1][MIRROR ? 65 : 1];
+  __shared__ uint32_t srow[RB][SW], scol[64][SW];
+  __shared__ int slen[RB];  // row length, -1 - length if the row holds a non-ACGT symbol
+  if (MIRROR && blockIdx.x < blockIdx.y) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t rbase = row0 + (int64_t)blockIdx.y * RB;
+  const int64_t cbase = (int64_t)blockIdx.x * 64;
+  int Ly = 0;
+  bool cbad = false;
+  if (wave < 2) {  // wave 0 stages the rows, wave 1 the columns
+    const int64_t t = (wave == 0 ? rbase : cbase) + lane;
+    const int64_t lim = wave == 0 ? row1 : q.n;
+    uint32_t(*dst)[SW] = wave == 0 ? srow : scol;
+    int len = 0;
+    bool bad = false;
+    if (t < lim) {
+      const uint32_t *rec = pk.w + t * pk.ldp;
+#pragma unroll
+      for (int w = 0; w < NC; ++w) dst[lane][w] = w < pk.cw ? rec[w] : 0u;
+      len = q.lens[t];
+      bad = wd_has_other(rec, pk.cw, len);
+    } else {
+#pragma unroll
+      for (int w = 0; w < NC; ++w) dst[lane][w] = 0u;
+    }
+    if (wave == 0) slen[lane] = bad ? -1 - len : len;
+  }
+  __syncthreads();
+  const int64_t j = cbase + lane;
+  const bool jin = j < q.n;
+  const int64_t jj = jin ? j : 0;
+  Ly = q.lens[jj];
+  cbad = wd_has_other(pk.w + jj * pk.ldp, pk.cw, Ly);
+  uint32_t y[NC], ky[NC];
+  const int Lyc = span > 0 ? min(Ly, span) : Ly;
+#pragma unroll
+  for (int w = 0; w < NC; ++w) {
+    y[w] = scol[lane][w];
+    ky[w] = wd_keep(Lyc, w);
+  }
+  ky[0] &= 0x7FFFFFFFu;  // l >= 1
+  const bool diag_tile = MIRROR && blockIdx.x == blockIdx.y;
+  for (int r = wave; r < RB; r += 4) {
+    const int64_t i = rbase + r;
+    if (i >= row1) break;
+    const int sl = __builtin_amdgcn_readfirstlane(slen[r]);
+    const bool rbad = sl < 0;
+    const int Lx = rbad ? -1 - sl : sl;
+    double val;
+    if (i == j) {
+      val = __dadd_rn((double)(Lx - 1), (double)(1 - d) / 3.0);  // kernels.py:96
+    } else {
+      uint32_t A[NC];
+      if (rbad || cbad) {
+        const int lim = span > 0 ? min(min(Lx, Ly), span) : min(Lx, Ly);
+        wd_mask_bytes<NC>(q, i, jj, lim, A);
+      } else {
+#pragma unroll
+        for (int w = 0; w < NC; ++w) {
+          const uint32_t kx = wd_keep(Lx, w);
+          const uint32_t v = srow[r][w] ^ y[w];
+          A[w] = (kx & ky[w]) & ~(v | (v << 1));
+        }
+      }
+      val = 0.0;
+      for (int k = 1; k <= d; ++k) {
+        int c = 0;
+#pragma unroll
+        for (int w = 0; w < NC; ++w) c += __popc(A[w]);
+        if (!__any(c != 0)) break;
+        if (c) val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], (double)c));
+#pragma unroll
+        for (int w = 0; w < NC; ++w) {
+          const uint32_t nxt = (w + 1 < NC) ? A[w + 1] : 0u;
+          A[w] &= __builtin_amdgcn_alignbit(A[w], nxt, 30);  // (A_w << 2) | (A_{w+1} >> 30)
+        }
+      }
+    }
+    if (jin) store_f(o, i - row0, j, val);
+    if (MIRROR) tile[r][lane] = val;
+  }
+  if (MIRROR && !diag_tile) {
+    __syncthreads();
+    // transpose: row j = J*64 + c of K gets columns I*64 + lane
+    const int64_t icol = rbase + lane;
+    for (int c = wave; c < 64; c += 4) {
+      const int64_t jr = cbase + c;
+      if (jr >= q.n) break;
+      if (icol < row1) store_f(o, jr - row0, icol, tile[lane][c]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ WDS
 // c_st = sum_{i=1}^{L-k} sum_{s=0}^{S} [s+i<L] delta_s * ([x[i+s:i+s+k]==y[i:i+k]] +
 // [x[i:i+k]==y[i+s:i+s+k]]), accumulated in exactly that (i, s) order; K += beta_k*c_st
@@ -495,6 +638,35 @@ hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, i
     hipLaunchKernelGGL((gram_wd_kernel<2>), grid, dim3(256), 0, s, q, row0, row1, d, span, cf, o);
   else
     hipLaunchKernelGGL((gram_wd_kernel<4>), grid, dim3(256), 0, s, q, row0, row1, d, span, cf, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row0, int64_t row1,
+                                 int d, int span, const double *beta, const OutSpec &o,
+                                 hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || q.n == 0) return hipSuccess;
+  const int need = (q.maxlen + 15) / 16;  // code words a pair compares
+  if (need > pk.cw) return hipErrorInvalidValue;
+  const Coef cf = make_coef(beta, nullptr);
+  // the whole square: upper tiles + transposed copies
+  const bool mirror = row0 == 0 && row1 == q.n;
+  const dim3 grid((unsigned)((q.n + 63) / 64), (unsigned)((rows + 63) / 64));
+#define KMG_WDP(NC_)                                                                             \
+  do {                                                                                           \
+    if (mirror)                                                                                  \
+      hipLaunchKernelGGL((gram_wdp_kernel<NC_, true>), grid, dim3(256), 0, s, q, pk, row0, row1, \
+                         d, span, cf, o);                                                        \
+    else                                                                                         \
+      hipLaunchKernelGGL((gram_wdp_kernel<NC_, false>), grid, dim3(256), 0, s, q, pk, row0,     \
+                         row1, d, span, cf, o);                                                  \
+  } while (0)
+  if (need <= 4) KMG_WDP(4);
+  else if (need <= 7) KMG_WDP(7);
+  else if (need <= 8) KMG_WDP(8);
+  else if (need <= 16) KMG_WDP(16);
+  else return hipErrorNotSupported;
+#undef KMG_WDP
   return hipGetLastError();
 }
 

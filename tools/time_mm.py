@@ -60,6 +60,14 @@ def main():
                 st[s] = round(tot / cnt, 4)
         ctx.set_timing(False)
         ok = None
+        if case.get("check", True) and kind == "wd":
+            import cref
+            import ctypes
+            ok = True
+            for r in (0, rows // 2, rows - 1):
+                row = np.empty(n, dtype=np.float64)
+                ctx.d2h(row, ctypes.c_void_p(do.value + r * n * esz))
+                ok &= bool(np.array_equal(row, cref.wd(codes, lens, case.get("d", 5), rows=(r, r + 1))[0]))
         if case.get("check", True) and kind == "mm":
             import cref
             r = rows - 1
