@@ -591,7 +591,7 @@ def main():
         "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
         "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": sp["ms_per_step"], "higher_is_better": True,
-        "scaling": "strong" if dist.world > 1 else "weak",
+        "scaling": "strong",  # fixed N at every G (SURVEY §8d t_build incl. all-gather)
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(2)",
         "config": {"workload": "spectrum k=8 full-K build, N=20000 x L=101 (BASELINE "

@@ -119,10 +119,10 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, Packed pk,
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   const int words = PACK16 ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
-  uint32_t *srec = acc + words;
+  // the row's record (52 B at L = 101) is read through the vector cache: one line a block
+  const uint32_t *__restrict__ srec = pk.w + i * pk.ldp;
   uint4 *acc4 = (uint4 *)acc;
   for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
-  stage_record(pk, i, srec);
   __syncthreads();
 
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
@@ -764,7 +764,7 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   const bool pack = g.pmax <= 255;
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
-  const size_t lds = ((size_t)words + (size_t)pk.ldp) * 4;
+  const size_t lds = (size_t)words * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
   // non-temporal 16-byte stores: K is written once and never re-read by this launch
   if (pack) {
