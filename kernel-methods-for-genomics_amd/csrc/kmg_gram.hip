@@ -354,23 +354,28 @@ __global__ __launch_bounds__(1024) void gram_mm1_kernel(IndexGeom g, Packed pk,
 // ------------------------------------------------------------------ mismatch m=1, pair table
 // Drop-two-letters formulation (PairGeom, kmg_internal.h).  For a row k-mer u and a pair
 // p < q, group key_pq(u) holds every occurrence z that agrees with u outside {p, q}, in 16
-// sub-bins (z_p, z_q), z_p-major.  Weights, an inclusion-exclusion over the pairs that
-// leaves every group but k-1 of the 36 with ONE interval test per entry:
-//   every pair: entries with z_p != u_p (all but the contiguous row u_p)  -> w2
-//     this counts each Hamming-2 neighbour at {p, q} once, and each Hamming-1 neighbour
-//     at r (k-1-r) times (the pairs (r, q > r)), Hamming 0 never;
-//   pairs (0, r), r >= 1, additionally: row u_0 (z_0 = u_0: Hamming 1 at r, or 0):
-//     Hamming 1 at r -> c_r = w1 - (k-1-r) w2, the exact bin (u_0, u_r) -> w0 for r = 1
-//     only; and for r = 1 the column bins (z_0 != u_0, z_1 = u_1) = Hamming 1 at 0 get
-//     c_0 = w1 - (k-1) w2 on top of w2.
+// sub-bins (z_p, z_q), z_p-major.  Weights, an inclusion-exclusion that leaves every entry
+// of every group with the same weight w2 and NO per-entry test:
+//   every entry of every group -> w2.  A Hamming-2 neighbour at {a, b} sits in group
+//     (a, b) only; a Hamming-1 neighbour at r in the k-1 groups (p, q) holding r; the
+//     row's own k-mer (Hamming 0) in all k(k-1)/2.
+//   corrections, in the pairs (0, r) only (k-1 of the 36 lists of a window):
+//     row u_0 of (0, r) minus the exact bin (z_0 = u_0, z_r != u_r: Hamming 1 at r)
+//       -> + c = w1 - (k-1) w2;
+//     r = 1: the exact bin (u_0, u_1) (Hamming 0) -> + h0 = w0 - k(k-1)/2 w2, and the
+//       column bins (z_0 != u_0, z_1 = u_1: Hamming 1 at 0) -> + c.
 // Net: every Hamming <= 2 neighbour gets exactly w[ham] (the closed form of
-// <Phi_x, Phi_y>, kernels.py:161-175, 211-215).  Per row: k(k-1)/2 lists per window (36
-// at k = 9, against 117 one-line lists of the drop-one table), each a few whole lines.
-// Eight lanes per list; per list (pipelined): a 32-byte summary record (L2) gives the
-// group's first line and line count nl (DPP sums over the 8 lanes), then lane gl loads the
-// group header and its pieces [gl*nl, gl*nl + nl) with buffer loads (pieces past nl fall
-// outside the buffer: no traffic), builds 64-bit masks of its entries from the 16
-// bin-end bytes and adds the weights with LDS atomics.
+// <Phi_x, Phi_y>, kernels.py:161-175, 211-215).  The pack kernel fills the tail of a
+// group's last line with lane-spread dummy columns (64 LDS words past the accumulator),
+// so a lane adds w2 for every halfword of its pieces: one SDWA + one ds_add per entry.
+// Per row: k(k-1)/2 lists per window (36 at k = 9, against 117 one-line lists of the
+// drop-one table), each a few whole lines.
+// Four lanes per list (the per-list decode is shared by fewer lanes than entries: 8 lanes
+// doubled the VALU work per line); per list (pipelined): a 32-byte summary record (L2)
+// gives the group's first line and line count nl (DPP sums over the 4 lanes), then lane gl
+// loads the group header and its pieces [2 gl nl, 2 gl nl + 2 nl) with buffer loads
+// (pieces past them fall outside the buffer: no traffic), builds 64-bit masks of its
+// entries from the 16 bin-end bytes and adds the weights with LDS atomics.
 __device__ __forceinline__ uint64_t span_mask(int a, int b) {  // bits [a, b) of 0..63
   const int lo = min(max(a, 0), 64), hi = min(max(b, 0), 64);
   const uint64_t mh = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
@@ -381,12 +386,10 @@ __device__ __forceinline__ uint32_t nibble_sum(uint32_t x) {
   const uint32_t y = (x & 0x0F0F0F0Fu) + ((x >> 4) & 0x0F0F0F0Fu);
   return (y * 0x01010101u) >> 24;
 }
-// sum over each aligned group of 8 lanes, result in all 8 (DPP: half-row mirror, then the
-// two quad swaps)
-__device__ __forceinline__ uint32_t sum8(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+// sum over each aligned group of 4 lanes, result in all 4 (DPP quad swaps)
+__device__ __forceinline__ uint32_t sum4(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
   return v;
 }
 // start / end of sub-bin b from the header dwords (bin ends as bytes, e[15] = n)
@@ -408,7 +411,9 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
                                                         const uint16_t *__restrict__ xent,
                                                         int64_t row0, int64_t rows, int w0, int w1,
                                                         int w2, OutSpec o) {
-  constexpr int G = 8, MAXP = 5;
+  // G lanes per list; a lane takes 2 nl of the group's 8 nl 16-byte pieces, MAXP of them
+  // in registers: groups of > 3 lines (n > 184) go the exact-index way like wide ones
+  constexpr int G = 4, MAXP = 6, MAXNL = MAXP * G / 8;
   constexpr int NP = K * (K - 1) / 2;
   constexpr uint32_t NK2 = 1u << (2 * (K - 2));
   // one dynamic LDS block, accumulator first: col_addr_sdwa needs acc at LDS offset 0, so
@@ -421,12 +426,12 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   const int accw = ((g.chunk + 3) >> 2) << 2;
   const int P = g.pmax;
-  int32_t *acc = (int32_t *)smem;
-  uint32_t *rowk = smem + accw;  // [P] row k-mers (KMG_INVALID: skipped)
+  int32_t *acc = (int32_t *)smem;  // [accw] + 64 dummy words (the pack kernel's padding)
+  uint32_t *rowk = smem + accw + 64;  // [P] row k-mers (KMG_INVALID: skipped)
   uint32_t *srec = rowk + P;     // packed row record
   uint32_t *spq = srec + pk.ldp; // [NP] p | q << 8 of every pair
   uint4 *acc4 = (uint4 *)acc;
-  for (int w = threadIdx.x; w < (accw >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  for (int w = threadIdx.x; w < (accw >> 2) + 16; w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
   stage_record(pk, i, srec);
   if (threadIdx.x < NP) spq[threadIdx.x] = pg.pq[threadIdx.x];
   __syncthreads();
@@ -439,7 +444,8 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   const int total = NP * P;
   const uint32_t chunk_base = (uint32_t)c * NK2;
   const uint32_t pair_stride = (uint32_t)g.nchunks * NK2;
-  const int c0 = w1 - (K - 1) * w2;  // Hamming 1 at 0, on top of the w2 it got K-1 times
+  const int cc = w1 - (K - 1) * w2;   // Hamming 1: on top of the w2 of its K-1 groups
+  const int h0 = w0 - NP * w2;        // Hamming 0: on top of the w2 of all NP groups
 
   // the lists of this lane group: L = grp + t * ngrp, pair-major (pi, a) = divmod(L, P),
   // walked incrementally (no division per list)
@@ -463,37 +469,52 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
       ++nx_pi;
     }
   };
-  // summary dword gl of the group's record
-  auto load_summary = [&](uint32_t gidx) -> uint32_t { return summary[(size_t)(gidx >> 5) * 8 + gl]; };
-  // base line and line count of the group from the 8 lanes' summary dwords
-  auto decode = [&](uint32_t sw, uint32_t gidx, uint32_t meta, uint32_t &base, uint32_t &nl) {
-    const int r = (int)(gidx & 31u);
-    const int below = r - 8 * (gl - 1);  // lanes 1..4: nibbles of this word before group r
-    const bool nib = gl >= 1 && gl <= 4;
-    const uint32_t m = below >= 8 ? 0xFFFFFFFFu : (below <= 0 ? 0u : ((1u << (4 * below)) - 1u));
-    const uint32_t part = gl == 0 ? sw : (nib ? nibble_sum(sw & m) : 0u);
-    const uint32_t own = (nib && below >= 0 && below < 8) ? (sw >> (4 * below)) & 15u : 0u;
-    base = sum8(part);
-    nl = (meta & 16u) ? sum8(own) : 0u;
+  // summary dwords 2 gl, 2 gl + 1 of the group's record (dword 0: base line, dwords 1..4:
+  // line-count nibbles of groups 0..31)
+  auto load_summary = [&](uint32_t gidx) -> uint2 {
+    return ((const uint2 *)summary)[(size_t)(gidx >> 5) * 4 + gl];
   };
-  // header (piece 0) and this lane's pieces [gl * nl, gl * nl + nl)
+  // nibble sum of word w (1..4) over the groups before r, and group r's own nibble
+  auto nib_part = [&](uint32_t sw, int w, int r, uint32_t &part, uint32_t &own) {
+    const int below = r - 8 * (w - 1);
+    const uint32_t m = below >= 8 ? 0xFFFFFFFFu : (below <= 0 ? 0u : ((1u << (4 * below)) - 1u));
+    part += nibble_sum(sw & m);
+    own += (below >= 0 && below < 8) ? (sw >> (4 * below)) & 15u : 0u;
+  };
+  // base line and line count of the group from the 4 lanes' summary dwords
+  auto decode = [&](uint2 sw, uint32_t gidx, uint32_t meta, uint32_t &base, uint32_t &nl) {
+    const int r = (int)(gidx & 31u);
+    uint32_t part = 0, own = 0;
+    if (gl == 0) {
+      part = sw.x;
+      nib_part(sw.y, 1, r, part, own);
+    } else if (gl == 1) {
+      nib_part(sw.x, 2, r, part, own);
+      nib_part(sw.y, 3, r, part, own);
+    } else if (gl == 2) {
+      nib_part(sw.x, 4, r, part, own);
+    }
+    base = sum4(part);
+    nl = (meta & 16u) ? sum4(own) : 0u;
+  };
+  // header (piece 0) and this lane's pieces [gl * 2nl, gl * 2nl + 2nl)
   auto load_lines = [&](uint32_t base, uint32_t nl, uint4 &hdr, uint4(&d)[MAXP]) {
-    const uint32_t first = (uint32_t)gl * nl;
+    const uint32_t np = nl <= (uint32_t)MAXNL ? 2u * nl : 0u;  // pieces of this lane
+    const uint32_t first = (uint32_t)gl * np;
     hdr = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, nl ? base * 128u : 0xFFFFFFF0u, 0, 0));
 #pragma unroll
     for (int s = 0; s < MAXP; ++s) {
-      const uint32_t off = (uint32_t)s < nl ? (base * 128u + (first + (uint32_t)s) * 16u) : 0xFFFFFFF0u;
+      const uint32_t off = (uint32_t)s < np ? (base * 128u + (first + (uint32_t)s) * 16u) : 0xFFFFFFF0u;
       d[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, off, 0, 0));
     }
   };
-  // weight of sub-bin (zp, zq) for the list (inclusion-exclusion above)
-  auto bin_weight = [&](uint32_t meta, uint32_t zp, uint32_t zq) -> int {
-    if (!(meta & 16u)) return 0;
+  // correction of sub-bin (zp, zq) on top of w2 (pairs (0, r) only; see above)
+  auto bin_corr = [&](uint32_t meta, uint32_t zp, uint32_t zq) -> int {
+    if (!(meta & 32u)) return 0;
     const uint32_t up = meta & 3u, uq = (meta >> 2) & 3u;
-    if (!(meta & 32u)) return zp != up ? w2 : 0;
     const int r = (int)(meta >> 8);
-    if (zp != up) return w2 + ((r == 1 && zq == uq) ? c0 : 0);
-    return zq == uq ? (r == 1 ? w0 : 0) : w1 - (K - 1 - r) * w2;
+    if (zp == up) return zq == uq ? (r == 1 ? h0 : 0) : cc;
+    return (r == 1 && zq == uq) ? cc : 0;
   };
   // wide group (> 255 entries): every bin straight from the exact index
   auto wide = [&](uint32_t gidx, uint32_t meta) {
@@ -502,7 +523,7 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
     const int p = spq[pi] & 0xFF, q = spq[pi] >> 8;
     const uint32_t *xo = xoff + (size_t)c * ((size_t)NK2 << 4);
     for (uint32_t b = 0; b < 16; ++b) {
-      const int w = bin_weight(meta, b >> 2, b & 3u);
+      const int w = (meta & 16u) ? w2 + bin_corr(meta, b >> 2, b & 3u) : 0;
       if (!w) continue;
       const uint32_t z = pair_insert(key, K, p, q, b >> 2, b & 3u);
       const uint32_t e1 = xo[z + 1];
@@ -517,52 +538,53 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
                      uint32_t meta) {
     if (nl == 0) return;
     const uint32_t hd[4] = {hdr.x, hdr.y, hdr.z, hdr.w};
-    if ((hdr.w >> 16) == 0x00FFu) {  // byte 14 = 0xFF, byte 15 = 0: wide marker
+    // wide marker (byte 14 = 0xFF, byte 15 = 0) or more lines than the lanes hold
+    if ((hdr.w >> 16) == 0x00FFu || nl > (uint32_t)MAXNL) {
       wide(gidx, meta);
       return;
     }
-    const int up = (int)(meta & 3u), n = (int)(hdr.w >> 24);
-    // this lane's entries: piece gl*nl holds entries 8 (gl*nl) - 8 ..; valid = [0, n)
-    const int t0 = 8 * gl * (int)nl - 8;
-    const uint64_t vm = span_mask(-t0, min(n - t0, 8 * (int)nl));
-    const uint64_t rm = span_mask(bin_start(hd, 4 * up) - t0, bin_end(hd, 4 * up + 3) - t0);
-    if (!__any(meta & 32u)) {  // no pair (0, r) list in this wave: one interval per entry
-      const uint64_t act = vm & ~rm;
+    const int np = 2 * (int)nl;  // pieces of this lane; piece 0 of the group is the header
+    // pieces [1, pe) hold the n entries (the last one padded with dummy columns): + w2 for
+    // every halfword of them
+    const int n = (int)(hdr.w >> 24);
+    const int pe = min(np, ((n + 7) >> 3) + 1 - gl * np);  // this lane's live pieces: sp < pe
+    const int p0 = gl == 0 ? 1 : 0;
 #pragma unroll
-      for (int s = 0; s < MAXP; ++s) {
-        if (!__any((uint32_t)s < nl)) break;
-        const uint32_t m8 = (uint32_t)(act >> (8 * s)) & 0xFFu;
-        const uint32_t wd[4] = {d[s].x, d[s].y, d[s].z, d[s].w};
+    for (int sp = 0; sp < MAXP; ++sp) {
+      if (!__any(sp < pe)) break;
+      if (sp >= p0 && sp < pe) {
+        const uint32_t wd[4] = {d[sp].x, d[sp].y, d[sp].z, d[sp].w};
 #pragma unroll
         for (int v = 0; v < 8; ++v)
-          if (m8 & (1u << v))
-            add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w2);
+          add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w2);
       }
-      return;
     }
-    // general form (pairs (0, r) in this wave): per-entry weight from row / bin / column
-    const int uq = (int)((meta >> 2) & 3u), r = (int)(meta >> 8);
-    const bool special = meta & 32u;
-    const int cr = w1 - (K - 1 - r) * w2;
-    const int wrow = special ? cr : 0, wex = (special && r == 1) ? w0 : 0;
-    const int wcol = (special && r == 1) ? w2 + c0 : w2;
-    const uint64_t bm = special ? span_mask(bin_start(hd, 4 * up + uq) - t0, bin_end(hd, 4 * up + uq) - t0) : 0ull;
+    if (!__any(meta & 32u)) return;
+    if (!(meta & 32u)) return;
+    // corrections of a pair (0, r) list: row u_0 (minus / plus the exact bin) and, for
+    // r = 1, the column bins (z_0 != u_0, z_1 = u_1)
+    const int up = (int)(meta & 3u), uq = (int)((meta >> 2) & 3u), r = (int)(meta >> 8);
+    const int t0 = 8 * gl * np - 8;  // entry index of the lane's first halfword
+    const uint64_t rm = span_mask(bin_start(hd, 4 * up) - t0, bin_end(hd, 4 * up + 3) - t0);
+    const uint64_t bm = span_mask(bin_start(hd, 4 * up + uq) - t0, bin_end(hd, 4 * up + uq) - t0);
     uint64_t cm = 0;
-    if (special && r == 1) {
+    if (r == 1) {
 #pragma unroll
       for (int zp = 0; zp < 4; ++zp)
-        cm |= span_mask(bin_start(hd, 4 * zp + uq) - t0, bin_end(hd, 4 * zp + uq) - t0);
+        if (zp != up) cm |= span_mask(bin_start(hd, 4 * zp + uq) - t0, bin_end(hd, 4 * zp + uq) - t0);
     }
+    const int wb = r == 1 ? h0 : 0;
+    const uint64_t any = rm | cm;
 #pragma unroll
-    for (int s = 0; s < MAXP; ++s) {
-      if (!__any((uint32_t)s < nl)) break;
-      const uint32_t wd[4] = {d[s].x, d[s].y, d[s].z, d[s].w};
+    for (int sp = 0; sp < MAXP; ++sp) {
+      const uint32_t m8 = sp < np ? (uint32_t)(any >> (8 * sp)) & 0xFFu : 0u;
+      if (!__any(m8 != 0u)) continue;
+      const uint32_t wd[4] = {d[sp].x, d[sp].y, d[sp].z, d[sp].w};
 #pragma unroll
       for (int v = 0; v < 8; ++v) {
-        const int j = 8 * s + v;
-        if ((vm >> j) & 1ull) {
-          const bool inr = (rm >> j) & 1ull;
-          const int w = inr ? (((bm >> j) & 1ull) ? wex : wrow) : (((cm >> j) & 1ull) ? wcol : w2);
+        if (m8 & (1u << v)) {
+          const int j = 8 * sp + v;
+          const int w = ((bm >> j) & 1ull) ? wb : cc;
           if (w) add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w);
         }
       }
@@ -574,7 +596,8 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   // list (loaded one round ago); per round and slot: atomics of the current list, decode
   // of the next list's summary + its line loads, then the summary load of the list after.
   uint4 dat[D][MAXP], hdr[D];
-  uint32_t nl[D], gid[D], met[D], gidn[D], metn[D], swn[D];
+  uint32_t nl[D], gid[D], met[D], gidn[D], metn[D];
+  uint2 swn[D];
 #pragma unroll
   for (int r = 0; r < D; ++r) {
     describe_next(gid[r], met[r]);
@@ -811,7 +834,7 @@ hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, c
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
   if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   if (nlines * 128 >= 0xFFFFFFF0LL) return hipErrorInvalidValue;  // 32-bit buffer offsets
-  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax + pk.ldp + KMG_PAIRS_MAX) * 4;
+  const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + 64 + g.pmax + pk.ldp + KMG_PAIRS_MAX) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)(rows * g.nchunks));
   const uint32_t lb = (uint32_t)(nlines * 128);

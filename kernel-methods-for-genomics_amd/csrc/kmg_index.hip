@@ -422,7 +422,11 @@ __global__ __launch_bounds__(256) void pair_pack_kernel(PairGeom pg,
   const bool live = g < pg.ngroups();
   // record base -> summary w0 (first lane of each record's first group)
   if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5];
-  for (int w = b; w < PAIR_MAX_LINES * 32; w += 16) img[lg][w] = 0;
+  // header words 0; every other halfword h a dummy column acc_words + (h & 63) (64 LDS words
+  // past the Gram kernel's accumulator, one per lane: conflict-free no-op adds)
+  const uint32_t dcol = (uint32_t)(((pg.chunk + 3) >> 2) << 2);
+  for (int w = b; w < PAIR_MAX_LINES * 32; w += 16)
+    img[lg][w] = w < 4 ? 0u : (dcol + ((2u * w) & 63u)) | ((dcol + ((2u * w + 1u) & 63u)) << 16);
   uint32_t s0 = 0, cnt = 0, key = 0;
   int p = 0, q = 1, c = 0;
   if (live) {
@@ -480,6 +484,7 @@ hipError_t launch_pair_pack(const PairGeom &pg, const uint32_t *xoff, const uint
                             hipStream_t s) {
   const int64_t blocks = (pg.ngroups() + PAIR_PACK_GROUPS - 1) / PAIR_PACK_GROUPS;
   if (blocks == 0) return hipSuccess;
+  if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
   hipLaunchKernelGGL(pair_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent,
                      rbase, summary, lines);
   return hipGetLastError();
