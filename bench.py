@@ -41,6 +41,7 @@ from kmgram.shard import block_cyclic_ranges, default_block, rows_padded  # noqa
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 XGMI_IN_PEAK = 7 * 76.5e9  # per-GPU ingress: 7 xGMI links x ~76.5 GB/s per direction
+GATHER_CEILING = 56.38e9  # random 128-B lines/s from a 78.6 MB table (profiles/r02_mall_gather.jsonl)
 INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROARCH.md)
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
           "(k=9,m=1), 1/2/4/8 GPUs")
@@ -613,6 +614,16 @@ def main():
             "N": n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
             "hbm_frac_of_gram_kernel": mm_bytes / (mm["stages_ms"]["gram"] / 1e3) / HBM_PEAK,
+            # the kernel's real bound: one random 128-B slot line per posting list, 117 lists
+            # per window (k + 3k(k-1)/2 at k = 9), 93 windows per row, against the measured
+            # random-line gather ceiling of a 79 MB table (tools/mall_gather.hip)
+            "gather_roofline": {
+                "bound": "infinity-cache random 128-B line gathers",
+                "lines_per_launch": mm_rows_launch * 93 * 117,
+                "achieved_Glines_per_s": mm_rows_launch * 93 * 117 / (mm["stages_ms"]["gram"] / 1e3) / 1e9,
+                "ceiling_Glines_per_s": GATHER_CEILING / 1e9,
+                "frac": mm_rows_launch * 93 * 117 / (mm["stages_ms"]["gram"] / 1e3) / GATHER_CEILING,
+                "source": "profiles/r02_mall_gather.jsonl (78.6 MB table, 128-B lines)"},
             "spot_check": mm["spot_check"],
         }
         if "collective_free" in mm:

@@ -61,6 +61,17 @@ def test_encode_roundtrip():
     assert c2[0, 1] == c2[1, 0] >= 132
 
 
+def test_encode_non_ascii_cap():
+    """123 distinct non-ASCII characters take codes 132..254 (255 stays the padding code);
+    a 124th is refused."""
+    chars = [chr(0x100 + t) for t in range(123)]
+    codes, lens = E.encode(["".join(chars), "A"])
+    assert sorted(set(codes[0, :123].tolist())) == list(range(132, 255))
+    assert codes[1, 1] == 255  # padding
+    with pytest.raises(ValueError):
+        E.encode(["".join(chars) + chr(0x100 + 123)])
+
+
 def test_synthetic_generator_matches_survey():
     codes, lens = E.synthetic(4, 101, seed=20261015)
     assert "".join("ACGT"[c] for c in codes[0, :16]) == "GACTCCTCGGACGGCG"
