@@ -110,6 +110,7 @@ struct Tuning {
   int idx_threads = 1024;   // KMG_IDX_THREADS
   int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
   int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky
+  int sp_store = 0;         // KMG_SP_STORE: spectrum K stores, 0 auto, 1 non-temporal, 2 plain
 };
 
 int env_or(const char *name, int dflt) {
@@ -132,6 +133,7 @@ void read_tuning(Tuning &t) {
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
+  t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -264,7 +266,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
     KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
     KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(nblk * cap)));
     KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
-    KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 64)));  // + pad: clamped reads
+    KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 512)));  // + pad: whole-piece reads
     {
       StageTimer t(c, ST_PLACE);
       KMG_HIP(launch_index_local(g, pk, (int)nblk, (uint32_t)cap,
@@ -286,7 +288,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
   KMG_TRY(c->bcursor.ensure(sizeof(uint32_t) * (size_t)nbk));
   KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
   KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
-  KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 64)));  // + pad: clamped reads
+  KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 512)));  // + pad: whole-piece reads
   // bucket counters are zero between calls (the fine pass re-zeroes them); only a fresh
   // allocation or an interrupted previous build needs an explicit clear
   if (realloc || c->index_dirty) {
@@ -702,7 +704,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       }
       return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         return exact ? launch_gram_spectrum(g, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
-                                            r0, r1, oq, c->stream)
+                                            r0, r1, oq, c->stream, c->tune.sp_store)
                      : launch_gram_mismatch1_slots(g, pkd, c->slots.as<uint4>(),
                                                    c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                                    r0, r1, (int)w[0], (int)w[1], (int)w[2], oq,

@@ -104,14 +104,23 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
 }
 
 // ------------------------------------------------------------------ spectrum
-// PACK16: two 16-bit counters per LDS word (valid when every K_ij <= 65535, i.e.
-// P_i * P_j <= 65535; the host checks P_max <= 255).  One lane per row window walks that
-// k-mer's posting list (k = 8, N = 20000: ~28 entries) with 8 independent loads in flight.
+// One workgroup of 1024 threads owns (row i, column chunk c); PACK16: two 16-bit counters
+// per LDS word (valid when every K_ij <= 65535, i.e. P_i * P_j <= 65535; the host checks
+// P_max <= 255), so a 20000-column chunk is 40 KB and two rows are in flight per CU.
+// Gather: lpw lanes per row window (a power of two filling the block: 8 at 94 windows);
+// the window's posting list is read as aligned 16-byte pieces of 8 entries, lane s of the
+// window taking pieces s, s + lpw, ...; the first two pieces of every lane are issued
+// before the accumulator is cleared, so the clear overlaps the entry loads.  Only pieces
+// holding entries of the list are read.
+// Store: 16 bytes per lane and step, every store instruction of a wave covering 1 KB of
+// the row (int32 / float32: 4 columns a lane; float64: 2), so every line is written whole.
+// NT: non-temporal stores (measured faster for multi-chunk and float64 K; plain stores
+// faster for a single-chunk int32 K, profiles/r02t_sp_store.jsonl).
 template <bool PACK16, int DT, bool NT>
-__global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, Packed pk,
-                                                      const uint32_t *__restrict__ off,
-                                                      const uint16_t *__restrict__ ent,
-                                                      int64_t row0, OutSpec o) {
+__global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
+                                                       const uint32_t *__restrict__ off,
+                                                       const uint16_t *__restrict__ ent,
+                                                       int64_t row0, OutSpec o) {
   extern __shared__ __align__(16) uint32_t acc[];
   const int64_t il = blockIdx.x / g.nchunks;
   const int64_t i = row0 + il;
@@ -119,46 +128,113 @@ __global__ __launch_bounds__(256) void gram_sp_kernel(IndexGeom g, Packed pk,
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   const int words = PACK16 ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
-  // the row's record (52 B at L = 101) is read through the vector cache: one line a block
   const uint32_t *__restrict__ srec = pk.w + i * pk.ldp;
-  uint4 *acc4 = (uint4 *)acc;
-  for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
+  const uint4 *__restrict__ e4 = (const uint4 *)ent;
   auto add = [&](uint32_t j0) {
     if (PACK16)
       atomicAdd(&acc[j0 >> 1], 1u << ((j0 & 1) << 4));
     else
       atomicAdd(&acc[j0], 1u);
   };
-  for (int a = threadIdx.x; a < g.pmax; a += blockDim.x) {
-    const uint32_t u = pk_window(srec, pk.cw, a, g.k);  // windows past len are masked
-    if (u == KMG_INVALID) continue;
-    const uint32_t beg = o_c[u], end = o_c[u + 1];
-    uint32_t e = beg;
-    for (; e + 8 <= end; e += 8) {
-      uint32_t j[8];
+  // entries of piece q (halfwords [8q, 8q + 8)) that fall in [beg, end)
+  auto piece = [&](const uint4 &v, uint32_t q, uint32_t beg, uint32_t len) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) j[q] = ent[e + q];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) add(j[q]);
+    for (int h = 0; h < 8; ++h) {
+      const uint32_t rel = 8u * q + (uint32_t)h - beg;
+      if (rel < len) add((w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu);
     }
-    for (; e < end; ++e) add(ent[e]);
+  };
+  // lanes per window: a power of two, >= 2, so that the windows of a row fill the block
+  int lpw = 2;
+  while (lpw < 16 && (lpw << 1) * g.pmax <= (int)blockDim.x) lpw <<= 1;
+  const int sub = threadIdx.x & (lpw - 1);
+  const int nwin = blockDim.x / lpw;
+  int a = threadIdx.x / lpw;
+  uint32_t beg = 0, len = 0;
+  if (a < g.pmax) {
+    const uint32_t u = pk_window(srec, pk.cw, a, g.k);
+    if (u != KMG_INVALID) {
+      beg = o_c[u];
+      len = o_c[u + 1] - beg;
+    }
+  }
+  uint32_t q0 = beg >> 3;
+  uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0;
+  // only pieces that hold entries of the list are read
+  if (len && 8u * (q0 + sub) < beg + len) p0 = e4[q0 + sub];
+  if (len && 8u * (q0 + sub + lpw) < beg + len) p1 = e4[q0 + sub + lpw];
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  for (;;) {
+    if (len) {
+      if (8u * (q0 + sub) < beg + len) piece(p0, q0 + sub, beg, len);
+      if (8u * (q0 + sub + lpw) < beg + len) piece(p1, q0 + sub + lpw, beg, len);
+      for (uint32_t q = q0 + 2 * lpw + sub; 8u * q < beg + len; q += lpw) piece(e4[q], q, beg, len);
+    }
+    a += nwin;
+    if (a >= g.pmax) break;  // more windows than lane groups (long sequences)
+    len = 0;
+    const uint32_t u = pk_window(srec, pk.cw, a, g.k);
+    if (u != KMG_INVALID) {
+      beg = o_c[u];
+      len = o_c[u + 1] - beg;
+    }
+    q0 = beg >> 3;
+    if (len && 8u * (q0 + sub) < beg + len) p0 = e4[q0 + sub];
+    if (len && 8u * (q0 + sub + lpw) < beg + len) p1 = e4[q0 + sub + lpw];
   }
   __syncthreads();
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
-  for (int q = threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
-    uint32_t v0, v1, v2, v3;
-    if (PACK16) {
-      const uint2 w = *(const uint2 *)&acc[q >> 1];
-      v0 = w.x & 0xFFFFu; v1 = w.x >> 16; v2 = w.y & 0xFFFFu; v3 = w.y >> 16;
-    } else {
-      const uint4 w = *(const uint4 *)&acc[q];
-      v0 = w.x; v1 = w.y; v2 = w.z; v3 = w.w;
+  if constexpr (DT == KMG_F64) {
+    // two columns (16 B) per lane and step, so every store instruction of a wave covers
+    // 1 KB of the row contiguously (whole lines: no partial-line writes)
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    double *prow = (double *)o.out + il * o.ld + col0;
+    const bool al = (((uintptr_t)prow) & 15) == 0;
+    const double di = norm ? o.dsq[i] : 1.0;
+    for (int q = threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
+      uint32_t v0, v1;
+      if (PACK16) {
+        const uint32_t w = acc[q >> 1];
+        v0 = w & 0xFFFFu; v1 = w >> 16;
+      } else {
+        const uint2 w = *(const uint2 *)&acc[q];
+        v0 = w.x; v1 = w.y;
+      }
+      const int64_t c0 = col0 + q;
+      const bool two = q + 1 < cw;
+      double r0 = (double)v0, r1 = (double)v1;
+      if (norm) {  // normalize_K: K[i,j] / (sqrt(K[i,i]) * sqrt(K[j,j])), diagonal := 1
+        r0 = (i == c0) ? 1.0 : (double)v0 / (di * o.dsq[c0]);
+        r1 = !two ? 0.0 : (i == c0 + 1) ? 1.0 : (double)v1 / (di * o.dsq[c0 + 1]);
+      }
+      if (al && two) {
+        const v2d x = {r0, r1};
+        if constexpr (NT)
+          __builtin_nontemporal_store(x, (v2d *)(prow + q));
+        else
+          *(v2d *)(prow + q) = x;
+      } else {
+        prow[q] = r0;
+        if (two) prow[q + 1] = r1;
+      }
     }
-    emit4<DT, NT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
+  } else {
+    for (int q = threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
+      uint32_t v0, v1, v2, v3;
+      if (PACK16) {
+        const uint2 w = *(const uint2 *)&acc[q >> 1];
+        v0 = w.x & 0xFFFFu; v1 = w.x >> 16; v2 = w.y & 0xFFFFu; v3 = w.y >> 16;
+      } else {
+        const uint4 w = *(const uint4 *)&acc[q];
+        v0 = w.x; v1 = w.y; v2 = w.z; v3 = w.w;
+      }
+      emit4<DT, NT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
+    }
   }
 }
 
@@ -781,7 +857,7 @@ __global__ __launch_bounds__(256) void diag_ham_small_kernel(IndexGeom g, Packed
 
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
-                                hipStream_t s) {
+                                hipStream_t s, int store) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
@@ -789,14 +865,17 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   const size_t lds = (size_t)words * 4;
   const dim3 grid((unsigned)(rows * g.nchunks));
-  // non-temporal 16-byte stores: K is written once and never re-read by this launch
+  // store policy: 0 auto (plain for a single-chunk int32 K, else non-temporal), 1 NT, 2 plain
+  const bool nt = store == 1 || (store == 0 && !(o.dtype == KMG_I32 && g.nchunks == 1));
+#define KMG_SP(PK, NTV)                                                                       \
+  KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<PK, D, NTV>), grid, dim3(1024), \
+                                              lds, s, g, pk, off, ent, row0, o))
   if (pack) {
-    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<true, D, true>), grid, dim3(256),
-                                                lds, s, g, pk, off, ent, row0, o));
+    if (nt) { KMG_SP(true, true); } else { KMG_SP(true, false); }
   } else {
-    KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<false, D, true>), grid, dim3(256),
-                                                lds, s, g, pk, off, ent, row0, o));
+    if (nt) { KMG_SP(false, true); } else { KMG_SP(false, false); }
   }
+#undef KMG_SP
   return hipGetLastError();
 }
 
