@@ -238,7 +238,10 @@ int check_params(const kmg_params *p, int64_t n, int64_t ldc, int32_t dt) {
 }
 
 // ----------------------------------------------------------------- posting index
-int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
+// codes != nullptr: the records in pk are packed by the index build itself (fused into the
+// v2 local pass; a separate pack launch before the v1 passes)
+int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk, const uint8_t *codes = nullptr,
+                const int32_t *lens = nullptr, int64_t ldc = 0) {
   // coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins: ~384 for the
   // spectrum index, ~1024 for the k-copy mismatch index (16.7M occurrences at N=20000,
   // where 288 buckets left the fine pass at 240 us and 576 halved it)
@@ -260,8 +263,13 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
   const int64_t nblk = (g.n + g.seqs_per_block - 1) / g.seqs_per_block;
   const int64_t cap = (int64_t)g.seqs_per_block * g.pmax * g.copies;
-  if (c->tune.idx_v2 && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
-      nblk * cap < ((int64_t)1 << 34)) {
+  const bool v2 = c->tune.idx_v2 && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
+                  nblk * cap < ((int64_t)1 << 34);
+  if (codes && !v2) {
+    StageTimer t(c, ST_PACK);
+    KMG_HIP(launch_pack(codes, lens, g.n, ldc, g.window, const_cast<uint32_t *>(pk.w), c->stream));
+  }
+  if (v2) {
     KMG_TRY(c->hcnt.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
     KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
     KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(nblk * cap)));
@@ -269,7 +277,7 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk) {
     KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 512)));  // + pad: whole-piece reads
     {
       StageTimer t(c, ST_PLACE);
-      KMG_HIP(launch_index_local(g, pk, (int)nblk, (uint32_t)cap,
+      KMG_HIP(launch_index_local(g, pk, codes, lens, ldc, (int)nblk, (uint32_t)cap,
                                  c->hcnt.as<uint32_t>(), c->hstart.as<uint32_t>(),
                                  c->tmp.as<uint32_t>(), c->stream));
     }
@@ -592,11 +600,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const int cw = packed_cw(ldc), mw = packed_mw(ldc);
       KMG_TRY(c->packed.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(1, n) * (cw + mw)));
       const Packed pkd{c->packed.as<uint32_t>(), (int64_t)(cw + mw), cw};
-      {
-        StageTimer t(c, ST_PACK);
-        KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, g.window, c->packed.as<uint32_t>(), c->stream));
-      }
       if (!use_index) {
+        {
+          StageTimer t(c, ST_PACK);
+          KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, g.window, c->packed.as<uint32_t>(), c->stream));
+        }
         // all-pairs Hamming formulation (any m, k <= 16)
         if (g.pmax > 256) return fail(KMG_EUNSUPPORTED, "Hamming path needs <= 256 k-mers");
         g.copies = 1;
@@ -632,7 +640,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
         choose_chunks(g, pair_chunk(n, g.pmax, k, c->tune.mm_chunk));
-        KMG_TRY(build_index(c, g, pkd));
+        KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         PairGeom pg{};
         pg.k = k;
         pg.nchunks = g.nchunks;
@@ -688,7 +696,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         const int64_t lim = c->tune.mm_chunk > 0 ? c->tune.mm_chunk : 20480;
         choose_chunks(g, (int)std::max<int64_t>(8, std::min<int64_t>({lim, cap, 64000})));
       }
-      KMG_TRY(build_index(c, g, pkd));
+      KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
       if (use_slots) {
         KMG_TRY(c->slots.ensure((size_t)(g.nbins() >> 2) * KMG_SLOT_BYTES));
         StageTimer t(c, ST_SLOTS);

@@ -103,6 +103,50 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
   }
 }
 
+// Stream one int32 LDS accumulator row [0, cw) to K row il (columns col0 ..): 16 bytes per
+// lane and step, so every store instruction of a wave covers 1 KB of the row contiguously
+// (int32 / float32: 4 columns a lane, float64: 2).  Two 16-byte stores 32 bytes apart per
+// lane (emit4's float64 form) leave half-written lines behind every store instruction,
+// which cost the spectrum kernel 2.2x as non-temporal stores (profiles/r02t_sp_store.jsonl).
+template <bool NT>
+__device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i, int64_t col0,
+                                         int cw, const int32_t *acc, bool norm) {
+  if (o.dtype == KMG_F64) {
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    double *prow = (double *)o.out + il * o.ld + col0;
+    const bool al = (((uintptr_t)prow) & 15) == 0;
+    const double di = norm ? o.dsq[i] : 1.0;
+    for (int q = threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
+      const int2 w = *(const int2 *)&acc[q];
+      const int64_t c0 = col0 + q;
+      const bool two = q + 1 < cw;
+      double r0 = (double)w.x, r1 = two ? (double)w.y : 0.0;
+      if (norm) {  // normalize_K: K[i,j] / (sqrt(K[i,i]) * sqrt(K[j,j])), diagonal := 1
+        r0 = (i == c0) ? 1.0 : (double)w.x / (di * o.dsq[c0]);
+        r1 = !two ? 0.0 : (i == c0 + 1) ? 1.0 : (double)w.y / (di * o.dsq[c0 + 1]);
+      }
+      if (al && two) {
+        const v2d x = {r0, r1};
+        if constexpr (NT)
+          __builtin_nontemporal_store(x, (v2d *)(prow + q));
+        else
+          *(v2d *)(prow + q) = x;
+      } else {
+        prow[q] = r0;
+        if (two) prow[q + 1] = r1;
+      }
+    }
+  } else {
+    for (int q = threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
+      const int4 w = *(const int4 *)&acc[q];
+      if (o.dtype == KMG_F32)
+        emit4<KMG_F32, NT>(o, il, i, col0 + q, min(4, cw - q), w.x, w.y, w.z, w.w, norm);
+      else
+        emit4<KMG_I32, NT>(o, il, i, col0 + q, min(4, cw - q), w.x, w.y, w.z, w.w, norm);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ spectrum
 // One workgroup of 1024 threads owns (row i, column chunk c); PACK16: two 16-bit counters
 // per LDS word (valid when every K_ij <= 65535, i.e. P_i * P_j <= 65535; the host checks
@@ -416,15 +460,7 @@ __global__ __launch_bounds__(1024) void gram_mm1_kernel(IndexGeom g, Packed pk,
   __syncthreads();
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
-  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
-    const int4 w = *(const int4 *)&acc[qq];
-    if (o.dtype == KMG_F64)
-      emit4<KMG_F64, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-    else if (o.dtype == KMG_F32)
-      emit4<KMG_F32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-    else
-      emit4<KMG_I32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-  }
+  emit_row<true>(o, il, i, col0, cw, (const int32_t *)acc, norm);
 }
 
 // ------------------------------------------------------------------ mismatch m=1, pair table
@@ -706,15 +742,7 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   __syncthreads();
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
-  for (int qq = threadIdx.x * 4; qq < cw; qq += blockDim.x * 4) {
-    const int4 w = *(const int4 *)&acc[qq];
-    if (o.dtype == KMG_F64)
-      emit4<KMG_F64, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-    else if (o.dtype == KMG_F32)
-      emit4<KMG_F32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-    else
-      emit4<KMG_I32, true>(o, il, i, col0 + qq, min(4, cw - qq), w.x, w.y, w.z, w.w, norm);
-  }
+  emit_row<true>(o, il, i, col0, cw, (const int32_t *)acc, norm);
 }
 
 // ------------------------------------------------------------------ Hamming forms

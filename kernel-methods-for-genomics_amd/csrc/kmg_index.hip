@@ -35,6 +35,50 @@ __device__ __forceinline__ uint32_t drop_letter(uint32_t code, int p, int k) {
 constexpr int IDX_THREADS = 1024;  // upper bound; blocks launch g.part_threads
 constexpr int FINE_THREADS = 1024;
 
+// symbols [32 b, 32 b + 32) of sequence j -> code words 2b, 2b+1 and mask word b
+__device__ __forceinline__ void pack_piece(const uint8_t *__restrict__ codes,
+                                           const int32_t *__restrict__ lens, int64_t ldc,
+                                           int64_t j, int b, uint32_t &c0, uint32_t &c1,
+                                           uint32_t &m) {
+  const int len = min(max(lens[j], 0), (int)ldc);
+  const uint8_t *r = codes + j * ldc;
+  c0 = 0, c1 = 0, m = 0;
+#pragma unroll 8
+  for (int q = 0; q < 32; ++q) {
+    const int pos = 32 * b + q;
+    const uint32_t v = pos < len ? (uint32_t)r[pos] : 4u;
+    m |= (v > 3u ? 1u : 0u) << q;
+    const uint32_t sym = v & 3u;
+    if (q < 16)
+      c0 |= sym << (30 - 2 * q);
+    else
+      c1 |= sym << (30 - 2 * (q - 16));
+  }
+}
+
+// fused 2-bit packing (part_local_kernel with codes != nullptr): pack the block's
+// sequences straight into LDS and publish their records for the Gram kernels
+__device__ __forceinline__ int stage_rows_packing(const IndexGeom &g, const Packed &pk,
+                                                  const uint8_t *__restrict__ codes,
+                                                  const int32_t *__restrict__ lens, int64_t ldc,
+                                                  uint32_t *srec, int64_t j0) {
+  const int ns = (int)min((int64_t)g.seqs_per_block, g.n - j0);
+  const int cw = pk.cw, mw = (int)pk.ldp - pk.cw;
+  const int nb = max((cw + 1) / 2, mw);
+  for (int t = threadIdx.x; t < ns * nb; t += blockDim.x) {
+    const int s = t / nb, b = t - s * nb;
+    uint32_t c0, c1, m;
+    pack_piece(codes, lens, ldc, j0 + s, b, c0, c1, m);
+    uint32_t *lrec = srec + s * pk.ldp;
+    uint32_t *grec = const_cast<uint32_t *>(pk.w) + (j0 + s) * pk.ldp;  // the context's record buffer
+    if (2 * b < cw) lrec[2 * b] = grec[2 * b] = c0;
+    if (2 * b + 1 < cw) lrec[2 * b + 1] = grec[2 * b + 1] = c1;
+    if (b < mw) lrec[cw + b] = grec[cw + b] = m;
+  }
+  __syncthreads();
+  return ns;
+}
+
 // stage the packed records (Packed, kmg_internal.h) of seqs_per_block sequences in LDS;
 // returns the number of staged sequences
 __device__ __forceinline__ int stage_rows(const IndexGeom &g, const Packed &pk, uint32_t *srec,
@@ -211,7 +255,8 @@ __global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, 
 //      sum_q hcnt[b][q]; LDS fine histogram + scan -> off[], then the items are gathered
 //      from every block's segment into ent[].  Results do not depend on dispatch order.
 __global__ __launch_bounds__(IDX_THREADS) void part_local_kernel(
-    IndexGeom g, Packed pk, int nblk, uint32_t cap, uint32_t *__restrict__ hcnt,
+    IndexGeom g, Packed pk, const uint8_t *__restrict__ codes, const int32_t *__restrict__ lens,
+    int64_t ldc, int nblk, uint32_t cap, uint32_t *__restrict__ hcnt,
     uint32_t *__restrict__ hstart, uint32_t *__restrict__ tmp) {
   extern __shared__ __align__(16) uint32_t sm[];
   __shared__ uint32_t wtmp[IDX_THREADS / 64];
@@ -221,7 +266,8 @@ __global__ __launch_bounds__(IDX_THREADS) void part_local_kernel(
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) h[b] = 0;
   const int q = blockIdx.x;
   const int64_t j0 = (int64_t)q * g.seqs_per_block;
-  const int ns = stage_rows(g, pk, srec, j0);
+  const int ns = codes ? stage_rows_packing(g, pk, codes, lens, ldc, srec, j0)
+                       : stage_rows(g, pk, srec, j0);
   const int fb = g.fine_bits;
   const uint32_t fmask = (1u << fb) - 1u;
   for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&h[bin >> fb], 1u); });
@@ -510,20 +556,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ c
   if (t >= n * nb) return;
   const int64_t j = t / nb;
   const int b = (int)(t - j * nb);
-  const int len = min(max(lens[j], 0), (int)ldc);
-  const uint8_t *r = codes + j * ldc;
-  uint32_t c0 = 0, c1 = 0, m = 0;
-#pragma unroll 8
-  for (int q = 0; q < 32; ++q) {
-    const int pos = 32 * b + q;
-    const uint32_t v = pos < len ? (uint32_t)r[pos] : 4u;
-    m |= (v > 3u ? 1u : 0u) << q;
-    const uint32_t sym = v & 3u;
-    if (q < 16)
-      c0 |= sym << (30 - 2 * q);
-    else
-      c1 |= sym << (30 - 2 * (q - 16));
-  }
+  uint32_t c0, c1, m;
+  pack_piece(codes, lens, ldc, j, b, c0, c1, m);
   uint32_t *rec = out + j * (int64_t)(cw + mw);
   if (2 * b < cw) rec[2 * b] = c0;
   if (2 * b + 1 < cw) rec[2 * b + 1] = c1;
@@ -679,11 +713,12 @@ size_t index_gather_lds(const IndexGeom &g, int64_t nblk) {
   return sizeof(uint32_t) * (((size_t)1 << g.fine_bits) + 2 * (size_t)nblk);
 }
 
-hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, int nblk, uint32_t cap,
+hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, const uint8_t *codes,
+                              const int32_t *lens, int64_t ldc, int nblk, uint32_t cap,
                               uint32_t *hcnt, uint32_t *hstart, uint32_t *tmp, hipStream_t s) {
   if (g.n == 0 || nblk == 0) return hipSuccess;
   hipLaunchKernelGGL(part_local_kernel, dim3((unsigned)nblk), dim3(g.part_threads),
-                     part_lds(g, pk, 1), s, g, pk, nblk, cap, hcnt, hstart, tmp);
+                     part_lds(g, pk, 1), s, g, pk, codes, lens, ldc, nblk, cap, hcnt, hstart, tmp);
   return hipGetLastError();
 }
 

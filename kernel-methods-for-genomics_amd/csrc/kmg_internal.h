@@ -90,9 +90,11 @@ hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uin
                              hipStream_t s);
 hipError_t launch_extract(const IndexGeom &g, const Packed &pk, uint32_t *kmers, hipStream_t s);
 // index build v2 (no device-scope atomics): per-block local sort, then per-bucket gather.
-// hcnt/hstart: nbuckets x nblk (bucket-major); tmp: nblk x cap items.
+// hcnt/hstart: nbuckets x nblk (bucket-major); tmp: nblk x cap items.  codes != nullptr:
+// the local pass also packs the sequences into pk (launch_pack fused into the first pass).
 size_t index_gather_lds(const IndexGeom &g, int64_t nblk);
-hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, int nblk, uint32_t cap,
+hipError_t launch_index_local(const IndexGeom &g, const Packed &pk, const uint8_t *codes,
+                              const int32_t *lens, int64_t ldc, int nblk, uint32_t cap,
                               uint32_t *hcnt, uint32_t *hstart, uint32_t *tmp, hipStream_t s);
 hipError_t launch_index_gather(const IndexGeom &g, int nblk, uint32_t cap, const uint32_t *hcnt,
                                const uint32_t *hstart, const uint32_t *tmp, uint32_t *off,
