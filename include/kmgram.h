@@ -215,8 +215,9 @@ int kmg_synchronize(kmg_ctx *ctx);
 int kmg_stream(kmg_ctx *ctx, void **hip_stream);
 
 /* Per-stage device timings from HIP events recorded on the context stream around
- * every launch while timing is enabled (kmg_set_timing(ctx,1)); nothing is
- * synchronised until a stage time is read.  Stage names: "count", "scan",
+ * every launch while timing is enabled (kmg_set_timing(ctx,1); kmg_set_timing(ctx,2)
+ * times only the "gram", "gather" and "memset" stages, 2 events per Gram launch instead
+ * of 2 per stage); nothing is synchronised until a stage time is read.  Stage names: "count", "scan",
  * "place", "fine", "diag", "gram", "extract", "features", "pack" (2-bit packing of the
  * input), "slots" (mismatch slot table), "combine", "solve", "memset", "gather" (the RCCL
  * all-gathers of kmg_gram_blocks, timed on their own stream).

@@ -155,7 +155,7 @@ struct kmg_ctx {
   rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
-  bool timing = false;
+  int timing = 0;  // 0 off, 1 every stage, 2 the Gram and gather stages only
   // per-stage event pairs of every timed call since the last reset (read after a sync)
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_log;
@@ -185,7 +185,7 @@ struct StageTimer {
   kmg_ctx *c;
   hipEvent_t end = nullptr;
   StageTimer(kmg_ctx *c_, int i) : c(c_) {
-    if (c->timing) {
+    if (c->timing == 1 || (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET))) {
       hipEvent_t b = pool_event(c);
       end = pool_event(c);
       (void)hipEventRecord(b, c->stream);
@@ -1090,7 +1090,7 @@ int kmg_stream(kmg_ctx *c, void **s) {
 int kmg_set_timing(kmg_ctx *c, int32_t enable) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
-  c->timing = enable != 0;
+  c->timing = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
   return KMG_OK;
 }
 

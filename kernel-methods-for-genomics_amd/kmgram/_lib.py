@@ -323,7 +323,8 @@ class Context:
         check(self.lib.kmg_synchronize(self._h))
 
     def set_timing(self, on=True):
-        check(self.lib.kmg_set_timing(self._h, 1 if on else 0))
+        """on: True / 1 every stage, 2 the Gram / gather / memset stages only, False off."""
+        check(self.lib.kmg_set_timing(self._h, 2 if on == 2 else (1 if on else 0)))
 
     def timing_reset(self):
         check(self.lib.kmg_timing_reset(self._h))
