@@ -322,10 +322,28 @@ __global__ __launch_bounds__(FINE_THREADS) void part_gather_kernel(
     total += red[0][w];
     base += red[1][w];
   }
-  for (int q = wave; q < nblk; q += nw) {
-    const uint32_t c = cnt[q];
-    const uint32_t *sp = tmp + (size_t)q * cap + src[q];
-    for (uint32_t x = lane; x < c; x += 64) atomicAdd(&fh[sp[x] >> 16], 1u);
+  // the segments of a bucket are short (~30 items at N=20000): a wave loads the first 64
+  // items of SEGU segments before using any, so the pass is not one L2 round trip per
+  // segment; longer segments finish in the remainder loop
+  constexpr int SEGU = 4;
+  for (int q0 = wave; q0 < nblk; q0 += SEGU * nw) {
+    uint32_t it[SEGU];
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u) {
+      const int q = q0 + u * nw;
+      it[u] = (q < nblk && (uint32_t)lane < cnt[q]) ? tmp[(size_t)q * cap + src[q] + lane] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u)
+      if (it[u] != 0xFFFFFFFFu) atomicAdd(&fh[it[u] >> 16], 1u);
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u) {
+      const int q = q0 + u * nw;
+      if (q >= nblk) break;
+      const uint32_t c = cnt[q];
+      const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+      for (uint32_t x = 64 + lane; x < c; x += 64) atomicAdd(&fh[sp[x] >> 16], 1u);
+    }
   }
   __syncthreads();
   lds_excl_scan(fh, nf, wtmp);
@@ -337,13 +355,31 @@ __global__ __launch_bounds__(FINE_THREADS) void part_gather_kernel(
   }
   if (b == (int)gridDim.x - 1 && threadIdx.x == 0) off[nb] = base + total;
   __syncthreads();
-  for (int q = wave; q < nblk; q += nw) {
-    const uint32_t c = cnt[q];
-    const uint32_t *sp = tmp + (size_t)q * cap + src[q];
-    for (uint32_t x = lane; x < c; x += 64) {
-      const uint32_t it = sp[x];
-      const uint32_t pos = atomicAdd(&fh[it >> 16], 1u);
-      ent[base + pos] = (uint16_t)(it & 0xFFFFu);
+  for (int q0 = wave; q0 < nblk; q0 += SEGU * nw) {
+    uint32_t it[SEGU];
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u) {
+      const int q = q0 + u * nw;
+      it[u] = (q < nblk && (uint32_t)lane < cnt[q]) ? tmp[(size_t)q * cap + src[q] + lane] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u) {
+      if (it[u] != 0xFFFFFFFFu) {
+        const uint32_t pos = atomicAdd(&fh[it[u] >> 16], 1u);
+        ent[base + pos] = (uint16_t)(it[u] & 0xFFFFu);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SEGU; ++u) {
+      const int q = q0 + u * nw;
+      if (q >= nblk) break;
+      const uint32_t c = cnt[q];
+      const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+      for (uint32_t x = 64 + lane; x < c; x += 64) {
+        const uint32_t v = sp[x];
+        const uint32_t pos = atomicAdd(&fh[v >> 16], 1u);
+        ent[base + pos] = (uint16_t)(v & 0xFFFFu);
+      }
     }
   }
 }
