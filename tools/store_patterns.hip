@@ -54,6 +54,16 @@ __global__ __launch_bounds__(1024) void rows_delay_kernel(char *out, int64_t n) 
     st16<NT>(row + b, (v4i){(int)i, (int)b, 1, 2});
 }
 
+// rows1024 through buffer stores with cache-policy bits AUX (1 sc0, 2 nt, 16 sc1)
+template <int ESZ, int AUX>
+__global__ __launch_bounds__(1024) void rows_buf_kernel(char *out, int64_t n) {
+  const int64_t i = blockIdx.x;
+  const int64_t bytes = n * ESZ;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out + i * bytes, 0, (int)bytes, 0x00020000);
+  for (int b = threadIdx.x * 16; b < bytes; b += 1024 * 16)
+    __builtin_amdgcn_raw_buffer_store_b128((v4i){(int)i, b, 1, 2}, rsrc, b, 0, AUX);
+}
+
 // persistent: G blocks, block b writes rows b, b + G, ... (G rows in flight)
 template <int ESZ, bool NT>
 __global__ __launch_bounds__(1024) void rows_persist_kernel(char *out, int64_t n) {
@@ -127,6 +137,13 @@ void run_all(char *d, int64_t n) {
   };
   rep("memset", time_it([&] { CK(hipMemsetAsync(d, 0, (size_t)bytes, 0)); }, 10));
   rep("rows1024", time_it([&] { rows_kernel<ESZ, NT><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB0", time_it([&] { rows_buf_kernel<ESZ, 0><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB1sc0", time_it([&] { rows_buf_kernel<ESZ, 1><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB2nt", time_it([&] { rows_buf_kernel<ESZ, 2><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB16sc1", time_it([&] { rows_buf_kernel<ESZ, 16><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB17sc0sc1", time_it([&] { rows_buf_kernel<ESZ, 17><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB18sc1nt", time_it([&] { rows_buf_kernel<ESZ, 18><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("rowsB3sc0nt", time_it([&] { rows_buf_kernel<ESZ, 3><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsD1", time_it([&] { rows_delay_kernel<ESZ, NT, 1><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsD2", time_it([&] { rows_delay_kernel<ESZ, NT, 2><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsD4", time_it([&] { rows_delay_kernel<ESZ, NT, 4><<<(unsigned)n, 1024>>>(d, n); }, 10));
