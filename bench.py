@@ -37,9 +37,10 @@ import numpy as np  # noqa: E402
 from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
-from kmgram.shard import block_cyclic_ranges, default_block, rows_padded  # noqa: E402
+from kmgram.shard import block_cyclic_ranges, default_block, rows_padded, triangle_rounds  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+GATHER_MODE = 2  # G > 1: upper-triangle round slabs + local mirror (--gather-mode 1: full rows)
 XGMI_IN_PEAK = 7 * 76.5e9  # per-GPU ingress: 7 xGMI links x ~76.5 GB/s per direction
 GATHER_CEILING = 56.38e9  # random 128-B lines/s from a 78.6 MB table (profiles/r02_mall_gather.jsonl)
 INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROARCH.md)
@@ -112,8 +113,9 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
     ctx.h2d(d_codes, codes)
     ctx.h2d(d_lens, lens)
     d_out = ctx.dmalloc(npad * n * esz)
-    gather = world > 1
+    gather = GATHER_MODE if world > 1 else 0
     res = {"name": name, "N": n, "block_rows": block, "rounds": npad // (world * block),
+           "gather_mode": gather,
            "rows_this_rank": sum(b - a for a, b in block_cyclic_ranges(n, world, rank, block))}
     try:
         def step(g):
@@ -151,10 +153,14 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
         t, stages = timed(gather, steps)
         res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages})
         if gather:
-            tcf, scf = timed(False, steps)
+            tcf, scf = timed(0, steps)
             res["collective_free"] = {"ms_per_step": tcf * 1e3, "pairs_per_s": n * n / tcf,
                                       "stages_ms": scf}
-            step(True)  # leave the gathered K for the spot check
+            alt = 1 if gather == 2 else 2  # the other assembly, for comparison
+            ta, sa = timed(alt, steps)
+            res["other_gather_mode"] = {"gather_mode": alt, "ms_per_step": ta * 1e3,
+                                        "pairs_per_s": n * n / ta, "stages_ms": sa}
+            step(gather)  # leave the gathered K for the spot check
             ctx.synchronize()
         # spot check: the first row of this rank's first block, plus (G > 1) a row computed
         # by the next rank and received through the all-gather
@@ -523,7 +529,11 @@ def gather_roofline(res, world, esz):
         return None
     n = res["N"]
     npad = rows_padded(n, world, res["block_rows"])
-    recv = (world - 1) / world * npad * n * esz
+    if res.get("gather_mode") == 2:  # upper-triangle round slabs
+        r = world * res["block_rows"]
+        recv = (world - 1) / world * sum(r * w for _, w in triangle_rounds(n, world, res["block_rows"])) * esz
+    else:
+        recv = (world - 1) / world * npad * n * esz
     launches_per_step = res["rounds"]
     t = st["gather"] * launches_per_step / 1e3  # gather seconds per step
     return {"bound": "xgmi", "bytes_received_per_step": recv, "gather_ms_per_step": t * 1e3,
@@ -537,12 +547,16 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--gather-mode", type=int, default=2, choices=(1, 2),
+                    help="G > 1 assembly: 2 upper-triangle slabs + mirror, 1 full rows")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mismatch", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the config 4 / 5, host-path, run.py and downstream lines")
     args = ap.parse_args()
+    global GATHER_MODE
+    GATHER_MODE = args.gather_mode
     # stdout carries exactly one JSON line: everything else written to fd 1 (gloo's
     # connection banner, runtime chatter) is sent to stderr
     sys.stdout.flush()

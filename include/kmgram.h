@@ -193,8 +193,13 @@ int kmg_svm_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
  * when the call's work completes (context-stream order) every rank holds the full K.
  * d_out: n_pad x ld_out elements, n_pad = kmg_rows_padded(n, nranks, block) (the padding
  * rows of the last round travel but are never written by a kernel); gather = 0 writes only
- * this rank's blocks and needs n rows.  gather = 1 with nranks > 1 needs kmg_comm_init with
- * the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
+ * this rank's blocks and needs n rows.  gather = 2 (upper triangle): round t
+ * computes only the columns >= t*R of its rows into a contiguous round slab, the slab is
+ * all-gathered in place (half the xGMI bytes of gather = 1) and every rank copies it into
+ * K and mirrors it into the lower triangle locally (K[x][t*R + y] = K[t*R + y][x]).
+ * gather = 3: the gather = 2 layout with every rank's blocks computed on this GPU (a
+ * one-GPU rehearsal of the multi-rank assembly; no RCCL).  gather = 1 or 2 with nranks > 1
+ * needs kmg_comm_init with the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
  * get_mismatch_K (kernels.py:41-45, 211-215) split over GPUs.
  */
 int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block);

@@ -148,6 +148,8 @@ struct kmg_ctx {
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
+  DevBuf tri_stage, tri_scratch;  // upper-triangle multi-GPU build: round slabs, full rows
+  int64_t cur_n = 0;              // columns of the current Gram call
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
@@ -167,6 +169,7 @@ struct kmg_ctx {
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr;  // RCCL all-gathers of kmg_gram_blocks
   hipEvent_t ev_sync = nullptr;       // context stream <-> comm stream ordering
+  hipEvent_t ev_tri[2] = {nullptr, nullptr};  // upper-triangle slabs released by their mirror
   int nranks = 1, rank = 0;
 };
 
@@ -435,21 +438,47 @@ int pair_chunk(int64_t n, int pmax, int k, int cap) {
 // `out` (row row0); the index / features / diagonal are built once per call.  `after(q)`
 // runs once range q's Gram launch is enqueued (the multi-GPU path hangs its all-gather of a
 // round there).
+// ld > 0 / col_lo > 0: this range's own leading dimension and first written column
+// (upper-triangle round slabs of kmg_gram_blocks; `out` then points at column 0 of row
+// row0 of a row whose columns < col_lo are never written).
 struct RowRange {
   int64_t row0, row1;
   void *out;
+  int64_t ld = 0, col_lo = 0;
 };
 using AfterRange = std::function<int(size_t)>;
 
+// native: the launch's kernels honour OutSpec::col_lo (spectrum, mismatch slots / pairs)
+// when it is a multiple of 8; otherwise a range with col_lo > 0 is computed as full rows
+// into a scratch slab and its columns >= col_lo copied out.
 template <typename Launch>
 int each_range(kmg_ctx *c, const std::vector<RowRange> &ranges, const OutSpec &o,
-               const AfterRange &after, Launch &&launch) {
+               const AfterRange &after, Launch &&launch, bool native = false) {
+  const size_t esz = dtype_size(o.dtype);
   for (size_t q = 0; q < ranges.size(); ++q) {
+    const RowRange &rg = ranges[q];
     OutSpec oq = o;
-    oq.out = ranges[q].out;
-    {
+    oq.out = rg.out;
+    if (rg.ld > 0) oq.ld = rg.ld;
+    oq.col_lo = rg.col_lo;
+    if (oq.col_lo > 0 && (!native || (oq.col_lo & 7)) && rg.row1 > rg.row0) {
+      const int64_t n = c->cur_n, rows = rg.row1 - rg.row0;
+      KMG_TRY(c->tri_scratch.ensure(esz * (size_t)rows * n));
+      OutSpec of = o;
+      of.out = c->tri_scratch.p;
+      of.ld = n;
+      of.col_lo = 0;
+      {
+        StageTimer t(c, ST_GRAM);
+        KMG_HIP(launch(rg.row0, rg.row1, of));
+      }
+      KMG_HIP(hipMemcpy2DAsync((char *)rg.out + (size_t)oq.col_lo * esz, (size_t)oq.ld * esz,
+                               (const char *)c->tri_scratch.p + (size_t)oq.col_lo * esz,
+                               (size_t)n * esz, (size_t)(n - oq.col_lo) * esz, (size_t)rows,
+                               hipMemcpyDeviceToDevice, c->stream));
+    } else {
       StageTimer t(c, ST_GRAM);
-      KMG_HIP(launch(ranges[q].row0, ranges[q].row1, oq));
+      KMG_HIP(launch(rg.row0, rg.row1, oq));
     }
     if (after) KMG_TRY(after(q));
   }
@@ -532,15 +561,20 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                 int maxlen, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
                 int32_t dt, int64_t ld, const AfterRange &after = nullptr) {
   c->last_call_first = (int)c->ev_log.size();
+  c->cur_n = n;
   for (const RowRange &r : ranges)
     if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
   if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
   OutSpec o{nullptr, ld, dt, 0, nullptr, nullptr};
   if (c->tune.poison && n > 0)  // testing: no stale output can pass
     for (const RowRange &r : ranges)
-      if (r.row1 > r.row0)
-        KMG_HIP(hipMemset2DAsync(r.out, (size_t)ld * dtype_size(dt), 0xA5,
-                                 (size_t)n * dtype_size(dt), (size_t)(r.row1 - r.row0), c->stream));
+      if (r.row1 > r.row0) {
+        const int64_t rld = r.ld > 0 ? r.ld : ld;
+        KMG_HIP(hipMemset2DAsync((char *)r.out + (size_t)r.col_lo * dtype_size(dt),
+                                 (size_t)rld * dtype_size(dt), 0xA5,
+                                 (size_t)(n - r.col_lo) * dtype_size(dt),
+                                 (size_t)(r.row1 - r.row0), c->stream));
+      }
   switch (p->kind) {
     case KMG_SPECTRUM:
     case KMG_MISMATCH: {
@@ -681,7 +715,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                              c->pr_lines.as<uint4>(), nlines,
                                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), r0,
                                              r1, (int)w[0], (int)w[1], (int)w[2], oq, c->stream);
-        });
+        }, true);
       }
       if (exact) {
         g.copies = 1;
@@ -717,7 +751,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                                    c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                                    r0, r1, (int)w[0], (int)w[1], (int)w[2], oq,
                                                    c->stream);
-      });
+      }, true);
     }
     case KMG_WD:
     case KMG_WDS: {
@@ -871,11 +905,14 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
                     &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
-                    &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info};
+                    &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
+                    &c->tri_stage, &c->tri_scratch};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
+  for (hipEvent_t e : c->ev_tri)
+    if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return KMG_OK;
@@ -949,53 +986,106 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   KMG_TRY(check_params(p, n, ldc, out_dtype));
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
   if (block < 1) return fail(KMG_EINVAL, "block < 1");
+  if (gather < 0 || gather > 3) return fail(KMG_EINVAL, "gather must be 0..3");
   if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
-  if (gather && nranks > 1 && (!c->comm || c->nranks != nranks || c->rank != rank))
+  const bool tri = gather >= 2;               // upper-triangle round slabs + local mirror
+  const bool rccl = (gather == 1 || gather == 2) && nranks > 1;
+  if (rccl && (!c->comm || c->nranks != nranks || c->rank != rank))
     return fail(KMG_EINVAL, "gather needs a communicator of %d ranks with this rank %d", nranks, rank);
   KMG_HIP(hipSetDevice(c->device));
   const size_t esz = dtype_size(out_dtype);
   const int64_t round = (int64_t)nranks * block;
   const int64_t nround = (n + round - 1) / round;
-  // this rank's block of every round: rows [t*round + rank*block, +block) clipped to n
+  if (rccl && !c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+  if ((rccl || tri) && !c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+  hipStream_t post = rccl ? c->comm_stream : c->stream;  // gather + mirror stream
+  auto gather_bytes = [&](char *recv, size_t count) -> int {  // in place, rank r at r * count
+    hipEvent_t b = nullptr, e = nullptr;
+    if (c->timing) {
+      b = pool_event(c);
+      e = pool_event(c);
+      KMG_HIP(hipEventRecord(b, c->comm_stream));
+    }
+    ncclResult_t r = ncclAllGather(recv + (size_t)rank * count, recv, count, ncclChar, c->comm,
+                                   c->comm_stream);
+    if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+    if (c->timing) {
+      KMG_HIP(hipEventRecord(e, c->comm_stream));
+      c->ev_log.push_back({ST_GATHER, {b, e}});
+    }
+    return KMG_OK;
+  };
   std::vector<RowRange> ranges;
-  for (int64_t t = 0; t < nround; ++t) {
-    const int64_t r0 = std::min(n, t * round + (int64_t)rank * block);
-    const int64_t r1 = std::min(n, r0 + block);
-    ranges.push_back(RowRange{r0, r1, (char *)d_out + (size_t)r0 * ld_out * esz});
-  }
+  std::vector<int64_t> last_of_round;  // range index -> round it completes (-1: none)
   AfterRange after = nullptr;
-  const bool do_gather = gather && nranks > 1;
-  if (do_gather) {
-    if (!c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-    if (!c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
-    after = [&](size_t t) -> int {
-      // round t's rows [t*round, (t+1)*round) are contiguous in d_out: rank q's block sits
-      // at q * block rows, i.e. send = recv + rank * count, so the all-gather is in place.
-      // It runs on its own stream behind an event of this rank's Gram launch, overlapped
-      // with the next round's Gram kernels.
-      // one event suffices: hipStreamWaitEvent captures the record made just before it
-      KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
-      KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
-      hipEvent_t b = nullptr, e = nullptr;
-      if (c->timing) {
-        b = pool_event(c);
-        e = pool_event(c);
-        KMG_HIP(hipEventRecord(b, c->comm_stream));
+  if (!tri) {
+    // this rank's block of every round: rows [t*round + rank*block, +block) clipped to n
+    for (int64_t t = 0; t < nround; ++t) {
+      const int64_t r0 = std::min(n, t * round + (int64_t)rank * block);
+      const int64_t r1 = std::min(n, r0 + block);
+      ranges.push_back(RowRange{r0, r1, (char *)d_out + (size_t)r0 * ld_out * esz});
+    }
+    if (rccl) {
+      after = [&](size_t t) -> int {
+        // round t's rows [t*round, (t+1)*round) are contiguous in d_out: rank q's block sits
+        // at q * block rows, i.e. send = recv + rank * count, so the all-gather is in place.
+        // It runs on its own stream behind an event of this rank's Gram launch, overlapped
+        // with the next round's Gram kernels (one event suffices: hipStreamWaitEvent
+        // captures the record made just before it).
+        KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+        KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+        return gather_bytes((char *)d_out + (size_t)(t * round) * ld_out * esz,
+                            (size_t)block * ld_out * esz);
+      };
+    }
+  } else {
+    // Upper triangle: round t computes only columns >= c_t = t*round of its
+    // rows, into a contiguous round slab S_t [round][w_t], w_t = n - c_t (rank q's block at
+    // q * block rows), which is all-gathered in place (half the xGMI bytes of full rows),
+    // copied into K's rows [c_t, c_t + round) at columns >= c_t, and mirrored into the
+    // columns [c_t, c_t + round) of every later row (K[x][c_t + y] = S_t[y][x - c_t]).
+    // Two slabs alternate; round t waits for the mirror of round t - 2 before reusing its
+    // slab.  gather = 3 computes every rank's blocks locally (a one-GPU rehearsal of the
+    // same layout, no RCCL).
+    const size_t slab = (size_t)round * (size_t)std::max<int64_t>(n, 1) * esz;
+    KMG_TRY(c->tri_stage.ensure(2 * slab));
+    for (int64_t t = 0; t < nround; ++t) {
+      const int64_t c0 = t * round, w = n - c0;
+      char *S = (char *)c->tri_stage.p + (size_t)(t & 1) * slab;
+      for (int32_t q = 0; q < nranks; ++q) {
+        if (gather != 3 && q != rank) continue;
+        const int64_t r0 = std::min(n, c0 + (int64_t)q * block);
+        const int64_t r1 = std::min(n, r0 + block);
+        // `out` addresses column 0 of row r0: columns < c0 are never written
+        char *out = S + ((int64_t)q * block * w - c0) * (int64_t)esz;
+        ranges.push_back(RowRange{r0, r1, out, w, c0});
+        last_of_round.push_back(-1);
       }
-      char *recv = (char *)d_out + (size_t)(t * round) * ld_out * esz;
-      const size_t count = (size_t)block * ld_out * esz;
-      ncclResult_t r = ncclAllGather(recv + (size_t)rank * count, recv, count, ncclChar, c->comm,
-                                     c->comm_stream);
-      if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather: %s", ncclGetErrorString(r));
-      if (c->timing) {
-        KMG_HIP(hipEventRecord(e, c->comm_stream));
-        c->ev_log.push_back({ST_GATHER, {b, e}});
+      last_of_round.back() = t;
+    }
+    if (!c->ev_tri[0]) {
+      for (int b = 0; b < 2; ++b)
+        KMG_HIP(hipEventCreateWithFlags(&c->ev_tri[b], hipEventDisableTiming));
+    }
+    after = [&](size_t q) -> int {
+      const int64_t t = last_of_round[q];
+      if (t < 0) return KMG_OK;
+      const int64_t c0 = t * round, w = n - c0;
+      char *S = (char *)c->tri_stage.p + (size_t)(t & 1) * slab;
+      if (rccl) {
+        KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+        KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+        KMG_TRY(gather_bytes(S, (size_t)block * w * esz));
       }
+      KMG_HIP(launch_tri_unpack(S, w, round, c0, n, d_out, ld_out, (int)esz, post));
+      KMG_HIP(hipEventRecord(c->ev_tri[t & 1], post));
+      // the next Gram launch (round t + 1) writes the slab round t - 1 used
+      if (t >= 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_tri[(t - 1) & 1], 0));
       return KMG_OK;
     };
   }
   KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, ld_out, after));
-  if (do_gather) {  // stream order: later work on the context stream sees the full K
+  if (rccl) {  // stream order: later work on the context stream sees the full K
     KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
     KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
   }

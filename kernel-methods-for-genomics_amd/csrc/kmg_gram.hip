@@ -22,6 +22,8 @@
 // position p, in 4 sub-bins by its letter at p.
 #include "kmg_internal.h"
 
+#include <algorithm>
+
 namespace kmg {
 
 __device__ __forceinline__ uint32_t letter_at_g(uint32_t code, int p, int k) {
@@ -111,12 +113,14 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
 template <bool NT>
 __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i, int64_t col0,
                                          int cw, const int32_t *acc, bool norm) {
+  // columns below o.col_lo are not written; col_lo - col0 is a multiple of 8 (host check)
+  const int qs = (int)max((int64_t)0, o.col_lo - col0);
   if (o.dtype == KMG_F64) {
     typedef double v2d __attribute__((ext_vector_type(2)));
     double *prow = (double *)o.out + il * o.ld + col0;
     const bool al = (((uintptr_t)prow) & 15) == 0;
     const double di = norm ? o.dsq[i] : 1.0;
-    for (int q = threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
+    for (int q = qs + threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
       const int2 w = *(const int2 *)&acc[q];
       const int64_t c0 = col0 + q;
       const bool two = q + 1 < cw;
@@ -137,7 +141,7 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
       }
     }
   } else {
-    for (int q = threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
+    for (int q = qs + threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
       const int4 w = *(const int4 *)&acc[q];
       if (o.dtype == KMG_F32)
         emit4<KMG_F32, NT>(o, il, i, col0 + q, min(4, cw - q), w.x, w.y, w.z, w.w, norm);
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
   const int c = (int)(blockIdx.x - il * g.nchunks);
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int words = PACK16 ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   const uint32_t *__restrict__ srec = pk.w + i * pk.ldp;
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
   __syncthreads();
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
+  const int qs = (int)max((int64_t)0, o.col_lo - col0);  // a multiple of 8 (host check)
   if constexpr (DT == KMG_F64) {
     // two columns (16 B) per lane and step, so every store instruction of a wave covers
     // 1 KB of the row contiguously (whole lines: no partial-line writes)
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
     double *prow = (double *)o.out + il * o.ld + col0;
     const bool al = (((uintptr_t)prow) & 15) == 0;
     const double di = norm ? o.dsq[i] : 1.0;
-    for (int q = threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
+    for (int q = qs + threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
       uint32_t v0, v1;
       if (PACK16) {
         const uint32_t w = acc[q >> 1];
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
       }
     }
   } else {
-    for (int q = threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
+    for (int q = qs + threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
       uint32_t v0, v1, v2, v3;
       if (PACK16) {
         const uint2 w = *(const uint2 *)&acc[q >> 1];
@@ -332,6 +338,7 @@ __global__ __launch_bounds__(1024) void gram_mm1_kernel(IndexGeom g, Packed pk,
   const int64_t i = row0 + il;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int accw = ((g.chunk + 3) >> 2) << 2;
   const int P = g.pmax;
   int32_t *acc = (int32_t *)smem;
@@ -536,6 +543,7 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   const int64_t i = row0 + il;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int accw = ((g.chunk + 3) >> 2) << 2;
   const int P = g.pmax;
   int32_t *acc = (int32_t *)smem;  // [accw] + 64 dummy words (the pack kernel's padding)
@@ -882,6 +890,52 @@ __global__ __launch_bounds__(256) void diag_ham_small_kernel(IndexGeom g, Packed
     case KMG_F32: { constexpr int D = KMG_F32; __VA_ARGS__; } break; \
     default: { constexpr int D = KMG_F64; __VA_ARGS__; } break;      \
   }
+
+// ------------------------------------------------------------------ multi-GPU assembly
+// One pass over the round slab S (R rows x w columns; row y = K row c0 + y at columns >= c0):
+// a 64 x 64 tile of S is read once (coalesced rows), written to K's rows c0 + y at columns
+// c0 + j (upper part, coalesced) and, for j >= R (K rows below the round), transposed from
+// LDS into K[c0 + j][c0 + y] (the mirror, coalesced along y).  Rows of S at or past n - c0
+// (padding of the last round) are skipped.
+template <typename T>
+__global__ __launch_bounds__(256) void tri_unpack_kernel(const T *__restrict__ S, int64_t w,
+                                                         int64_t R, int64_t c0, int64_t n,
+                                                         T *__restrict__ K, int64_t ld) {
+  __shared__ T tile[64][65];
+  const int64_t j0 = (int64_t)blockIdx.x * 64;  // S column (K column / mirror row c0 + j)
+  const int64_t y0 = (int64_t)blockIdx.y * 64;  // S row (K row / mirror column c0 + y)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t yend = min(R, n - c0);
+  for (int r = wv; r < 64; r += 4) {
+    const int64_t y = y0 + r, j = j0 + lane;
+    if (y < yend && j < w) {
+      const T v = S[y * w + j];
+      K[(c0 + y) * ld + c0 + j] = v;
+      tile[r][lane] = v;
+    }
+  }
+  if (j0 + 64 <= R) return;  // no column of this tile lies below the round (block-uniform)
+  __syncthreads();
+  for (int r = wv; r < 64; r += 4) {
+    const int64_t j = j0 + r, y = y0 + lane;
+    if (j >= R && j < w && y < yend) K[(c0 + j) * ld + c0 + y] = tile[lane][r];
+  }
+}
+
+hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, int64_t n, void *K,
+                             int64_t ld, int esz, hipStream_t s) {
+  if (w <= 0 || R <= 0 || c0 >= n) return hipSuccess;
+  const int64_t ry = std::min(R, n - c0);
+  const dim3 grid((unsigned)((w + 63) / 64), (unsigned)((ry + 63) / 64));
+  if (grid.y > 65535u) return hipErrorInvalidValue;
+  if (esz == 8)
+    hipLaunchKernelGGL(tri_unpack_kernel<uint64_t>, grid, dim3(256), 0, s, (const uint64_t *)S, w,
+                       R, c0, n, (uint64_t *)K, ld);
+  else
+    hipLaunchKernelGGL(tri_unpack_kernel<uint32_t>, grid, dim3(256), 0, s, (const uint32_t *)S, w,
+                       R, c0, n, (uint32_t *)K, ld);
+  return hipGetLastError();
+}
 
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,

@@ -167,8 +167,16 @@ struct OutSpec {
   int normalize;     // fused normalize_K epilogue
   const double *diagv;  // raw diagonal (normalize)
   const double *dsq;    // sqrt(raw diagonal) (normalize)
+  int64_t col_lo = 0;   // columns < col_lo are not written (upper-triangle multi-GPU
+                        // builds; kernels that honour it: spectrum, mismatch slots / pairs)
 };
 
+// multi-GPU upper-triangle assembly (kmg_gram_blocks): round slab S (R rows x w = n - c0
+// columns, row-major: rows c0 .. c0 + R of K restricted to columns >= c0) -> K's rows
+// c0 + y at columns >= c0, and the lower-triangle mirror K[c0 + j][c0 + y] = S[y][j] for
+// j >= R; one LDS-tiled pass over S (esz = 4 or 8 bytes)
+hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, int64_t n, void *K,
+                             int64_t ld, int esz, hipStream_t s);
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store = 0);

@@ -197,10 +197,14 @@ class Context:
 
     def gram_blocks(self, params, d_codes, d_lens, n, ldc, out_dtype, d_out, ld, nranks, rank,
                     block, gather):
-        """Block-cyclic rows of this rank (+ in-place RCCL all-gather per round when gather)."""
+        """Block-cyclic rows of this rank.  gather: False / 0 this rank's blocks only; True / 1
+        full rows all-gathered in place over RCCL per round; 2 upper-triangle round slabs
+        all-gathered + local mirror; 3 the upper-triangle layout with every rank's blocks
+        computed locally (one-GPU rehearsal, no RCCL)."""
+        g = int(gather) if not isinstance(gather, bool) else (1 if gather else 0)
         check(self.lib.kmg_gram_blocks(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        out_dtype, d_out, ld, int(nranks), int(rank), int(block),
-                                       1 if gather else 0))
+                                       g))
 
     def reload_tuning(self):
         """Re-read the KMG_* environment knobs (read once at context creation)."""

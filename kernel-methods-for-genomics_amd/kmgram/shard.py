@@ -68,4 +68,29 @@ def default_block(n, world, row_bytes, target_bytes=256 << 20):
         return 1
     b = max(1, target_bytes // max(1, world * row_bytes))
     b = min(b, max(1, -(-n // (4 * world))))
+    if b >= 8:
+        b -= b % 8  # round starts stay multiples of 8 (the upper-triangle slabs' first column)
     return int(b)
+
+
+def triangle_rounds(n, world, block):
+    """Upper-triangle layout (kmg_gram_blocks gather = 2): [(c0, w)] per round, the round's
+    first row c0 = t * R and the slab width w = n - c0 (columns >= c0 of its rows)."""
+    r = world * block
+    return [(t * r, n - t * r) for t in range(-(-n // r) if n > 0 else 0)]
+
+
+def assemble_upper_triangle(slabs, n, world, block, dtype):
+    """Host restatement of the gather = 2 assembly: slabs[t] is round t's gathered slab
+    (world * block rows x w_t columns, rank q's block at rows q * block); returns K with
+    K[c0 + i][c0 + j] = slab[i][j] and the mirror K[x][c0 + y] = slab[y][x - c0] for
+    x >= c0 + R.  Used by the world-size-2 gloo test against the one-rank K."""
+    import numpy as np
+    K = np.zeros((n, n), dtype=dtype)
+    r = world * block
+    for (c0, w), S in zip(triangle_rounds(n, world, block), slabs):
+        rows = min(r, n - c0)
+        K[c0:c0 + rows, c0:] = S[:rows, :w]
+        if c0 + r < n:
+            K[c0 + r:, c0:c0 + r] = S[:r, r:w].T
+    return K

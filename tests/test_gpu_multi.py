@@ -63,6 +63,30 @@ def test_blocks_union_equals_full(ctx, data, case, world, block):
     assert np.array_equal(got, full)
 
 
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("world,block", [(1, 1500), (1, 336), (2, 256), (3, 100), (8, 64),
+                                         (4, 50)])
+def test_upper_triangle_assembly_equals_full(ctx, data, case, world, block):
+    """gather = 3: every rank's upper-triangle round slabs (columns >= the round's first row)
+    computed on this GPU, copied into K and mirrored into the lower triangle: exactly the
+    single-call K, every element written (the buffer starts poisoned).  Blocks that are not
+    multiples of 8 and the WD kernel take the full-row scratch + copy-out path."""
+    params, dt = CASES[case]
+    codes, lens = data[0], data[1]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data, params, dt, world, [0], block, gather=3)
+    assert np.array_equal(got, full)
+
+
+def test_upper_triangle_one_rank_gather2(ctx, data):
+    """gather = 2 on one rank needs no communicator and assembles the same K."""
+    params, dt = CASES[1]
+    codes, lens = data[0], data[1]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data, params, dt, 1, [0], 256, gather=2)
+    assert np.array_equal(got, full)
+
+
 def test_block_cyclic_ranges_match_library(ctx, data):
     """The Python layout helper (used by bench.py) and the library agree: rank 1 of 3 writes
     exactly the rows block_cyclic_ranges lists, nothing else."""

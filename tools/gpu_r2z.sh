@@ -2,5 +2,5 @@
 set -u
 OUT=gpurun_out/${1:-r2z}
 mkdir -p "$OUT"
-timeout -k 10 300 python3 -u tools/time_mm.py '[{"kind": "sp", "steps": 20}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 40, "KMG_IDX_THREADS": 256}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 40, "KMG_IDX_THREADS": 512}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 40, "KMG_IDX_THREADS": 1024}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 80, "KMG_IDX_THREADS": 256}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 80, "KMG_IDX_THREADS": 512}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 80, "KMG_IDX_THREADS": 1024}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 160, "KMG_IDX_THREADS": 256}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 160, "KMG_IDX_THREADS": 512}, {"kind": "sp", "steps": 20, "KMG_IDX_SEQS": 160, "KMG_IDX_THREADS": 1024}, {"kind": "sp", "steps": 20, "KMG_IDX_BUCKETS": 128}, {"kind": "sp", "steps": 20, "KMG_IDX_BUCKETS": 256}, {"kind": "sp", "steps": 20, "KMG_IDX_BUCKETS": 512}, {"kind": "sp", "steps": 20}, {"kind": "mm", "steps": 3, "KMG_IDX_SEQS": 40, "check": false}, {"kind": "mm", "steps": 3, "KMG_IDX_SEQS": 80, "check": false}, {"kind": "mm", "steps": 3, "KMG_IDX_SEQS": 160, "check": false}]' > "$OUT/time.jsonl" 2>&1 || { echo "time failed"; tail "$OUT/time.jsonl"; exit 1; }
+timeout -k 10 300 python3 -u tools/time_mm.py '[{"kind": "sp", "k": 5, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 5}, {"kind": "sp", "k": 4, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 5}, {"kind": "sp", "k": 5, "steps": 10, "KMG_DENSE_KMAX_SP": 5}, {"kind": "sp", "k": 6, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 5}, {"kind": "sp", "k": 5, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 4}, {"kind": "sp", "k": 4, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 4}, {"kind": "sp", "k": 5, "steps": 10, "KMG_DENSE_KMAX_SP": 4}, {"kind": "sp", "k": 6, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 4}, {"kind": "sp", "k": 5, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 3}, {"kind": "sp", "k": 4, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 3}, {"kind": "sp", "k": 5, "steps": 10, "KMG_DENSE_KMAX_SP": 3}, {"kind": "sp", "k": 6, "n": 9000, "f64": 1, "steps": 10, "KMG_DENSE_KMAX_SP": 3}]' > "$OUT/time.jsonl" 2>&1 || { echo "time failed"; tail "$OUT/time.jsonl"; exit 1; }
 cat "$OUT/time.jsonl"
