@@ -11,7 +11,8 @@ Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G
 process per GPU, the SAME N=20000 problem (strong scaling), rows dealt block-cyclically
 (kmg_gram_blocks): every rank builds the replicated index, computes its row blocks, and
 each round of G blocks is all-gathered in place over RCCL/xGMI on a second stream while
-the next round is computed.  `value` = N^2 / max-over-ranks step time including that
+the next round is computed (default: only the round's upper-triangle slab travels and every
+GPU mirrors it locally; --gather-mode 1 sends full rows).  `value` = N^2 / max-over-ranks step time including that
 all-gather; `collective_free` reports the same build without it.
 
 Also reported: the mismatch (k=9, m=1) Gram at the same N (BASELINE configs[2], float64
@@ -621,8 +622,9 @@ def main():
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(2)",
         "config": {"workload": "spectrum k=8 full-K build, N=20000 x L=101 (BASELINE "
-                               "configs[1]); G>1: same N, block-cyclic rows + in-place RCCL "
-                               "all-gather so every GPU ends with K",
+                               "configs[1]); G>1: same N, block-cyclic rows, upper-triangle "
+                               "round slabs all-gathered in place over RCCL + local mirror, so "
+                               "every GPU ends with K",
                    "N": n, "L": 101, "k": 8, "rows_this_rank": sp["rows_this_rank"],
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
