@@ -64,6 +64,21 @@ __global__ __launch_bounds__(1024) void rows_buf_kernel(char *out, int64_t n) {
     __builtin_amdgcn_raw_buffer_store_b128((v4i){(int)i, b, 1, 2}, rsrc, b, 0, AUX);
 }
 
+// grid-stride, U stores in flight per thread: iteration it covers [it*G*16*U, ...), thread
+// t writes 16 B at t*16 + u*G*16 (every instruction of a wave contiguous)
+template <int U, int TPB>
+__global__ __launch_bounds__(TPB) void stride_kernel(char *out, int64_t bytes) {
+  const int64_t G = (int64_t)gridDim.x * TPB;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  for (int64_t base = 0; base < bytes; base += G * 16 * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = base + (t + u * G) * 16;
+      if (b + 16 <= bytes) st16<true>(out + b, (v4i){(int)b, u, 1, 2});
+    }
+  }
+}
+
 // persistent: G blocks, block b writes rows b, b + G, ... (G rows in flight)
 template <int ESZ, bool NT>
 __global__ __launch_bounds__(1024) void rows_persist_kernel(char *out, int64_t n) {
@@ -144,6 +159,11 @@ void run_all(char *d, int64_t n) {
   rep("rowsB17sc0sc1", time_it([&] { rows_buf_kernel<ESZ, 17><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsB18sc1nt", time_it([&] { rows_buf_kernel<ESZ, 18><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsB3sc0nt", time_it([&] { rows_buf_kernel<ESZ, 3><<<(unsigned)n, 1024>>>(d, n); }, 10));
+  rep("strideU8_256x1024", time_it([&] { stride_kernel<8, 256><<<1024, 256>>>(d, (int64_t)bytes); }, 10));
+  rep("strideU4_256x2048", time_it([&] { stride_kernel<4, 256><<<2048, 256>>>(d, (int64_t)bytes); }, 10));
+  rep("strideU8_64x4096", time_it([&] { stride_kernel<8, 64><<<4096, 64>>>(d, (int64_t)bytes); }, 10));
+  rep("strideU1_256x8192", time_it([&] { stride_kernel<1, 256><<<8192, 256>>>(d, (int64_t)bytes); }, 10));
+  rep("strideU16_1024x256", time_it([&] { stride_kernel<16, 1024><<<256, 1024>>>(d, (int64_t)bytes); }, 10));
   rep("rowsD1", time_it([&] { rows_delay_kernel<ESZ, NT, 1><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsD2", time_it([&] { rows_delay_kernel<ESZ, NT, 2><<<(unsigned)n, 1024>>>(d, n); }, 10));
   rep("rowsD4", time_it([&] { rows_delay_kernel<ESZ, NT, 4><<<(unsigned)n, 1024>>>(d, n); }, 10));
