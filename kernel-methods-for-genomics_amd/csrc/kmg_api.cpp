@@ -247,8 +247,14 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk, const uint8_t *codes
                 const int32_t *lens = nullptr, int64_t ldc = 0) {
   // coarse buckets (one fine block each), fine LDS histogram <= 2^14 bins: ~384 for the
   // spectrum index, ~1024 for the k-copy mismatch index (16.7M occurrences at N=20000,
-  // where 288 buckets left the fine pass at 240 us and 576 halved it)
-  const int target_buckets = c->tune.idx_buckets > 0 ? c->tune.idx_buckets : (g.copies > 1 ? 1024 : 384);
+  // where 288 buckets left the fine pass at 240 us and 576 halved it); large builds one
+  // bucket per ~40000 occurrences, up to 4096 (N=200000 MM(9,1), 167M occurrences:
+  // place + fine 3.95 -> 2.65 ms at 4096, profiles/r02ad_index_geometry.jsonl)
+  const int64_t occ = g.n * g.pmax * std::max(1, g.copies);
+  const int target_buckets =
+      c->tune.idx_buckets > 0 ? c->tune.idx_buckets
+                              : (int)std::max<int64_t>(g.copies > 1 ? 1024 : 384,
+                                                       std::min<int64_t>(4096, occ / 40000));
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
   g.seqs_per_block = std::max(1, c->tune.idx_seqs);
@@ -432,6 +438,43 @@ int pair_chunk(int64_t n, int pmax, int k, int cap) {
     }
   }
   return (int)std::max<int64_t>(8, (best + 7) & ~7LL);
+}
+
+// Columns per chunk of the drop-one slot table.  A row reads one 128-byte line per
+// (chunk, list), so the lines per row are nch x (1 + the CSR-tail cost of the groups
+// past KMG_SLOT_INLINE entries): fewer, fuller chunks win until the inline line
+// overflows.  Cost per list: 1 line + T with probability P(X > inline), X ~
+// Poisson(chunk * pmax / 4^(k-1)), T = 6 lines: the CSR tail (offsets, then 2-byte
+// entries read by two lanes) costs about six lines' time, calibrated on N=200000
+// MM(9,1) (25000-row slab: 10 chunks 46.8 ms, 8 chunks 38.7, 7 chunks 34.8, 6 chunks
+// 35.7; profiles/r02ac_*).  Largest chunk: the int32 LDS accumulator plus the kernel's
+// tables (launch_gram_mismatch1_slots) in 160 KB, and uint16 entries (<= 65536 columns).
+int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
+  const int nsub = k + 3 * k * (k - 1) / 2;
+  int64_t max_chunk = (160 * 1024 / 4 - (int64_t)pmax * k - nsub - ldp) & ~7LL;
+  max_chunk = std::min<int64_t>(max_chunk, 65536);
+  if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
+  if (max_chunk < 8) return 8;
+  const double keys = (double)pow4(k - 1);
+  int64_t best = std::min<int64_t>(std::max<int64_t>(n, 8), max_chunk);
+  double best_cost = 1e300;
+  const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
+  for (int64_t nch = nch0; nch <= nch0 + 16; ++nch) {
+    const int64_t ch = ((n + nch - 1) / nch + 7) & ~7LL;
+    if (ch > max_chunk) continue;
+    const double mean = (double)ch * pmax / keys;
+    double pr = std::exp(-mean), cdf = 0.0;  // P(X <= inline)
+    for (int x = 0; x <= KMG_SLOT_INLINE; ++x) {
+      if (x > 0) pr *= mean / x;
+      cdf += pr;
+    }
+    const double cost = (double)nch * (1.0 + 6.0 * std::max(0.0, 1.0 - cdf));
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = ch;
+    }
+  }
+  return (int)std::max<int64_t>(8, best);
 }
 
 // Row ranges of one Gram call: every range [row0, row1) x all n columns is written at
@@ -725,10 +768,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = k;
         g.rot = 1;
         g.nkeys = (uint32_t)pow4(k);
-        // mean list (4-bin group) length <= 40: inline in one 128-byte line
-        const int64_t cap = 40 * pow4(k - 1) / std::max(1, g.pmax);
-        const int64_t lim = c->tune.mm_chunk > 0 ? c->tune.mm_chunk : 20480;
-        choose_chunks(g, (int)std::max<int64_t>(8, std::min<int64_t>({lim, cap, 64000})));
+        choose_chunks(g, slot_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk));
       }
       KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
       if (use_slots) {

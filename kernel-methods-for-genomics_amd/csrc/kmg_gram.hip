@@ -972,6 +972,7 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, con
   if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
   const int nsub = g.k + 3 * g.k * (g.k - 1) / 2;
   const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k + nsub + pk.ldp) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)(rows * g.nchunks));
   switch (g.k) {
 #define KMG_MM(KK)                                                                               \
