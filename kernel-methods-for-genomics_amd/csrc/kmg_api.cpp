@@ -111,6 +111,7 @@ struct Tuning {
   int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
   int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky
   int sp_store = 0;         // KMG_SP_STORE: spectrum K stores, 0 auto, 1 non-temporal, 2 plain
+  int dense_sb = 0;         // KMG_DENSE_SB: dense Gram super-block edge in tiles (0: by F panel size)
 };
 
 int env_or(const char *name, int dflt) {
@@ -134,6 +135,7 @@ void read_tuning(Tuning &t) {
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
+  t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -146,6 +148,8 @@ struct kmg_ctx {
   DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
   DevBuf hcnt, hstart;            // index build v2: per-(bucket, block) counts / local starts
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
+  DevBuf dense_tiles;             // dense Gram tile order (dense_tile_order)
+  int64_t dense_key[4] = {-1, -1, -1, -1};
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
   DevBuf tri_stage, tri_scratch;  // upper-triangle multi-GPU build: round slabs, full rows
@@ -528,6 +532,44 @@ int each_range(kmg_ctx *c, const std::vector<RowRange> &ranges, const OutSpec &o
   return KMG_OK;
 }
 
+// Tile order of gram_dense_kernel: S x S super-blocks of 256 x 256 tiles, super-row-major
+// (tiles tm <= tn only for the full square).  The launch deals contiguous ranges of this
+// order to the XCDs, so the ~32 tiles in flight on one XCD read S row panels and 2S column
+// panels of F (256 x dp bytes each) that the XCD's L2 / the Infinity Cache then serve
+// several times, where the plain row-band order read a fresh column panel per tile (F
+// panel reads ~ the K bytes written at k = 5).  S = 4 measured best at every k
+// (N=20000 int32 Gram, S = 1 / 2 / 4 / 8: SP k=5 0.425 / 0.399 / 0.377 / 0.377 ms,
+// SP k=4 0.325 / 0.321 / 0.268 / 0.327, MM k=6 0.990 / 0.948 / 0.922 / 0.931;
+// profiles/r02ae_dense_superblocks.jsonl).  The list is cached per geometry (one upload
+// per shape, stream-synchronised).
+int dense_tile_order(kmg_ctx *c, int64_t n, int64_t r0, int64_t r1, int dp, const uint32_t **out) {
+  *out = nullptr;
+  const int64_t rows = r1 - r0;
+  const bool sym = r0 == 0 && rows == n;
+  const int64_t tm_n = (rows + 255) / 256, tn_n = (n + 255) / 256;
+  if (rows <= 0 || n <= 0 || tm_n > 65535 || tn_n > 65535) return KMG_OK;  // kernel's own order
+  (void)dp;
+  const int S = c->tune.dense_sb > 0 ? std::min(c->tune.dense_sb, 64) : 4;
+  const int64_t key[4] = {tm_n, tn_n, sym ? 1 : 0, S};
+  if (memcmp(key, c->dense_key, sizeof(key)) != 0) {
+    std::vector<uint32_t> v;
+    v.reserve((size_t)(sym ? tn_n * (tn_n + 1) / 2 : tm_n * tn_n));
+    const int64_t sm = (tm_n + S - 1) / S, sn = (tn_n + S - 1) / S;
+    for (int64_t TM = 0; TM < sm; ++TM)
+      for (int64_t TN = sym ? TM : 0; TN < sn; ++TN)
+        for (int64_t tm = TM * S; tm < std::min(tm_n, TM * S + S); ++tm)
+          for (int64_t tn = TN * S; tn < std::min(tn_n, TN * S + S); ++tn)
+            if (!sym || tn >= tm) v.push_back((uint32_t)tm | ((uint32_t)tn << 16));
+    KMG_TRY(c->dense_tiles.ensure(sizeof(uint32_t) * v.size()));
+    KMG_HIP(hipMemcpyAsync(c->dense_tiles.p, v.data(), sizeof(uint32_t) * v.size(),
+                           hipMemcpyHostToDevice, c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));  // pageable source
+    memcpy(c->dense_key, key, sizeof(key));
+  }
+  *out = c->dense_tiles.as<uint32_t>();
+  return KMG_OK;
+}
+
 // F = int8 count / neighbour-count rows, diagonal ||F_i||^2, then K = F F^T (MFMA)
 int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
                const int32_t *d_lens, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
@@ -552,7 +594,9 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
     o.dsq = c->dsq.as<double>();
   }
   return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, oq, c->stream);
+    const uint32_t *order = nullptr;
+    if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream);
   });
 }
 
@@ -595,7 +639,9 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
     o.dsq = c->dsq.as<double>();
   }
   return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, oq, c->stream);
+    const uint32_t *order = nullptr;
+    if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream);
   });
 }
 

@@ -126,6 +126,7 @@ template <int DT, bool SYM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
                                                             int64_t n, int64_t row0, int64_t rows,
                                                             int tiles_m, int tiles_n, int64_t ntiles,
+                                                            const uint32_t *__restrict__ order,
                                                             OutSpec o) {
   using T = typename std::conditional<DT == KMG_F64, double,
                                       typename std::conditional<DT == KMG_F32, float, int32_t>::type>::type;
@@ -134,7 +135,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int64_t logical = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (logical >= ntiles) return;
   int tm, tn;
-  if constexpr (SYM) {  // row-band-major over tm <= tn: band tm holds tiles_n - tm tiles
+  if (order) {  // host-built super-block order (dense_tile_order, kmg_api.cpp)
+    const uint32_t t = order[logical];
+    tm = (int)(t & 0xFFFFu);
+    tn = (int)(t >> 16);
+  } else if constexpr (SYM) {  // row-band-major over tm <= tn: band tm holds tiles_n - tm tiles
     const double Tn = (double)tiles_n;
     int64_t t = (int64_t)((2.0 * Tn + 1.0 - sqrt((2.0 * Tn + 1.0) * (2.0 * Tn + 1.0) - 8.0 * (double)logical)) * 0.5);
     auto cum = [&](int64_t b) { return b * tiles_n - b * (b - 1) / 2; };
@@ -368,7 +373,7 @@ hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, i
 }
 
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
-                             const OutSpec &o, hipStream_t s) {
+                             const uint32_t *order, const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || n <= 0) return hipSuccess;
   if (dp & (DT_BK - 1)) return hipErrorInvalidValue;
@@ -381,7 +386,7 @@ hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, i
   const size_t lds = DT_LDS;
 #define KMG_DENSE(DTV, SY)                                                                       \
   hipLaunchKernelGGL((gram_dense_kernel<DTV, SY>), dim3(grid), dim3(512), lds, s, F, dp, n, row0, \
-                     rows, tiles_m, tiles_n, total, o)
+                     rows, tiles_m, tiles_n, total, order, o)
   switch (o.dtype) {
     case KMG_I32:
       if (sym) KMG_DENSE(KMG_I32, true); else KMG_DENSE(KMG_I32, false);
