@@ -153,6 +153,7 @@ struct kmg_ctx {
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
   DevBuf tri_stage, tri_scratch;  // upper-triangle multi-GPU build: round slabs, full rows
+  DevBuf ovf;                     // 16-bit round slabs: count-overflow flag
   int64_t cur_n = 0;              // columns of the current Gram call
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   Tuning tune;
@@ -204,7 +205,7 @@ struct StageTimer {
   }
 };
 
-size_t dtype_size(int32_t dt) { return dt == KMG_F64 ? 8 : 4; }
+size_t dtype_size(int32_t dt) { return dt == KMG_F64 ? 8 : dt == KMG_U16 ? 2 : 4; }
 
 int64_t pow4(int e) { return (int64_t)1 << (2 * e); }
 
@@ -646,6 +647,35 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 }
 
 // ----------------------------------------------------------------- dispatch
+// Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
+// kmg_gram_blocks' choice of the round-slab format).
+enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS };
+SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax) {
+  const bool mm = p->kind == KMG_MISMATCH;
+  const int k = p->k;
+  const bool exact = !mm || p->m == 0;  // spectrum-shaped: only ham 0 counts
+  // mismatch m = 1: drop-two pair table (auto for k = 10, 11: fewest posting lines per
+  // row) or the drop-one slot table (auto for k = 8, 9 and 12).  At k = 9 the pair kernel
+  // fetches 24% fewer bytes but issues 2x the VALU/SALU work and loses (6.3 vs 4.45 ms,
+  // profiles/r02_mm_pmc.txt); at k = 12 the 66 x 4^10 pair groups cost more to build.
+  const int form = t.mm_form;
+  const bool s1 = mm && p->m == 1;
+  const bool use_pairs = s1 && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
+  const bool use_slots = s1 && !use_pairs && k >= 8 && k <= 12 && form != 2;
+  const bool use_index = (exact && k <= 12) || use_slots || use_pairs;
+  // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
+  // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
+  // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
+  const int mm_eff = mm ? std::min(p->m, k) : 0;
+  const bool dense_ok = k <= 8 && pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096;
+  if (t.algo == 1 || (t.algo == 0 && dense_ok &&
+                      (mm ? (k <= t.dense_kmax_mm) : (k <= t.dense_kmax_sp))))
+    return SM_DENSE;  // (algo 1 without dense_ok: gram_device reports it)
+  if (!use_index) return SM_HAMMING;
+  if (use_pairs) return SM_PAIRS;
+  return exact ? SM_POSTING : SM_SLOTS;
+}
+
 int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
                 int maxlen, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
                 int32_t dt, int64_t ld, const AfterRange &after = nullptr) {
@@ -654,7 +684,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
   for (const RowRange &r : ranges)
     if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
   if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
+  if (dt == KMG_U16 && p->kind != KMG_SPECTRUM && p->kind != KMG_MISMATCH)
+    return fail(KMG_EINVAL, "internal: 16-bit slabs need a posting-list formulation");
   OutSpec o{nullptr, ld, dt, 0, nullptr, nullptr};
+  if (dt == KMG_U16) {  // raw 16-bit slabs: counts above 65535 raise this flag
+    KMG_TRY(c->ovf.ensure(sizeof(uint32_t)));
+    KMG_HIP(hipMemsetAsync(c->ovf.p, 0, sizeof(uint32_t), c->stream));
+    o.ovf = c->ovf.as<uint32_t>();
+  }
   if (c->tune.poison && n > 0)  // testing: no stale output can pass
     for (const RowRange &r : ranges)
       if (r.row1 > r.row0) {
@@ -690,31 +727,18 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
-      // mismatch m = 1: drop-two pair table (auto for k = 10, 11: fewest posting lines per
-      // row) or the drop-one slot table (auto for k = 8, 9 and 12).  At k = 9 the pair kernel
-      // fetches 24% fewer bytes but issues 2x the VALU/SALU work and loses (6.3 vs 4.45 ms,
-      // profiles/r02_mm_pmc.txt); at k = 12 the 66 x 4^10 pair groups cost more to build.
-      const int form = c->tune.mm_form;
-      const bool s1 = mm && p->m == 1;
-      const bool use_pairs = s1 && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
-      const bool use_slots = s1 && !use_pairs && k >= 8 && k <= 12 && form != 2;
-      const bool use_index = (exact && k <= 12) || use_slots || use_pairs;
+      const SmPath path = sm_path(c->tune, p, g.pmax);
+      const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
+      const bool use_index = path == SM_POSTING || use_slots || use_pairs;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
-      // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
-      // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
-      // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
       const int mm_eff = mm ? std::min(p->m, k) : 0;
-      const bool dense_ok = k <= 8 && g.pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096;
-      const int algo = c->tune.algo;
-      bool dense = false;
-      if (algo == 1) {
-        if (!dense_ok)
-          return fail(KMG_EUNSUPPORTED, "dense formulation needs k <= 8 and <= 127 windows");
-        dense = true;
-      } else if (algo == 0 && dense_ok) {
-        dense = mm ? (k <= c->tune.dense_kmax_mm) : (k <= c->tune.dense_kmax_sp);
-      }
+      const bool dense = path == SM_DENSE;
+      if (dense && !(k <= 8 && g.pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096))
+        return fail(KMG_EUNSUPPORTED, "dense formulation needs k <= 8 and <= 127 windows");
+      // raw 16-bit round slabs (kmg_gram_blocks) only from the posting-list kernels
+      if (dt == KMG_U16 && (path == SM_DENSE || path == SM_HAMMING || (exact && g.pmax > 255)))
+        return fail(KMG_EINVAL, "internal: 16-bit slabs need a posting-list formulation");
       if (dense)
         return gram_dense(c, k, mm_eff, mm ? g.window : 0, d_codes, d_lens, n, ldc, ranges, o,
                           mm && p->normalize, after);
@@ -1064,12 +1088,33 @@ int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block) {
   return (n + round - 1) / round * round;
 }
 
+namespace {
+constexpr int KMG_RETRY_WIDE = 1000;  // internal: a 16-bit slab overflowed, redo with 32 bits
+
+int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
+                     void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
+                     int32_t gather, bool allow16);
+}  // namespace
+
 int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype, void *d_out,
                     int64_t ld_out, int32_t nranks, int32_t rank, int64_t block, int32_t gather) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
   KMG_TRY(check_params(p, n, ldc, out_dtype));
+  const int r = gram_blocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks,
+                                 rank, block, gather, true);
+  if (r != KMG_RETRY_WIDE) return r;
+  return gram_blocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks, rank,
+                          block, gather, false);
+}
+
+namespace {
+int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
+                     void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
+                     int32_t gather, bool allow16) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
   if (block < 1) return fail(KMG_EINVAL, "block < 1");
   if (gather < 0 || gather > 3) return fail(KMG_EINVAL, "gather must be 0..3");
@@ -1082,6 +1127,25 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   const size_t esz = dtype_size(out_dtype);
   const int64_t round = (int64_t)nranks * block;
   const int64_t nround = (n + round - 1) / round;
+  // Upper-triangle round slabs travel as raw uint16 counts whenever a posting-list kernel
+  // builds them (spectrum: every count <= P_max^2 <= 65025 for P_max <= 255; mismatch:
+  // checked, a count above 65535 sets a flag and the build is redone with 32-bit slabs):
+  // half the xGMI bytes of an int32 K, a quarter of a float64 one; the unpack pass widens
+  // (and normalises) them into K.
+  int32_t wire = out_dtype;
+  bool check16 = false;
+  if (gather >= 2 && allow16 && (p->kind == KMG_SPECTRUM || p->kind == KMG_MISMATCH) &&
+      p->k >= 1 && p->k <= 16) {
+    const bool mm = p->kind == KMG_MISMATCH;
+    const int L = mm ? (p->window > 0 ? p->window : 101) : (int)ldc;  // gram_device's maxlen
+    const int pmax = std::max(1, L - p->k + 1);
+    const SmPath path = sm_path(c->tune, p, pmax);
+    if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS) {
+      wire = KMG_U16;
+      check16 = path != SM_POSTING;
+    }
+  }
+  const size_t wsz = dtype_size(wire);
   if (rccl && !c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   if ((rccl || tri) && !c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
   hipStream_t post = rccl ? c->comm_stream : c->stream;  // gather + mirror stream
@@ -1133,7 +1197,7 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     // Two slabs alternate; round t waits for the mirror of round t - 2 before reusing its
     // slab.  gather = 3 computes every rank's blocks locally (a one-GPU rehearsal of the
     // same layout, no RCCL).
-    const size_t slab = (size_t)round * (size_t)std::max<int64_t>(n, 1) * esz;
+    const size_t slab = (size_t)round * (size_t)std::max<int64_t>(n, 1) * wsz;
     KMG_TRY(c->tri_stage.ensure(2 * slab));
     for (int64_t t = 0; t < nround; ++t) {
       const int64_t c0 = t * round, w = n - c0;
@@ -1143,7 +1207,7 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
         const int64_t r0 = std::min(n, c0 + (int64_t)q * block);
         const int64_t r1 = std::min(n, r0 + block);
         // `out` addresses column 0 of row r0: columns < c0 are never written
-        char *out = S + ((int64_t)q * block * w - c0) * (int64_t)esz;
+        char *out = S + ((int64_t)q * block * w - c0) * (int64_t)wsz;
         ranges.push_back(RowRange{r0, r1, out, w, c0});
         last_of_round.push_back(-1);
       }
@@ -1161,22 +1225,44 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
       if (rccl) {
         KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
         KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
-        KMG_TRY(gather_bytes(S, (size_t)block * w * esz));
+        KMG_TRY(gather_bytes(S, (size_t)block * w * wsz));
       }
-      KMG_HIP(launch_tri_unpack(S, w, round, c0, n, d_out, ld_out, (int)esz, post));
+      if (wire == KMG_U16)
+        KMG_HIP(launch_tri_unpack16((const uint16_t *)S, w, round, c0, n, d_out, ld_out, out_dtype,
+                                    p->normalize, c->diagv.as<double>(), c->dsq.as<double>(), post));
+      else
+        KMG_HIP(launch_tri_unpack(S, w, round, c0, n, d_out, ld_out, (int)esz, post));
       KMG_HIP(hipEventRecord(c->ev_tri[t & 1], post));
       // the next Gram launch (round t + 1) writes the slab round t - 1 used
       if (t >= 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_tri[(t - 1) & 1], 0));
       return KMG_OK;
     };
   }
-  KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, ld_out, after));
+  KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, tri ? wire : out_dtype,
+                      ld_out, after));
   if (rccl) {  // stream order: later work on the context stream sees the full K
     KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
     KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
   }
+  if (check16 && n > 0) {
+    // one 4-byte read per build; all ranks agree (max over ranks) before any redoes
+    if (rccl) {
+      KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+      KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+      ncclResult_t r = ncclAllReduce(c->ovf.p, c->ovf.p, 1, ncclUint32, ncclMax, c->comm,
+                                     c->comm_stream);
+      if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+      KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
+      KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+    }
+    uint32_t flag = 0;
+    KMG_HIP(hipMemcpyAsync(&flag, c->ovf.p, sizeof(flag), hipMemcpyDeviceToHost, c->stream));
+    KMG_HIP(hipStreamSynchronize(c->stream));
+    if (flag) return KMG_RETRY_WIDE;
+  }
   return KMG_OK;
 }
+}  // namespace
 
 int kmg_normalize(kmg_ctx *c, double *K, int64_t n, int64_t ld, int32_t *skipped) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");

@@ -23,6 +23,7 @@
 #include "kmg_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace kmg {
 
@@ -115,6 +116,44 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
                                          int cw, const int32_t *acc, bool norm) {
   // columns below o.col_lo are not written; col_lo - col0 is a multiple of 8 (host check)
   const int qs = (int)max((int64_t)0, o.col_lo - col0);
+  if (o.dtype == KMG_U16) {
+    // raw counts as uint16 (multi-GPU round slabs; no normalisation here: the unpack pass
+    // applies it), 8 columns = 16 B per lane and step; a count above 65535 is clipped and
+    // flagged, and the caller redoes the build with 32-bit slabs
+    uint16_t *prow = (uint16_t *)o.out + il * o.ld + col0;
+    bool big = false;
+    for (int q = qs + threadIdx.x * 8; q < cw; q += blockDim.x * 8) {
+      uint32_t v[8];
+      if (q + 8 <= cw) {
+        const uint4 a = *(const uint4 *)&acc[q], b = *(const uint4 *)&acc[q + 4];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      } else {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) v[h] = q + h < cw ? (uint32_t)acc[q + h] : 0u;
+      }
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        big |= v[h] > 0xFFFFu;
+        v[h] = min(v[h], 0xFFFFu);
+      }
+      uint16_t *d = prow + q;
+      if (q + 8 <= cw && (((uintptr_t)d) & 15) == 0) {
+        const uint4 x = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16),
+                                   v[6] | (v[7] << 16));
+        if constexpr (NT) {
+          typedef int v4i __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(__builtin_bit_cast(v4i, x), (v4i *)d);
+        } else {
+          *(uint4 *)d = x;
+        }
+      } else {
+        for (int h = 0; h < 8 && q + h < cw; ++h) d[h] = (uint16_t)v[h];
+      }
+    }
+    if (big && o.ovf) atomicOr(o.ovf, 1u);
+    return;
+  }
   if (o.dtype == KMG_F64) {
     typedef double v2d __attribute__((ext_vector_type(2)));
     double *prow = (double *)o.out + il * o.ld + col0;
@@ -239,7 +278,28 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
   const int qs = (int)max((int64_t)0, o.col_lo - col0);  // a multiple of 8 (host check)
-  if constexpr (DT == KMG_F64) {
+  if constexpr (DT == KMG_U16) {
+    // raw counts as uint16 (multi-GPU round slabs, never normalised here): with PACK16 the
+    // LDS words are the uint16 pairs themselves (column 2w in the low half = little-endian
+    // order), 8 columns = 16 B per lane and step; P_max <= 255 bounds every count by 65025
+    static_assert(PACK16, "16-bit slabs need the packed accumulator");
+    uint16_t *prow = (uint16_t *)o.out + il * o.ld + col0;
+    for (int q = qs + threadIdx.x * 8; q < cw; q += blockDim.x * 8) {
+      const uint4 w = *(const uint4 *)&acc[q >> 1];
+      uint16_t *d = prow + q;
+      if (q + 8 <= cw && (((uintptr_t)d) & 15) == 0) {
+        if constexpr (NT) {
+          typedef int v4i __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(__builtin_bit_cast(v4i, w), (v4i *)d);
+        } else {
+          *(uint4 *)d = w;
+        }
+      } else {
+        const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+        for (int h = 0; h < 8 && q + h < cw; ++h) d[h] = (uint16_t)(x[h >> 1] >> (16 * (h & 1)));
+      }
+    }
+  } else if constexpr (DT == KMG_F64) {
     // two columns (16 B) per lane and step, so every store instruction of a wave covers
     // 1 KB of the row contiguously (whole lines: no partial-line writes)
     typedef double v2d __attribute__((ext_vector_type(2)));
@@ -922,6 +982,70 @@ __global__ __launch_bounds__(256) void tri_unpack_kernel(const T *__restrict__ S
   }
 }
 
+// The same pass from a uint16 slab of raw counts, widened to K's dtype on the way; with
+// normalisation every element is K_ij / (sqrt(K_ii) * sqrt(K_jj)), diagonal 1 — the
+// Gram kernels' fused epilogue (emit4 / emit_row), bit for bit, and symmetric because the
+// product of the two square roots is commutative, so the tile holds the final values for
+// the mirror too (mirrored elements are never diagonal: j >= R > y).
+template <typename TO>
+__global__ __launch_bounds__(256) void tri_unpack16_kernel(const uint16_t *__restrict__ S, int64_t w,
+                                                           int64_t R, int64_t c0, int64_t n,
+                                                           TO *__restrict__ K, int64_t ld,
+                                                           int normalize,
+                                                           const double *__restrict__ diagv,
+                                                           const double *__restrict__ dsq) {
+  __shared__ TO tile[64][65];
+  const int64_t j0 = (int64_t)blockIdx.x * 64;
+  const int64_t y0 = (int64_t)blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t yend = min(R, n - c0);
+  const bool norm = normalize && diagv[0] != 1.0;
+  for (int r = wv; r < 64; r += 4) {
+    const int64_t y = y0 + r, j = j0 + lane;
+    if (y < yend && j < w) {
+      const uint32_t v = S[y * w + j];
+      const int64_t gr = c0 + y, gc = c0 + j;
+      TO x;
+      if constexpr (std::is_same<TO, int32_t>::value) {
+        x = (int32_t)v;
+      } else {
+        const double d = !norm ? (double)v : (gr == gc) ? 1.0 : (double)v / (dsq[gr] * dsq[gc]);
+        x = (TO)d;
+      }
+      K[gr * ld + gc] = x;
+      tile[r][lane] = x;
+    }
+  }
+  if (j0 + 64 <= R) return;
+  __syncthreads();
+  for (int r = wv; r < 64; r += 4) {
+    const int64_t j = j0 + r, y = y0 + lane;
+    if (j >= R && j < w && y < yend) K[(c0 + j) * ld + c0 + y] = tile[lane][r];
+  }
+}
+
+hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
+                               void *K, int64_t ld, int dt, int normalize, const double *diagv,
+                               const double *dsq, hipStream_t s) {
+  if (w <= 0 || R <= 0 || c0 >= n) return hipSuccess;
+  if (normalize && (!diagv || !dsq)) return hipErrorInvalidValue;
+  const int64_t ry = std::min(R, n - c0);
+  const dim3 grid((unsigned)((w + 63) / 64), (unsigned)((ry + 63) / 64));
+  if (grid.y > 65535u) return hipErrorInvalidValue;
+  if (dt == KMG_I32)
+    hipLaunchKernelGGL(tri_unpack16_kernel<int32_t>, grid, dim3(256), 0, s, S, w, R, c0, n,
+                       (int32_t *)K, ld, 0, diagv, dsq);
+  else if (dt == KMG_F32)
+    hipLaunchKernelGGL(tri_unpack16_kernel<float>, grid, dim3(256), 0, s, S, w, R, c0, n,
+                       (float *)K, ld, normalize, diagv, dsq);
+  else if (dt == KMG_F64)
+    hipLaunchKernelGGL(tri_unpack16_kernel<double>, grid, dim3(256), 0, s, S, w, R, c0, n,
+                       (double *)K, ld, normalize, diagv, dsq);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, int64_t n, void *K,
                              int64_t ld, int esz, hipStream_t s) {
   if (w <= 0 || R <= 0 || c0 >= n) return hipSuccess;
@@ -949,6 +1073,12 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   const dim3 grid((unsigned)(rows * g.nchunks));
   // store policy: 0 auto (plain for a single-chunk int32 K, else non-temporal), 1 NT, 2 plain
   const bool nt = store == 1 || (store == 0 && !(o.dtype == KMG_I32 && g.nchunks == 1));
+  if (o.dtype == KMG_U16) {  // raw 16-bit round slab (kmg_gram_blocks), plain stores
+    if (!pack) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U16, false>), grid, dim3(1024), lds, s, g, pk,
+                       off, ent, row0, o);
+    return hipGetLastError();
+  }
 #define KMG_SP(PK, NTV)                                                                       \
   KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<PK, D, NTV>), grid, dim3(1024), \
                                               lds, s, g, pk, off, ent, row0, o))

@@ -13,6 +13,9 @@
 // slot layout of the rotated mismatch index: 128-byte line = 8-byte header + 60 entries
 #define KMG_SLOT_BYTES 128
 #define KMG_SLOT_INLINE 60
+// internal output dtype (not in the ABI): raw counts as uint16, the round slabs of the
+// multi-GPU upper-triangle assembly (kmg_gram_blocks), widened by tri_unpack16_kernel
+#define KMG_U16 16
 
 namespace kmg {
 
@@ -169,6 +172,8 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
   int64_t col_lo = 0;   // columns < col_lo are not written (upper-triangle multi-GPU
                         // builds; kernels that honour it: spectrum, mismatch slots / pairs)
+  uint32_t *ovf = nullptr;  // dtype KMG_U16: set to 1 when a count exceeds 65535 (the
+                            // stored value is then clipped and the caller redoes the build)
 };
 
 // multi-GPU upper-triangle assembly (kmg_gram_blocks): round slab S (R rows x w = n - c0
@@ -177,6 +182,12 @@ struct OutSpec {
 // j >= R; one LDS-tiled pass over S (esz = 4 or 8 bytes)
 hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, int64_t n, void *K,
                              int64_t ld, int esz, hipStream_t s);
+// the same from a uint16 slab of raw counts into K of dtype dt (int32 / float32 / float64),
+// normalize_K applied on the way when `normalize` and diagv[0] != 1 (the fused epilogue's
+// formula, bit for bit)
+hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
+                               void *K, int64_t ld, int dt, int normalize, const double *diagv,
+                               const double *dsq, hipStream_t s);
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store = 0);

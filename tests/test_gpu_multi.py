@@ -78,6 +78,36 @@ def test_upper_triangle_assembly_equals_full(ctx, data, case, world, block):
     assert np.array_equal(got, full)
 
 
+@pytest.fixture(scope="module")
+def data_repeats(ctx):
+    """Every 97th row a homopolymer: its raw mismatch (9,1) self-count is 93 * 93 * 28 =
+    242172, past the 16-bit round slabs (the build must notice and redo with 32 bits); the
+    spectrum counts stay <= 94^2."""
+    codes, lens = E.synthetic(600, 101, seed=72)
+    codes[::97] = 0
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    yield codes, lens, d_codes, d_lens
+    ctx.dfree(d_codes)
+    ctx.dfree(d_lens)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+@pytest.mark.parametrize("world,block", [(2, 128), (3, 64)])
+def test_upper_triangle_16bit_slabs_overflow(ctx, data_repeats, case, world, block):
+    """Round slabs travel as raw uint16 counts (spectrum: always; mismatch: until a count
+    passes 65535, then the whole build is redone with 32-bit slabs): the assembled K equals
+    the single-call K with homopolymer rows in the input."""
+    params, dt = CASES[case]
+    codes, lens = data_repeats[0], data_repeats[1]
+    full = ctx.gram(params, codes, lens, dt)
+    if case == 2:
+        assert full.max() > 65535  # the redo path really runs
+    got = _run_blocks(ctx, data_repeats, params, dt, world, [0], block, gather=3)
+    assert np.array_equal(got, full)
+
+
 def test_upper_triangle_one_rank_gather2(ctx, data):
     """gather = 2 on one rank needs no communicator and assembles the same K."""
     params, dt = CASES[1]
