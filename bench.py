@@ -530,7 +530,8 @@ def gather_roofline(res, world, esz):
         return None
     n = res["N"]
     npad = rows_padded(n, world, res["block_rows"])
-    if res.get("gather_mode") == 2:  # upper-triangle round slabs
+    if res.get("gather_mode") == 2:  # upper-triangle round slabs, raw uint16 counts
+        esz = 2  # (posting-list kernels; a mismatch count past 65535 redoes with 32 bits)
         r = world * res["block_rows"]
         recv = (world - 1) / world * sum(r * w for _, w in triangle_rounds(n, world, res["block_rows"])) * esz
     else:

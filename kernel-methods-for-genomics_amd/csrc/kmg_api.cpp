@@ -175,6 +175,8 @@ struct kmg_ctx {
   hipStream_t comm_stream = nullptr;  // RCCL all-gathers of kmg_gram_blocks
   hipEvent_t ev_sync = nullptr;       // context stream <-> comm stream ordering
   hipEvent_t ev_tri[2] = {nullptr, nullptr};  // upper-triangle slabs released by their mirror
+  hipStream_t unpack_stream = nullptr;          // upper triangle over RCCL: unpack of round t
+  hipEvent_t ev_gath[2] = {nullptr, nullptr};   // overlaps the all-gather of round t + 1
   int nranks = 1, rank = 0;
 };
 
@@ -1021,6 +1023,9 @@ int kmg_destroy(kmg_ctx *c) {
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
+  if (c->unpack_stream) (void)hipStreamDestroy(c->unpack_stream);
+  for (hipEvent_t e : c->ev_gath)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_tri)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1120,7 +1125,9 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   if (gather < 0 || gather > 3) return fail(KMG_EINVAL, "gather must be 0..3");
   if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
   const bool tri = gather >= 2;               // upper-triangle round slabs + local mirror
-  const bool rccl = (gather == 1 || gather == 2) && nranks > 1;
+  // RCCL path: more than one rank, or a communicator of exactly this one rank (a 1-rank
+  // all-gather is an in-place no-op: the one-GPU test of the stream / event ordering)
+  const bool rccl = (gather == 1 || gather == 2) && (nranks > 1 || (c->comm && c->nranks == 1));
   if (rccl && (!c->comm || c->nranks != nranks || c->rank != rank))
     return fail(KMG_EINVAL, "gather needs a communicator of %d ranks with this rank %d", nranks, rank);
   KMG_HIP(hipSetDevice(c->device));
@@ -1148,7 +1155,13 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   const size_t wsz = dtype_size(wire);
   if (rccl && !c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   if ((rccl || tri) && !c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
-  hipStream_t post = rccl ? c->comm_stream : c->stream;  // gather + mirror stream
+  // unpack (mirror) stream: its own stream over RCCL, so the unpack of round t overlaps the
+  // all-gather of round t + 1 on the comm stream
+  if (rccl && tri && !c->unpack_stream) {
+    KMG_HIP(hipStreamCreateWithFlags(&c->unpack_stream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) KMG_HIP(hipEventCreateWithFlags(&c->ev_gath[b], hipEventDisableTiming));
+  }
+  hipStream_t post = rccl ? (tri ? c->unpack_stream : c->comm_stream) : c->stream;
   auto gather_bytes = [&](char *recv, size_t count) -> int {  // in place, rank r at r * count
     hipEvent_t b = nullptr, e = nullptr;
     if (c->timing) {
@@ -1226,6 +1239,8 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
         KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
         KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
         KMG_TRY(gather_bytes(S, (size_t)block * w * wsz));
+        KMG_HIP(hipEventRecord(c->ev_gath[t & 1], c->comm_stream));
+        KMG_HIP(hipStreamWaitEvent(post, c->ev_gath[t & 1], 0));
       }
       if (wire == KMG_U16)
         KMG_HIP(launch_tri_unpack16((const uint16_t *)S, w, round, c0, n, d_out, ld_out, out_dtype,
@@ -1243,6 +1258,10 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   if (rccl) {  // stream order: later work on the context stream sees the full K
     KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
     KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+    if (post != c->comm_stream) {
+      KMG_HIP(hipEventRecord(c->ev_sync, post));
+      KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+    }
   }
   if (check16 && n > 0) {
     // one 4-byte read per build; all ranks agree (max over ranks) before any redoes

@@ -982,45 +982,122 @@ __global__ __launch_bounds__(256) void tri_unpack_kernel(const T *__restrict__ S
   }
 }
 
-// The same pass from a uint16 slab of raw counts, widened to K's dtype on the way; with
-// normalisation every element is K_ij / (sqrt(K_ii) * sqrt(K_jj)), diagonal 1 — the
-// Gram kernels' fused epilogue (emit4 / emit_row), bit for bit, and symmetric because the
-// product of the two square roots is commutative, so the tile holds the final values for
-// the mirror too (mirrored elements are never diagonal: j >= R > y).
+// The same assembly from a uint16 slab of raw counts, widened to K's dtype on the way, as
+// two streaming passes with 16-byte accesses on both sides: (1) rows — K[c0 + y][c0 + j] =
+// S[y][j], 8 columns a thread; (2) mirror — 64 x 64 tiles of S[:, R:] through LDS into
+// K[c0 + j][c0 + y0 .. + 64) (256 / 512 contiguous bytes per output row).  With
+// normalisation every element is K_ij / (sqrt(K_ii) * sqrt(K_jj)), diagonal 1: the Gram
+// kernels' fused epilogue (emit4 / emit_row) bit for bit, and symmetric because the
+// product of the two square roots is commutative.  (The round-2 single-pass 64 x 64 kernel
+// with 4-byte accesses moved ~3.3 TB/s.)
 template <typename TO>
-__global__ __launch_bounds__(256) void tri_unpack16_kernel(const uint16_t *__restrict__ S, int64_t w,
-                                                           int64_t R, int64_t c0, int64_t n,
+__device__ __forceinline__ TO widen16(uint32_t v, int64_t gr, int64_t gc, bool norm,
+                                      const double *__restrict__ dsq) {
+  if constexpr (std::is_same<TO, int32_t>::value) {
+    return (int32_t)v;
+  } else {
+    const double d = !norm ? (double)v : (gr == gc) ? 1.0 : (double)v / (dsq[gr] * dsq[gc]);
+    return (TO)d;
+  }
+}
+
+template <typename TO>
+__device__ __forceinline__ void store_out(TO *p, const TO (&v)[16 / sizeof(TO)]) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i x;
+  __builtin_memcpy(&x, v, 16);
+  *(v4i *)p = x;
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void tri_rows16_kernel(const uint16_t *__restrict__ S, int64_t w,
+                                                         int64_t yend, int64_t c0,
+                                                         TO *__restrict__ K, int64_t ld,
+                                                         int normalize,
+                                                         const double *__restrict__ diagv,
+                                                         const double *__restrict__ dsq) {
+  constexpr int V = 16 / (int)sizeof(TO);  // outputs per 16-byte store
+  const int64_t per_row = (w + 7) >> 3;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per_row * yend) return;
+  const bool norm = normalize && diagv[0] != 1.0;
+  const int64_t y = t / per_row, j = (t - y * per_row) * 8;
+  const uint16_t *src = S + y * w + j;
+  const int64_t gr = c0 + y, gc = c0 + j;
+  TO *dst = K + gr * ld + gc;
+  const int cnt = (int)min((int64_t)8, w - j);
+  uint32_t v[8];
+  if (cnt == 8 && (((uintptr_t)src) & 15) == 0) {
+    const uint4 x = *(const uint4 *)src;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h) v[h] = (xs[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+  } else {
+#pragma unroll
+    for (int h = 0; h < 8; ++h) v[h] = h < cnt ? (uint32_t)src[h] : 0u;
+  }
+  if (cnt == 8 && (((uintptr_t)dst) & 15) == 0) {
+#pragma unroll
+    for (int b = 0; b < 8; b += V) {
+      TO o[V];
+#pragma unroll
+      for (int q = 0; q < V; ++q) o[q] = widen16<TO>(v[b + q], gr, gc + b + q, norm, dsq);
+      store_out<TO>(dst + b, o);
+    }
+  } else {
+    for (int h = 0; h < cnt; ++h) dst[h] = widen16<TO>(v[h], gr, gc + h, norm, dsq);
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void tri_mirror16_kernel(const uint16_t *__restrict__ S, int64_t w,
+                                                           int64_t R, int64_t yend, int64_t c0,
                                                            TO *__restrict__ K, int64_t ld,
                                                            int normalize,
                                                            const double *__restrict__ diagv,
                                                            const double *__restrict__ dsq) {
-  __shared__ TO tile[64][65];
-  const int64_t j0 = (int64_t)blockIdx.x * 64;
+  constexpr int V = 16 / (int)sizeof(TO);
+  __shared__ uint32_t tile[64][65];  // [y][j]
+  const int64_t j0 = R + (int64_t)blockIdx.x * 64;  // S column of the tile (>= R)
   const int64_t y0 = (int64_t)blockIdx.y * 64;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t yend = min(R, n - c0);
   const bool norm = normalize && diagv[0] != 1.0;
-  for (int r = wv; r < 64; r += 4) {
-    const int64_t y = y0 + r, j = j0 + lane;
-    if (y < yend && j < w) {
-      const uint32_t v = S[y * w + j];
-      const int64_t gr = c0 + y, gc = c0 + j;
-      TO x;
-      if constexpr (std::is_same<TO, int32_t>::value) {
-        x = (int32_t)v;
-      } else {
-        const double d = !norm ? (double)v : (gr == gc) ? 1.0 : (double)v / (dsq[gr] * dsq[gc]);
-        x = (TO)d;
-      }
-      K[gr * ld + gc] = x;
-      tile[r][lane] = x;
+  // load: 64 rows x 8 chunks of 8 columns
+  for (int c = threadIdx.x; c < 512; c += blockDim.x) {
+    const int r = c >> 3, q8 = (c & 7) * 8;
+    const int64_t y = y0 + r, j = j0 + q8;
+    uint32_t v[8];
+    const uint16_t *src = S + y * w + j;
+    if (y < yend && j + 8 <= w && (((uintptr_t)src) & 15) == 0) {
+      const uint4 x = *(const uint4 *)src;
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) v[h] = (xs[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+    } else {
+#pragma unroll
+      for (int h = 0; h < 8; ++h) v[h] = (y < yend && j + h < w) ? (uint32_t)src[h] : 0u;
     }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) tile[r][q8 + h] = v[h];
   }
-  if (j0 + 64 <= R) return;
   __syncthreads();
-  for (int r = wv; r < 64; r += 4) {
-    const int64_t j = j0 + r, y = y0 + lane;
-    if (j >= R && j < w && y < yend) K[(c0 + j) * ld + c0 + y] = tile[lane][r];
+  // store: output row c0 + j0 + jj, columns c0 + y0 + [0, 64): 64 / V chunks of 16 bytes
+  constexpr int CPR = 64 / V;
+  for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
+    const int jj = c / CPR, yy = (c - jj * CPR) * V;
+    const int64_t j = j0 + jj;
+    if (j >= w) continue;
+    const int64_t gr = c0 + j, gc = c0 + y0 + yy;
+    TO *dst = K + gr * ld + gc;
+    const int cnt = (int)min((int64_t)V, yend - (y0 + yy));
+    if (cnt <= 0) continue;
+    TO o[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) o[q] = widen16<TO>(tile[yy + q][jj], gr, gc + q, norm, dsq);
+    if (cnt == V && (((uintptr_t)dst) & 15) == 0) {
+      store_out<TO>(dst, o);
+    } else {
+      for (int q = 0; q < cnt; ++q) dst[q] = o[q];
+    }
   }
 }
 
@@ -1029,20 +1106,29 @@ hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t 
                                const double *dsq, hipStream_t s) {
   if (w <= 0 || R <= 0 || c0 >= n) return hipSuccess;
   if (normalize && (!diagv || !dsq)) return hipErrorInvalidValue;
-  const int64_t ry = std::min(R, n - c0);
-  const dim3 grid((unsigned)((w + 63) / 64), (unsigned)((ry + 63) / 64));
-  if (grid.y > 65535u) return hipErrorInvalidValue;
+  const int64_t yend = std::min(R, n - c0);
+  const int64_t items = ((w + 7) >> 3) * yend;
+  const dim3 g1((unsigned)((items + 255) / 256));
+  const bool mir = w > R;
+  const dim3 g2((unsigned)(mir ? (w - R + 63) / 64 : 0), (unsigned)((yend + 63) / 64));
+  if (g2.y > 65535u || (items + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+#define KMG_UNPACK(T)                                                                            \
+  do {                                                                                           \
+    hipLaunchKernelGGL(tri_rows16_kernel<T>, g1, dim3(256), 0, s, S, w, yend, c0, (T *)K, ld,    \
+                       dt == KMG_I32 ? 0 : normalize, diagv, dsq);                               \
+    if (mir)                                                                                     \
+      hipLaunchKernelGGL(tri_mirror16_kernel<T>, g2, dim3(256), 0, s, S, w, R, yend, c0, (T *)K, \
+                         ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);                         \
+  } while (0)
   if (dt == KMG_I32)
-    hipLaunchKernelGGL(tri_unpack16_kernel<int32_t>, grid, dim3(256), 0, s, S, w, R, c0, n,
-                       (int32_t *)K, ld, 0, diagv, dsq);
+    KMG_UNPACK(int32_t);
   else if (dt == KMG_F32)
-    hipLaunchKernelGGL(tri_unpack16_kernel<float>, grid, dim3(256), 0, s, S, w, R, c0, n,
-                       (float *)K, ld, normalize, diagv, dsq);
+    KMG_UNPACK(float);
   else if (dt == KMG_F64)
-    hipLaunchKernelGGL(tri_unpack16_kernel<double>, grid, dim3(256), 0, s, S, w, R, c0, n,
-                       (double *)K, ld, normalize, diagv, dsq);
+    KMG_UNPACK(double);
   else
     return hipErrorInvalidValue;
+#undef KMG_UNPACK
   return hipGetLastError();
 }
 

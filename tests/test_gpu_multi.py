@@ -133,15 +133,18 @@ def test_block_cyclic_ranges_match_library(ctx, data):
 
 
 def test_blocks_gather_single_rank_comm(ctx, data):
-    """gather=1 on a 1-rank RCCL communicator: the comm-stream / event ordering path with
-    in-place ncclAllGather per round; the result is the full K on the context stream."""
+    """gather = 1 (full rows) and 2 (upper-triangle uint16 slabs, unpacked on their own
+    stream) on a 1-rank RCCL communicator: the comm-stream / unpack-stream / event ordering
+    path with an in-place ncclAllGather per round; the result is the full K on the context
+    stream."""
     uid = L.Context.unique_id()
     ctx.comm_init(uid, 1, 0)
     try:
-        for params, dt in CASES[:2]:
+        for params, dt in CASES[:3]:
             full = ctx.gram(params, data[0], data[1], dt)
-            got = _run_blocks(ctx, data, params, dt, 1, [0], 200, gather=True)
-            assert np.array_equal(got, full)
+            for gather, block in ((1, 200), (2, 200), (2, 96)):
+                got = _run_blocks(ctx, data, params, dt, 1, [0], block, gather=gather)
+                assert np.array_equal(got, full), (gather, block)
         with pytest.raises(L.KmgError):  # communicator size must match
             _run_blocks(ctx, data, CASES[0][0], CASES[0][1], 2, [0], 200, gather=True)
     finally:
