@@ -118,6 +118,18 @@ int kmg_gram_device(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
                     const int32_t *d_lens, int64_t n, int64_t ldc, int64_t row0, int64_t row1,
                     int32_t out_dtype, void *d_out, int64_t ld_out);
 
+/*
+ * The full K of all n rows into HOST memory h_out (row stride ld_host elements; e.g. a
+ * memory-mapped .npy), built on the device in slabs of slab_rows rows: the posting index /
+ * features / diagonal are built once for all slabs, and slab t's device-to-host copy (a
+ * second stream) overlaps slab t+1's Gram.  The slab unit of utils.get_training_datas'
+ * K cache at N >= 100k (utils.py:139-155, select_method kernels.py:461-505).  Returns
+ * after the last copy has landed.
+ */
+int kmg_gram_to_host(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
+                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
+                     int64_t slab_rows, void *h_out, int64_t ld_host);
+
 /* normalize_K (kernels.py:398-415) in place on a host float64 matrix, including the
  * "K[0,0]==1 -> unchanged" rule (returns 1 in *skipped then). */
 int kmg_normalize(kmg_ctx *ctx, double *K, int64_t n, int64_t ld, int32_t *skipped);

@@ -162,6 +162,10 @@ struct kmg_ctx {
   rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
+  DevBuf slabs;                   // kmg_gram_to_host: two device row slabs
+  hipStream_t d2h_stream = nullptr;             // kmg_gram_to_host: slab copies out
+  hipEvent_t ev_slab[2] = {nullptr, nullptr};   // slab Gram done / copied out
+  hipEvent_t ev_out[2] = {nullptr, nullptr};
   int timing = 0;  // 0 off, 1 every stage, 2 the Gram and gather stages only
   // per-stage event pairs of every timed call since the last reset (read after a sync)
   std::vector<hipEvent_t> ev_pool;
@@ -1018,7 +1022,7 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
-                    &c->tri_stage, &c->tri_scratch};
+                    &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -1027,6 +1031,11 @@ int kmg_destroy(kmg_ctx *c) {
   for (hipEvent_t e : c->ev_gath)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_tri)
+    if (e) (void)hipEventDestroy(e);
+  if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
+  for (hipEvent_t e : c->ev_slab)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_out)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1078,6 +1087,56 @@ int kmg_gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   // max(lens) <= ldc (checked in the host path).  maxlen = ldc bounds every kernel.
   return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, {RowRange{row0, row1, d_out}},
                      out_dtype, ld_out);
+}
+
+int kmg_gram_to_host(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
+                     int64_t slab_rows, void *h_out, int64_t ld_host) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_TRY(check_params(p, n, ldc, out_dtype));
+  if (n == 0) return KMG_OK;
+  if (!h_out || ld_host < n || slab_rows < 1) return fail(KMG_EINVAL, "bad host output / slab_rows");
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t esz = dtype_size(out_dtype);
+  slab_rows = std::min<int64_t>(slab_rows, n);
+  const size_t sb = (size_t)slab_rows * (size_t)n * esz;
+  KMG_TRY(c->slabs.ensure(2 * sb));
+  if (!c->d2h_stream) {
+    KMG_HIP(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      KMG_HIP(hipEventCreateWithFlags(&c->ev_slab[b], hipEventDisableTiming));
+      KMG_HIP(hipEventCreateWithFlags(&c->ev_out[b], hipEventDisableTiming));
+    }
+  }
+  std::vector<RowRange> ranges;
+  for (int64_t r0 = 0, q = 0; r0 < n; r0 += slab_rows, ++q)
+    ranges.push_back(RowRange{r0, std::min(n, r0 + slab_rows), (char *)c->slabs.p + (q & 1) * sb, n});
+  // slab q's copy: on the d2h stream behind slab q's Gram, into host rows [r0, r1)
+  auto copy_out = [&](size_t q) -> int {
+    const RowRange &rg = ranges[q];
+    KMG_HIP(hipStreamWaitEvent(c->d2h_stream, c->ev_slab[q & 1], 0));
+    KMG_HIP(hipMemcpy2DAsync((char *)h_out + (size_t)rg.row0 * ld_host * esz, (size_t)ld_host * esz,
+                             rg.out, (size_t)n * esz, (size_t)n * esz, (size_t)(rg.row1 - rg.row0),
+                             hipMemcpyDeviceToHost, c->d2h_stream));
+    KMG_HIP(hipEventRecord(c->ev_out[q & 1], c->d2h_stream));
+    return KMG_OK;
+  };
+  // after slab q's Gram is enqueued: copy slab q - 1 out (overlapping slab q's Gram), and
+  // hold slab q + 1's Gram (same buffer as q - 1) until that copy has landed
+  AfterRange after = [&](size_t q) -> int {
+    KMG_HIP(hipEventRecord(c->ev_slab[q & 1], c->stream));
+    if (q >= 1) {
+      KMG_TRY(copy_out(q - 1));
+      KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_out[(q - 1) & 1], 0));
+    }
+    return KMG_OK;
+  };
+  KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, n, after));
+  KMG_TRY(copy_out(ranges.size() - 1));
+  KMG_HIP(hipStreamSynchronize(c->d2h_stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
 }
 
 int kmg_reload_tuning(kmg_ctx *c) {

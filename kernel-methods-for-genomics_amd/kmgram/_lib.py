@@ -33,6 +33,7 @@ EXPORTS = (
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
+    "kmg_gram_to_host",
 )
 
 
@@ -109,6 +110,8 @@ def load():
             "kmg_gram_blocks": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64, I32,
                                  I32, I64, I32], ctypes.c_int),
             "kmg_reload_tuning": ([P], ctypes.c_int),
+            "kmg_gram_to_host": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, I64, P,
+                                  I64], ctypes.c_int),
             "kmg_combine": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
             "kmg_combine_device": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
             "kmg_nlck_grad": ([P, P, I32, P, I32, P, I64, I64, P], ctypes.c_int),
@@ -205,6 +208,18 @@ class Context:
         check(self.lib.kmg_gram_blocks(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        out_dtype, d_out, ld, int(nranks), int(rank), int(block),
                                        g))
+
+    def gram_to_host(self, params, d_codes, d_lens, n, ldc, out_dtype, slab_rows, out):
+        """K of all n rows into the host array ``out`` (n x n, C-contiguous rows; a numpy
+        memmap works), built in device slabs of ``slab_rows`` rows with one index build and
+        each slab's copy overlapping the next slab's Gram.  Synchronous."""
+        if out.shape[0] < n or out.shape[1] < n or out.dtype != np.dtype(DTYPES[out_dtype]):
+            raise ValueError("gram_to_host: output shape / dtype")
+        if out.strides[1] != out.itemsize:
+            raise ValueError("gram_to_host: output rows must be contiguous")
+        check(self.lib.kmg_gram_to_host(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
+                                        out_dtype, int(slab_rows), out.ctypes.data,
+                                        out.strides[0] // out.itemsize))
 
     def reload_tuning(self):
         """Re-read the KMG_* environment knobs (read once at context creation)."""

@@ -11,9 +11,10 @@ At N >= 100k a float64 K is 80+ GB, so a pickle (one in-memory blob) no longer w
 Here:
   * ``read_csv_codes`` parses an ``Id,seq`` CSV straight into the symbol codes the C ABI
     takes (no DataFrame, no per-row Python strings kept);
-  * ``gram_to_npy`` builds K on the device in row slabs (``kmg_gram_device``) and streams
-    each slab into a ``.npy`` file opened with ``numpy.lib.format.open_memmap``, so host
-    memory holds one slab, not K;
+  * ``gram_to_npy`` builds K on the device in row slabs (``kmg_gram_to_host``: posting
+    index and diagonal built once, each slab's copy overlapping the next slab's Gram) and
+    streams them into a ``.npy`` file opened with ``numpy.lib.format.open_memmap``, so
+    host memory never holds K;
   * ``load_gram`` maps such a file read-only (``np.load(..., mmap_mode='r')``).
 The ``.npy`` file holds exactly the array ``select_method`` would return for SP / MM
 (float64, or int32 raw spectrum counts on request).
@@ -88,19 +89,18 @@ def gram_to_npy(path, codes, lens, method, out_dtype=L.KMG_F64, slab_rows=None, 
     out = np.lib.format.open_memmap(path, mode="w+", dtype=dt, shape=(n, n))
     own = ctx is None
     ctx = ctx or L.Context(0)
-    d_codes = d_lens = d_out = None
+    d_codes = d_lens = None
     try:
         d_codes, d_lens = ctx.dmalloc(max(1, codes.nbytes)), ctx.dmalloc(max(1, lens.nbytes))
         ctx.h2d(d_codes, codes)
         ctx.h2d(d_lens, lens)
-        d_out = ctx.dmalloc(max(1, slab_rows * n * dt.itemsize))
-        for r0 in range(0, n, slab_rows):
-            r1 = min(n, r0 + slab_rows)
-            ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, d_out, n)
-            ctx.d2h(out[r0:r1], d_out)
+        if n:
+            # one index / diagonal build for all slabs; slab t's copy into the memmap
+            # overlaps slab t+1's Gram (kmg_gram_to_host)
+            ctx.gram_to_host(params, d_codes, d_lens, n, ldc, out_dtype, slab_rows, out)
         out.flush()
     finally:
-        for p in (d_codes, d_lens, d_out):
+        for p in (d_codes, d_lens):
             if p is not None:
                 ctx.dfree(p)
         if own:

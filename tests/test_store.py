@@ -73,3 +73,25 @@ def test_gram_to_npy_mismatch_validation(ctx, tmp_path):
     codes[3, 7] = 9
     with pytest.raises(ValueError):
         store.gram_to_npy(tmp_path / "a.npy", codes, lens, "MM_k9_m1", ctx=ctx)
+
+
+@pytest.mark.gpu
+def test_gram_to_host_strided_output(ctx):
+    """kmg_gram_to_host into a host array whose rows are longer than n (ld_host > n): the
+    n x n block equals the one-call Gram, the columns past n stay untouched."""
+    from kmgram import params as P
+    codes, lens = E.synthetic(230, 101, seed=23)
+    n, ldc = codes.shape
+    params = P.make(L.KMG_SPECTRUM, k=8)
+    ref = ctx.gram(params, codes, lens, L.KMG_I32)
+    buf = np.full((n, n + 5), -7, dtype=np.int32)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_to_host(params, d_codes, d_lens, n, ldc, L.KMG_I32, 50, buf[:, :n])
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    assert np.array_equal(buf[:, :n], ref)
+    assert np.all(buf[:, n:] == -7)
