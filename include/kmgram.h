@@ -61,7 +61,9 @@ enum { KMG_I32 = 1, KMG_F32 = 2, KMG_F64 = 3 };
 
 /* semantics modes (kmg_params.la_mode; LA and GP) */
 enum { KMG_LA_REFERENCE = 0 /* bit-for-bit the reference: all zeros (kernels.py:238,262) */,
-       KMG_LA_INTENDED = 1  /* aliasing fixed, report §3.5 recurrence; parity unpinned */ };
+       KMG_LA_INTENDED = 1  /* five DP arrays (no aliasing), cells up to [n_x, n_y] on
+                               x[i-1], y[j-1], gap factors exp(-beta e) / exp(-beta d):
+                               kernels.py:226-270 as meant; parity unpinned */ };
 enum { KMG_MODE_REFERENCE = 0 /* the reference's behaviour (GP: k=1,g=0 only) */,
        KMG_MODE_INTENDED = 1  /* GP: binary (k-g)-mer presence over the gapped subsequences
                                  of every 101-window k-mer, normalised (kernels.py:420-455 as

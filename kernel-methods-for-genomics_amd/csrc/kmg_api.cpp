@@ -928,8 +928,33 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     }
     case KMG_LOCALALIGN: {
       if (dt == KMG_I32) return fail(KMG_EINVAL, "LA produces float64 values");
-      if (p->la_mode != KMG_LA_REFERENCE)
-        return fail(KMG_EUNSUPPORTED, "LA intended mode not built in this version");
+      if (p->la_mode == KMG_LA_INTENDED) {
+        // the recurrence the reference means (kernels.py:226-270 with its aliasing, loop
+        // bounds and gap signs fixed; gram_la_kernel): parity unpinned
+        if (!(p->la_beta > 0.0)) return fail(KMG_EINVAL, "LA: beta must be > 0");
+        if (maxlen > 1024) return fail(KMG_EUNSUPPORTED, "LA: sequences longer than 1024");
+        SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+        bool unsupported = false;
+        const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          const bool full = r0 == 0 && r1 == n;  // square: upper triangle + mirror
+          for (int64_t a = r0; a < r1; a += 65535) {
+            OutSpec os = oq;
+            os.out = (char *)oq.out + (size_t)(a - r0) * oq.ld * dtype_size(dt);
+            const int64_t b = std::min(r1, a + 65535);
+            hipError_t e = launch_gram_la(q, a, b, p->la_e, p->la_d, p->la_beta, p->smith,
+                                          full && b - a == n ? 1 : 0, os, c->stream);
+            if (e == hipErrorNotSupported) {
+              unsupported = true;
+              return hipSuccess;
+            }
+            if (e != hipSuccess) return e;
+          }
+          return hipSuccess;
+        });
+        if (unsupported) return fail(KMG_EUNSUPPORTED, "LA parameters");
+        return r;
+      }
+      if (p->la_mode != KMG_LA_REFERENCE) return fail(KMG_EINVAL, "LA: unknown la_mode");
       // The reference aliases M,X,Y,X2,Y2 to one array and never writes cell
       // [n_x, n_y] (kernels.py:238-240, 262-264): every entry is log(1+0)/beta = 0.
       return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {

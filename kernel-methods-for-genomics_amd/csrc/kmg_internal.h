@@ -225,6 +225,9 @@ hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, 
                            hipStream_t s);
 hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
                           double lam2, int mirror, const OutSpec &o, hipStream_t s);
+// LA kernel, intended semantics (KMG_LA_INTENDED): five-array affine-gap DP per pair
+hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
+                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int window,
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);

@@ -11,6 +11,8 @@
 // center_K (kernels.py:387-395).
 #include "kmg_internal.h"
 
+#include <cmath>
+
 namespace kmg {
 
 struct Coef {
@@ -514,6 +516,129 @@ __global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, i
     store_f(o, i - row0, j, result);
     if (mirror && j != i && j >= row0 && j < row1) store_f(o, j - row0, i, result);
   }
+}
+
+// ------------------------------------------------------------------ LA (intended)
+// Local-alignment kernel with the reference's three defects removed (KMG_LA_INTENDED;
+// oracle cpu_ref.la_intended_pair documents the semantics; parity unpinned): five DP
+// arrays, cells (r, c) for r in 1..n_x, c in 1..n_y on x[r-1], y[c-1], gap opening factor
+// exp(-beta e) and extension exp(-beta d).  One wave per pair (x = row min(i, j), y = row
+// max(i, j): the reference's j >= i fill, kernels.py:293-297), the SS kernel's
+// anti-diagonal sweep: lane l of a 64-row strip owns row r = s0 + l and at step st
+// computes column c = st - l; its left neighbour is its own previous cell, "up" comes
+// from lane l - 1 by a shuffle (lane 0: the previous strip's last row, kept in LDS), the
+// diagonal is the previous step's "up".  Every cell is evaluated in the oracle's order
+// with separately rounded products (no FMA): bit-identical sums, the final log within
+// an ulp of libm's.
+struct LaCoef {
+  double es[16];   // exp(beta * S[a][b]), a * 4 + b (kernels.py:223)
+  double eo, ee;   // exp(-beta e), exp(-beta d)
+  double inv_beta; // 1 / beta (the reference's (1/beta) * log(...))
+};
+
+template <bool SMITH>
+__global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, int64_t row1,
+                                                      LaCoef cf, int mirror, OutSpec o) {
+  extern __shared__ __align__(16) double lsm[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = row0 + blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 4 + wave;
+  if (j >= q.n || i >= row1) return;
+  if (mirror && j < i) return;
+  const int ML = q.maxlen;
+  // per wave: rowbuf[4][ML + 1] (M, X, Y, X2 of the strip's last row), result slot, y bytes
+  const int per = 4 * (ML + 1) + 1 + (ML + 8) / 8;
+  double *rowbuf = lsm + (size_t)wave * per;
+  double *res = rowbuf + 4 * (ML + 1);
+  uint8_t *yb = (uint8_t *)(res + 1);
+  const int64_t ia = min(i, j), ib = max(i, j);
+  const uint8_t *xs = q.codes + ia * q.ldc;
+  const uint8_t *ys = q.codes + ib * q.ldc;
+  const int nx = q.lens[ia], ny = q.lens[ib];
+  for (int c = lane; c < ny; c += 64) yb[c] = ys[c];
+  if (lane == 0) *res = 1.0;  // n_x or n_y == 0: cell [n_x, n_y] is the zero boundary
+  __builtin_amdgcn_wave_barrier();
+  const double eo = cf.eo, ee = cf.ee;
+  for (int s0 = 0; s0 <= nx; s0 += 64) {
+    const int r = s0 + lane;
+    const bool live = r <= nx;
+    const uint32_t xr = (r >= 1 && live) ? xs[r - 1] : 0u;
+    // left (own previous cell) and diagonal values; row 0 / column 0 are zero
+    double lM = 0.0, lX = 0.0, lY = 0.0, lX2 = 0.0, lY2 = 0.0;
+    double dM = 0.0, dX = 0.0, dY = 0.0;
+    const bool store_row = (lane == 63) && (s0 + 64 <= nx);
+    for (int st = 0; st <= ny + 63; ++st) {
+      const int c = st - lane;
+      double uM = __shfl_up(lM, 1, 64), uX = __shfl_up(lX, 1, 64);
+      double uY = __shfl_up(lY, 1, 64), uX2 = __shfl_up(lX2, 1, 64);
+      if (lane == 0) {
+        const bool rb = s0 > 0 && c >= 0 && c <= ny;
+        uM = rb ? rowbuf[c] : 0.0;
+        uX = rb ? rowbuf[(ML + 1) + c] : 0.0;
+        uY = rb ? rowbuf[2 * (ML + 1) + c] : 0.0;
+        uX2 = rb ? rowbuf[3 * (ML + 1) + c] : 0.0;
+      }
+      if (live && c >= 0 && c <= ny) {
+        double M = 0.0, X = 0.0, Y = 0.0, X2 = 0.0, Y2 = 0.0;
+        if (r >= 1 && c >= 1) {
+          const double sub = cf.es[xr * 4 + yb[c - 1]];
+          if (SMITH) {
+            M = __dmul_rn(sub, fmax(fmax(fmax(1.0, dX), dY), dM));
+            X = fmax(__dmul_rn(eo, uM), __dmul_rn(ee, uX));
+            Y = fmax(fmax(__dmul_rn(eo, lM), __dmul_rn(eo, lX)), __dmul_rn(ee, lY));
+            X2 = fmax(uM, uX2);
+            Y2 = fmax(fmax(lM, lX2), lY2);
+          } else {
+            M = __dmul_rn(sub, __dadd_rn(__dadd_rn(__dadd_rn(1.0, dX), dY), dM));
+            X = __dadd_rn(__dmul_rn(eo, uM), __dmul_rn(ee, uX));
+            Y = __dadd_rn(__dmul_rn(eo, __dadd_rn(lM, lX)), __dmul_rn(ee, lY));
+            X2 = __dadd_rn(uM, uX2);
+            Y2 = __dadd_rn(__dadd_rn(lM, lX2), lY2);
+          }
+        }
+        dM = uM; dX = uX; dY = uY;
+        lM = M; lX = X; lY = Y; lX2 = X2; lY2 = Y2;
+        if (store_row) {
+          rowbuf[c] = M;
+          rowbuf[(ML + 1) + c] = X;
+          rowbuf[2 * (ML + 1) + c] = Y;
+          rowbuf[3 * (ML + 1) + c] = X2;
+        }
+        if (r == nx && c == ny && r >= 1 && c >= 1)
+          *res = SMITH ? fmax(fmax(fmax(1.0, X2), Y2), M)
+                       : __dadd_rn(__dadd_rn(__dadd_rn(1.0, X2), Y2), M);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    const double result = __dmul_rn(cf.inv_beta, log(*res));
+    store_f(o, i - row0, j, result);
+    if (mirror && j != i && j >= row0 && j < row1) store_f(o, j - row0, i, result);
+  }
+}
+
+hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
+                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || q.n == 0) return hipSuccess;
+  const int ML = q.maxlen;
+  const size_t lds = (size_t)4 * (4 * (ML + 1) + 1 + (ML + 8) / 8) * sizeof(double);
+  if (lds > 160 * 1024 || rows > 65535) return hipErrorNotSupported;
+  static const int S[4][4] = {{4, 0, 0, 0}, {0, 9, -3, -1}, {0, -3, 6, 2}, {0, -1, -2, 5}};
+  LaCoef cf;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b) cf.es[a * 4 + b] = std::exp(beta * (double)S[a][b]);
+  cf.eo = std::exp(-beta * e);
+  cf.ee = std::exp(-beta * d);
+  cf.inv_beta = 1.0 / beta;
+  const dim3 grid((unsigned)((q.n + 3) / 4), (unsigned)rows);
+  if (smith)
+    hipLaunchKernelGGL((gram_la_kernel<true>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
+  else
+    hipLaunchKernelGGL((gram_la_kernel<false>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ GP (k=1, g=0)

@@ -128,12 +128,25 @@ class GramEngine:
         """get_string_K (kernels.py:367-382)."""
         return self._run(P.make(L.KMG_SUBSTRING, k=int(k), lbda=lbda), seqs)
 
-    def local_alignment(self, seqs, e=11, d=1, beta=0.5, smith=0, eig=1):
+    def local_alignment(self, seqs, e=11, d=1, beta=0.5, smith=0, eig=1, intended=False):
         """get_LA_K (kernels.py:273-302), reference semantics (the reference
-        always returns an all-zero K, and raises ArpackError for eig=1, n >= 8)."""
+        always returns an all-zero K, and raises ArpackError for eig=1, n >= 8).
+
+        intended=True: the local-alignment kernel the reference means — five DP arrays
+        instead of one aliased array, every cell up to [n_x, n_y], gap opening / extension
+        factors exp(-beta e) / exp(-beta d) (g(n) = e + d(n-1), the docstring's affine
+        gap) — computed on the device (gram_la_kernel; parity unpinned: the reference
+        never produces it).  Like the reference, K itself is returned (its eig step only
+        builds K1, kernels.py:288-302)."""
         seqs = list(seqs)
         self._require_acgt(seqs)
         n = len(seqs)
+        if intended:
+            if not beta > 0:
+                raise ValueError("LA kernel needs beta > 0")
+            p = P.make(L.KMG_LOCALALIGN, smith=int(smith), la_mode=L.KMG_LA_INTENDED,
+                       la_e=e, la_d=d, la_beta=beta)
+            return self._run(p, seqs)
         if eig == 1 and n >= 8:
             # eigs(K1) on the all-zero K: ARPACK info=-9 (kernels.py:294)
             from scipy.sparse.linalg import ArpackError

@@ -262,6 +262,63 @@ def local_alignment_reference(n):
     return np.zeros((n, n))
 
 
+# substitution matrix of the LA kernel (kernels.py:223, rows/columns A, C, G, T)
+LA_S = np.array([[4, 0, 0, 0], [0, 9, -3, -1], [0, -3, 6, 2], [0, -1, -2, 5]])
+
+
+def la_intended_pair(x, y, e, d, beta, smith):
+    """The LA kernel value the reference means (affine_align / Smith_Waterman,
+    kernels.py:226-270) with its three defects removed — parity unpinned, the reference
+    never produces it:
+      * M, X, Y, X2, Y2 are five arrays (the reference aliases one, kernels.py:238, 262);
+      * cells (i, j) for i in 1..n_x, j in 1..n_y read x[i-1], y[j-1] (the reference's
+        range(1, n) never reaches [n_x, n_y] and skips x[0]);
+      * gaps cost what the docstring says, g(n) = e + d(n-1) with e the opening and d the
+        extension penalty: opening factor exp(-beta e), extension exp(-beta d) (the
+        reference multiplies by exp(+beta d) and exp(+beta e)).
+    Same recurrences and the same evaluation order otherwise (sum form, or max for
+    smith=1); returns (1/beta) log(1 + X2 + Y2 + M) at [n_x, n_y].  Pure Python floats
+    (IEEE double, no fused multiply-add), small cases only."""
+    import math  # libm exp / log (the device path computes its table with the same libm)
+    es = [[math.exp(beta * float(v)) for v in row] for row in LA_S]
+    eo, ee = math.exp(-beta * e), math.exp(-beta * d)
+    nx, ny = len(x), len(y)
+    z = [0.0] * (ny + 1)
+    M, X, Y, X2, Y2 = list(z), list(z), list(z), list(z), list(z)  # row i-1
+    for i in range(1, nx + 1):
+        m, xx, yy, x2, y2 = [0.0], [0.0], [0.0], [0.0], [0.0]  # row i, column 0
+        xi = int(x[i - 1])
+        for j in range(1, ny + 1):
+            sub = es[xi][int(y[j - 1])]
+            if smith:
+                m.append(sub * max(1.0, X[j - 1], Y[j - 1], M[j - 1]))
+                xx.append(max(eo * M[j], ee * X[j]))
+                yy.append(max(eo * m[j - 1], eo * xx[j - 1], ee * yy[j - 1]))
+                x2.append(max(M[j], X2[j]))
+                y2.append(max(m[j - 1], x2[j - 1], y2[j - 1]))
+            else:
+                m.append(sub * (1.0 + X[j - 1] + Y[j - 1] + M[j - 1]))
+                xx.append(eo * M[j] + ee * X[j])
+                yy.append(eo * (m[j - 1] + xx[j - 1]) + ee * yy[j - 1])
+                x2.append(M[j] + X2[j])
+                y2.append(m[j - 1] + x2[j - 1] + y2[j - 1])
+        M, X, Y, X2, Y2 = m, xx, yy, x2, y2
+    v = max(1.0, X2[ny], Y2[ny], M[ny]) if smith else 1.0 + X2[ny] + Y2[ny] + M[ny]
+    return (1 / beta) * math.log(v)
+
+
+def la_intended(codes, lens, e=11, d=1, beta=0.5, smith=0):
+    """get_LA_K with the intended recurrence: K[i, j] = K[j, i] = la_intended_pair(x_i,
+    x_j) for j >= i (the reference's fill order, kernels.py:293-297)."""
+    seqs = _codes_list(codes, lens)
+    n = len(seqs)
+    K = np.zeros((n, n))
+    for i in range(n):
+        for j in range(i, n):
+            K[i, j] = K[j, i] = la_intended_pair(seqs[i], seqs[j], e, d, beta, smith)
+    return K
+
+
 def gappy_k1g0(codes, lens, window=101):
     """get_gappy_K(X, 1, 0): phi_c = [letter c occurs in x[:window]] (kernels.py:420-433)."""
     seqs = _codes_list(codes, lens)
