@@ -322,6 +322,54 @@ __global__ __launch_bounds__(FINE_THREADS) void part_gather_kernel(
     total += red[0][w];
     base += red[1][w];
   }
+  // Few blocks (nblk <= SEGR waves' worth, e.g. 250 at N=20000): every wave loads the
+  // first 64 items of all its segments at once and keeps them in registers across the
+  // scan, so both passes cost one L2 round trip (the loop below pays one per SEGU
+  // segments and loads every item twice).  Longer segments finish in remainder loops.
+  constexpr int SEGR = 16;
+  if (nblk <= SEGR * nw) {
+    uint32_t it[SEGR];
+#pragma unroll
+    for (int u = 0; u < SEGR; ++u) {
+      const int q = wave + u * nw;
+      it[u] = (q < nblk && (uint32_t)lane < cnt[q]) ? tmp[(size_t)q * cap + src[q] + lane] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < SEGR; ++u)
+      if (it[u] != 0xFFFFFFFFu) atomicAdd(&fh[it[u] >> 16], 1u);
+    for (int q = wave; q < nblk; q += nw) {
+      const uint32_t c = cnt[q];
+      const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+      for (uint32_t x = 64 + lane; x < c; x += 64) atomicAdd(&fh[sp[x] >> 16], 1u);
+    }
+    __syncthreads();
+    lds_excl_scan(fh, nf, wtmp);
+    const int64_t nb = g.nbins();
+    const int64_t bin0 = (int64_t)b << fb;
+    for (int f = threadIdx.x; f < nf; f += blockDim.x) {
+      const int64_t bin = bin0 + f;
+      if (bin < nb) off[bin] = base + fh[f];
+    }
+    if (b == (int)gridDim.x - 1 && threadIdx.x == 0) off[nb] = base + total;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SEGR; ++u) {
+      if (it[u] != 0xFFFFFFFFu) {
+        const uint32_t pos = atomicAdd(&fh[it[u] >> 16], 1u);
+        ent[base + pos] = (uint16_t)(it[u] & 0xFFFFu);
+      }
+    }
+    for (int q = wave; q < nblk; q += nw) {
+      const uint32_t c = cnt[q];
+      const uint32_t *sp = tmp + (size_t)q * cap + src[q];
+      for (uint32_t x = 64 + lane; x < c; x += 64) {
+        const uint32_t v = sp[x];
+        const uint32_t pos = atomicAdd(&fh[v >> 16], 1u);
+        ent[base + pos] = (uint16_t)(v & 0xFFFFu);
+      }
+    }
+    return;
+  }
   // the segments of a bucket are short (~30 items at N=20000): a wave loads the first 64
   // items of SEGU segments before using any, so the pass is not one L2 round trip per
   // segment; longer segments finish in the remainder loop
