@@ -1,24 +1,26 @@
 #!/usr/bin/env python3
 """bench.py — Gram pairs/s of the MI355X string-kernel Gram engine.
 
-Workload (BASELINE.json configs[1]): spectrum k=8 Gram of N=20000 synthetic DNA
-sequences of length L=101, int32 exact counts, device-resident (input codes already in
-HBM when the timed region starts).  A "step" is one full-K build (SURVEY §8d t_build):
+Workload (BASELINE.json configs[3], the north_star's target: "≥100× the reference CPU Gram
+build at N=100k, L=101, spectrum k=8 on one MI355X"): spectrum k=8 Gram of N=100000
+synthetic DNA sequences of length L=101, int32 exact counts (40 GB), device-resident (input
+codes already in HBM when the timed region starts); posting-list formulation (DESIGN.md §4
+on the configs[3] "count-vector GEMM" wording).  A "step" is one full-K build (SURVEY §8d t_build):
 2-bit packing + posting-index build + Gram kernel, and with G > 1 GPUs the RCCL
 all-gather that leaves the complete K on every GPU.
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`): one
-process per GPU, the SAME N=20000 problem (strong scaling), rows dealt block-cyclically
+process per GPU, the SAME N=100000 problem (strong scaling), rows dealt block-cyclically
 (kmg_gram_blocks): every rank builds the replicated index, computes its row blocks, and
 each round of G blocks is all-gathered in place over RCCL/xGMI on a second stream while
 the next round is computed (default: only the round's upper-triangle slab travels and every
 GPU mirrors it locally; --gather-mode 1 sends full rows).  `value` = N^2 / max-over-ranks step time including that
 all-gather; `collective_free` reports the same build without it.
 
-Also reported: the mismatch (k=9, m=1) Gram at the same N (BASELINE configs[2], float64
+Also reported: the mismatch (k=9, m=1) Gram at N=20000 (BASELINE configs[2], float64
 normalised), per-stage device times from HIP events, the HBM roofline of the dominant
-kernel, the oracle timed on the host cores (cpu_baseline), and (N=1) BASELINE configs[3]
-and [4], the drop-in host path, run.py's nine kernels at N=9000 and the downstream
+kernel, the oracle timed on the host cores (cpu_baseline), and (N=1) BASELINE configs[1]
+(N=20000 spectrum) and [4], the drop-in host path, run.py's nine kernels at N=9000 and the downstream
 consumers.  At G > 1 the config[4] strong-scaling line (N=200000, raw int32 K gathered)
 is added.
 """
@@ -220,9 +222,12 @@ _F = _FT = None
 
 
 def _rows_product(ab):
+    """Rows [a, b) of Phi Phi^T as dense float64 rows (what the reference materialises), in
+    sub-blocks of 256 rows so a worker holds at most 256 x N doubles (0.2 GB at N=100000)."""
     a, b = ab
     t0 = time.perf_counter()
-    (_F[a:b] @ _FT).toarray()
+    for s in range(a, b, 256):
+        (_F[s:min(b, s + 256)] @ _FT).toarray()
     return time.perf_counter() - t0
 
 
@@ -332,18 +337,15 @@ def extras(ctx, cpu_rates, steps4):
     sp = lambda c, l, r: cref.spectrum(c, l, 8, rows=(r, r + 1))[0]  # noqa: E731
     mmr = lambda c, l, r: cref.mismatch_raw(c, l, 9, 1, rows=(r, r + 1))[0]  # noqa: E731
     mm = lambda c, l, r: cref.mismatch_rows(c, l, 9, 1, rows=(r, r + 1))[0]  # noqa: E731
-    n4 = 100000
-    c4 = run_slab(ctx, P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n4, 4, 0, n4, steps4, 2,
-                  (0, 54321, n4 - 1), sp)
-    c4["workload"] = ("BASELINE configs[3]: spectrum k=8, N=100000 x L=101, full K on 1 GPU, "
-                      "int32 (40 GB), posting-list formulation (DESIGN.md §6: why not the "
-                      "count-vector fp32 GEMM)")
-    c4["gram_hbm_frac"] = (4.0 * n4 * n4 + 52.0 * n4) / (c4["stages_ms"]["gram"] / 1e3) / HBM_PEAK
-    c4["reference_model_s"] = reference_model_s("spectrum_k8", n4)
-    c4["speedup_vs_reference_model"] = c4["reference_model_s"] / (c4["ms_per_step"] / 1e3)
-    if cpu_rates.get("spectrum_k8"):
-        c4["speedup_vs_cpu_baseline"] = c4["pairs_per_s"] / cpu_rates["spectrum_k8"]
-    out["config4_spectrum_k8_n100000"] = c4
+    n2 = 20000
+    c2 = run_slab(ctx, P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n2, 2, 0, n2, steps4, 3,
+                  (0, 12345, n2 - 1), sp)
+    c2["workload"] = ("BASELINE configs[1]: spectrum k=8, N=20000 x L=101, full K on 1 GPU, "
+                      "int32 (1.6 GB), bit-exact spot rows")
+    c2["gram_hbm_frac"] = (4.0 * n2 * n2 + 52.0 * n2) / (c2["stages_ms"]["gram"] / 1e3) / HBM_PEAK
+    c2["reference_model_s"] = reference_model_s("spectrum_k8", n2)
+    c2["speedup_vs_reference_model"] = c2["reference_model_s"] / (c2["ms_per_step"] / 1e3)
+    out["config2_spectrum_k8_n20000"] = c2
     n5 = 200000
     c5 = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64, n5,
                   5, 0, n5 // 8, 2, 1, (0, n5 // 8 - 1), mm)
@@ -508,8 +510,9 @@ def downstream(ctx):
     return out
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from the committed PMC pass (profiles/*pmc*.json), if any."""
+def load_traffic(workload, n):
+    """HBM bytes per launch from the committed PMC pass of this workload at this N
+    (profiles/*pmc*.json, written by profiles/pmc_summary.py), if any."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -517,7 +520,7 @@ def load_traffic(workload):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+        if d.get("workload") == workload and d.get("N") == n and d.get("hbm_bytes_per_launch"):
             best = d["hbm_bytes_per_launch"]
     return best
 
@@ -548,7 +551,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--n", type=int, default=100000, help="spectrum N (headline)")
+    ap.add_argument("--mm-n", type=int, default=20000, help="mismatch N (secondary)")
     ap.add_argument("--gather-mode", type=int, default=2, choices=(1, 2),
                     help="G > 1 assembly: 2 upper-triangle slabs + mirror, 1 full rows")
     ap.add_argument("--no-cpu", action="store_true")
@@ -575,13 +579,13 @@ def main():
         ctx.comm_init(uid, dist.world, dist.rank)
     n = args.n
 
-    sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n, 2,
-                   args.steps, args.warmup, check_spectrum)
+    sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
+                   4 if n == 100000 else 2, args.steps, args.warmup, check_spectrum)
     mm = None
     if not args.no_mismatch:
         mm = run_build(ctx, dist, "mismatch_k9_m1",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
-                       n, 3, max(3, args.steps // 4), 1, check_mismatch)
+                       args.mm_n, 3, max(3, args.steps // 4), 1, check_mismatch)
     c5 = None
     if dist.world > 1 and not args.no_extra:
         # config-5 strong scaling: the full 200000^2 raw int32 K (160 GB) on every GPU
@@ -592,10 +596,10 @@ def main():
     if dist.world == 1 and not args.no_cpu:
         cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
         if mm:
-            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", n, args.cpu_budget / 2)
+            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", args.mm_n, args.cpu_budget / 2)
     extra = None
     if dist.world == 1 and not args.no_extra:
-        extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(10, args.steps // 2))
+        extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(20, args.steps))
     if dist.world > 1:
         ctx.comm_destroy()
     ctx.close()
@@ -608,8 +612,9 @@ def main():
     kern_s = st["gram"] / 1e3
     achieved = alg_bytes / kern_s
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK, "traffic": load_traffic("spectrum_k8"),
-            "kernel": "kmg::gram_sp_kernel<true,1,false>", "kernel_ms": st["gram"],
+            "frac": achieved / HBM_PEAK, "traffic": load_traffic("spectrum_k8", n),
+            "kernel": "kmg::gram_sp_kernel<true,1,%s>" % ("true" if n > 24576 else "false"),
+            "kernel_ms": st["gram"],
             "alg_bytes_per_launch": alg_bytes,
             "measured_write_ceiling_GBps": sp.get("write_ceiling_GBps"),
             "frac_of_measured_ceiling": (achieved / 1e9 / sp["write_ceiling_GBps"]
@@ -621,11 +626,12 @@ def main():
         "ms_per_step": sp["ms_per_step"], "higher_is_better": True,
         "scaling": "strong",  # fixed N at every G (SURVEY §8d t_build incl. all-gather)
         "vs_baseline": None, "dtype": "int32",
-        "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(2)",
-        "config": {"workload": "spectrum k=8 full-K build, N=20000 x L=101 (BASELINE "
-                               "configs[1]); G>1: same N, block-cyclic rows, upper-triangle "
-                               "round slabs all-gathered in place over RCCL + local mirror, so "
-                               "every GPU ends with K",
+        "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(%d)" % (4 if n == 100000 else 2),
+        "config": {"workload": "spectrum k=8 full-K build, N=%d x L=101 (BASELINE configs[%d]%s); "
+                               "G>1: same N, block-cyclic rows, upper-triangle uint16 round slabs "
+                               "all-gathered in place over RCCL + local unpack/mirror, so every "
+                               "GPU ends with K" % (n, 3 if n == 100000 else 1,
+                                                    ", the north_star's target config" if n == 100000 else ""),
                    "N": n, "L": 101, "k": 8, "rows_this_rank": sp["rows_this_rank"],
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
@@ -636,10 +642,10 @@ def main():
         line["gather_roofline"] = gather_roofline(sp, dist.world, 4)
     if mm:
         mm_rows_launch = mm["rows_this_rank"] / max(1, mm["rounds"])
-        mm_bytes = 8.0 * mm_rows_launch * n + 52.0 * n
+        mm_bytes = 8.0 * mm_rows_launch * args.mm_n + 52.0 * args.mm_n
         line["secondary"] = {
             "workload": "mismatch (k=9,m=1) full-K build, float64 normalised (BASELINE configs[2])",
-            "N": n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
+            "N": args.mm_n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
             "hbm_frac_of_gram_kernel": mm_bytes / (mm["stages_ms"]["gram"] / 1e3) / HBM_PEAK,
             # the kernel's real bound: one random 128-B slot line per posting list, 117 lists
@@ -668,6 +674,7 @@ def main():
         line["cpu_baseline_one_process"] = cpu["spectrum_k8"]["one_process"]
         line["reference_model"] = {
             "s": reference_model_s("spectrum_k8", n),
+            "speedup_vs_model": reference_model_s("spectrum_k8", n) / (sp["ms_per_step"] / 1e3),
             "note": "reference kernels.py cost model (BASELINE.md), survey container 8-core Xeon"}
         if mm:
             line["secondary"]["cpu_baseline"] = cpu["mismatch_k9_m1"]

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output for the committed profiles/ evidence.
 
-usage: python profiles/pmc_summary.py <prof_dir> <tag>
+usage: python profiles/pmc_summary.py <prof_dir> <tag> [N (default 100000)]
   <prof_dir>/trace/run_kernel_stats.csv          (--kernel-trace --stats)
   <prof_dir>/pmc_fetch/run_counter_collection.csv (--pmc FETCH_SIZE, own pass)
   <prof_dir>/pmc_write/run_counter_collection.csv (--pmc WRITE_SIZE, own pass)
@@ -38,6 +38,7 @@ def short(name):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 100000  # the bench's spectrum N
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(HERE, f"{tag}_kernel_stats.csv"))
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
@@ -52,7 +53,7 @@ def main():
         kernels[short(k)] = {"fetch_bytes_raw": fk, "fetch_bytes_x2": 2 * fk, "write_bytes": wk,
                              "hbm_bytes_est": 2 * fk + wk, "avg_ns": stats.get(short(k))}
     gram = next((v for k, v in kernels.items() if "gram_sp_kernel" in k), None)
-    out = {"tag": tag, "workload": "spectrum_k8", "kernels": kernels,
+    out = {"tag": tag, "workload": "spectrum_k8", "N": n, "kernels": kernels,
            "hbm_bytes_per_launch": gram["hbm_bytes_est"] if gram else None}
     with open(os.path.join(HERE, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
