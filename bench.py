@@ -154,7 +154,8 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
             return wall / k, stages
 
         t, stages = timed(gather, steps)
-        res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages})
+        res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages,
+                    "wire_bytes": ctx.blocks_wire()})
         if gather:
             tcf, scf = timed(0, steps)
             res["collective_free"] = {"ms_per_step": tcf * 1e3, "pairs_per_s": n * n / tcf,
@@ -533,8 +534,8 @@ def gather_roofline(res, world, esz):
         return None
     n = res["N"]
     npad = rows_padded(n, world, res["block_rows"])
-    if res.get("gather_mode") == 2:  # upper-triangle round slabs, raw uint16 counts
-        esz = 2  # (posting-list kernels; a mismatch count past 65535 redoes with 32 bits)
+    if res.get("gather_mode") == 2:  # upper-triangle round slabs of raw 8/16-bit counts
+        esz = res.get("wire_bytes") or esz  # (kmg_gram_blocks_wire: what actually travelled)
         r = world * res["block_rows"]
         recv = (world - 1) / world * sum(r * w for _, w in triangle_rounds(n, world, res["block_rows"])) * esz
     else:

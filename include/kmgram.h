@@ -220,6 +220,9 @@ int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block);
 int kmg_gram_blocks(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype, void *d_out,
                     int64_t ld_out, int32_t nranks, int32_t rank, int64_t block, int32_t gather);
+/* Bytes per slab element the last kmg_gram_blocks call sent over the all-gather (gather 2/3:
+ * 1 = uint8 counts, 2 = uint16, else the output dtype's size; gather 0/1: the output's). */
+int kmg_gram_blocks_wire(kmg_ctx *ctx);
 
 /* Re-read the KMG_* tuning variables of the environment (read once at kmg_create). */
 int kmg_reload_tuning(kmg_ctx *ctx);

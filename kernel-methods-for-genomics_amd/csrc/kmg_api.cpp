@@ -184,6 +184,7 @@ struct kmg_ctx {
   hipEvent_t ev_tri[2] = {nullptr, nullptr};  // upper-triangle slabs released by their mirror
   hipStream_t unpack_stream = nullptr;          // upper triangle over RCCL: unpack of round t
   hipEvent_t ev_gath[2] = {nullptr, nullptr};   // overlaps the all-gather of round t + 1
+  int last_wire_bytes = 0;                      // slab element bytes of the last blocks call
   int nranks = 1, rank = 0;
 };
 
@@ -214,7 +215,7 @@ struct StageTimer {
   }
 };
 
-size_t dtype_size(int32_t dt) { return dt == KMG_F64 ? 8 : dt == KMG_U16 ? 2 : 4; }
+size_t dtype_size(int32_t dt) { return dt == KMG_F64 ? 8 : dt == KMG_U16 ? 2 : dt == KMG_U8 ? 1 : 4; }
 
 int64_t pow4(int e) { return (int64_t)1 << (2 * e); }
 
@@ -693,10 +694,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
   for (const RowRange &r : ranges)
     if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
   if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
-  if (dt == KMG_U16 && p->kind != KMG_SPECTRUM && p->kind != KMG_MISMATCH)
-    return fail(KMG_EINVAL, "internal: 16-bit slabs need a posting-list formulation");
+  const bool narrow = dt == KMG_U16 || dt == KMG_U8;
+  if (narrow && p->kind != KMG_SPECTRUM && p->kind != KMG_MISMATCH)
+    return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
   OutSpec o{nullptr, ld, dt, 0, nullptr, nullptr};
-  if (dt == KMG_U16) {  // raw 16-bit slabs: counts above 65535 raise this flag
+  if (narrow) {  // raw 8/16-bit slabs: counts past the slab's range raise this flag
     KMG_TRY(c->ovf.ensure(sizeof(uint32_t)));
     KMG_HIP(hipMemsetAsync(c->ovf.p, 0, sizeof(uint32_t), c->stream));
     o.ovf = c->ovf.as<uint32_t>();
@@ -746,8 +748,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (dense && !(k <= 8 && g.pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096))
         return fail(KMG_EUNSUPPORTED, "dense formulation needs k <= 8 and <= 127 windows");
       // raw 16-bit round slabs (kmg_gram_blocks) only from the posting-list kernels
-      if (dt == KMG_U16 && (path == SM_DENSE || path == SM_HAMMING || (exact && g.pmax > 255)))
-        return fail(KMG_EINVAL, "internal: 16-bit slabs need a posting-list formulation");
+      if ((dt == KMG_U16 || dt == KMG_U8) &&
+          (path == SM_DENSE || path == SM_HAMMING || (exact && g.pmax > 255)))
+        return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
       if (dense)
         return gram_dense(c, k, mm_eff, mm ? g.window : 0, d_codes, d_lens, n, ldc, ranges, o,
                           mm && p->normalize, after);
@@ -825,12 +828,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                    c->pr_rbase.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
                                    c->pr_lines.as<uint4>(), c->stream));
         }
-        if (p->normalize) {
+        if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));
           KMG_TRY(diag_hamming(c, g, pkd));
-          o.normalize = 1;
-          o.diagv = c->diagv.as<double>();
-          o.dsq = c->dsq.as<double>();
+          if (p->normalize) {
+            o.normalize = 1;
+            o.diagv = c->diagv.as<double>();
+            o.dsq = c->dsq.as<double>();
+          }
         }
         return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_pairs(pg, g, pkd, c->pr_summary.as<uint32_t>(),
@@ -856,12 +861,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_HIP(launch_slot_pack(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                  c->slots.as<uint4>(), c->stream));
       }
-      if (p->normalize) {
+      if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
         KMG_TRY(upload_wtab(c, w));
         KMG_TRY(diag_hamming(c, g, pkd));
-        o.normalize = 1;
-        o.diagv = c->diagv.as<double>();
-        o.dsq = c->dsq.as<double>();
+        if (p->normalize) {
+          o.normalize = 1;
+          o.diagv = c->diagv.as<double>();
+          o.dsq = c->dsq.as<double>();
+        }
       }
       return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         return exact ? launch_gram_spectrum(g, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
@@ -1187,7 +1194,7 @@ constexpr int KMG_RETRY_WIDE = 1000;  // internal: a 16-bit slab overflowed, red
 int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
                      void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
-                     int32_t gather, bool allow16);
+                     int32_t gather, int narrow_bits);
 }  // namespace
 
 int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
@@ -1196,18 +1203,23 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
   KMG_TRY(check_params(p, n, ldc, out_dtype));
-  const int r = gram_blocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks,
-                                 rank, block, gather, true);
-  if (r != KMG_RETRY_WIDE) return r;
-  return gram_blocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks, rank,
-                          block, gather, false);
+  // round slabs as narrow as the counts allow: 8 bits, else 16, else the output dtype
+  int r = KMG_RETRY_WIDE;
+  for (int bits : {8, 16, 0}) {
+    r = gram_blocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks, rank,
+                         block, gather, bits);
+    if (r != KMG_RETRY_WIDE) break;
+  }
+  return r;
 }
+
+int kmg_gram_blocks_wire(kmg_ctx *c) { return c ? c->last_wire_bytes : 0; }
 
 namespace {
 int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
                      void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
-                     int32_t gather, bool allow16) {
+                     int32_t gather, int narrow_bits) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
   if (block < 1) return fail(KMG_EINVAL, "block < 1");
   if (gather < 0 || gather > 3) return fail(KMG_EINVAL, "gather must be 0..3");
@@ -1227,20 +1239,28 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   // checked, a count above 65535 sets a flag and the build is redone with 32-bit slabs):
   // half the xGMI bytes of an int32 K, a quarter of a float64 one; the unpack pass widens
   // (and normalises) them into K.
+  // Slabs as raw uint8 (diagonal left out; every rank computes K_ii itself) or uint16
+  // counts when a posting-list kernel builds them; a count past the slab's range sets a
+  // flag the ranks agree on, and the build is redone one width up (kmg_gram_blocks).
   int32_t wire = out_dtype;
   bool check16 = false;
-  if (gather >= 2 && allow16 && (p->kind == KMG_SPECTRUM || p->kind == KMG_MISMATCH) &&
+  if (gather >= 2 && narrow_bits && (p->kind == KMG_SPECTRUM || p->kind == KMG_MISMATCH) &&
       p->k >= 1 && p->k <= 16) {
     const bool mm = p->kind == KMG_MISMATCH;
     const int L = mm ? (p->window > 0 ? p->window : 101) : (int)ldc;  // gram_device's maxlen
     const int pmax = std::max(1, L - p->k + 1);
     const SmPath path = sm_path(c->tune, p, pmax);
+    // 8 bits only for spectrum-shaped counts: their off-diagonal entries stay far below 256
+    // unless sequences repeat k-mers, where mismatch counts of random 101-mers pass 255
+    // (a shared 12-mer already contributes 4 exact 9-mer windows x 28)
+    if (narrow_bits == 8 && path != SM_POSTING) return KMG_RETRY_WIDE;
     if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS) {
-      wire = KMG_U16;
-      check16 = path != SM_POSTING;
+      wire = narrow_bits == 8 ? KMG_U8 : KMG_U16;
+      check16 = wire == KMG_U8 || path != SM_POSTING;  // spectrum counts <= P^2 < 65536
     }
   }
   const size_t wsz = dtype_size(wire);
+  c->last_wire_bytes = (int)(gather >= 2 ? wsz : esz);
   if (rccl && !c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   if ((rccl || tri) && !c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
   // unpack (mirror) stream: its own stream over RCCL, so the unpack of round t overlaps the
@@ -1330,7 +1350,10 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
         KMG_HIP(hipEventRecord(c->ev_gath[t & 1], c->comm_stream));
         KMG_HIP(hipStreamWaitEvent(post, c->ev_gath[t & 1], 0));
       }
-      if (wire == KMG_U16)
+      if (wire == KMG_U8)
+        KMG_HIP(launch_tri_unpack8((const uint8_t *)S, w, round, c0, n, d_out, ld_out, out_dtype,
+                                   p->normalize, c->diagv.as<double>(), c->dsq.as<double>(), post));
+      else if (wire == KMG_U16)
         KMG_HIP(launch_tri_unpack16((const uint16_t *)S, w, round, c0, n, d_out, ld_out, out_dtype,
                                     p->normalize, c->diagv.as<double>(), c->dsq.as<double>(), post));
       else

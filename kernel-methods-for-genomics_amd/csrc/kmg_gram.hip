@@ -116,6 +116,36 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
                                          int cw, const int32_t *acc, bool norm) {
   // columns below o.col_lo are not written; col_lo - col0 is a multiple of 8 (host check)
   const int qs = (int)max((int64_t)0, o.col_lo - col0);
+  if (o.dtype == KMG_U8) {
+    // raw off-diagonal counts as uint8 (the diagonal column is stored as 0: the unpack takes
+    // K_ii from the diagonal), 16 columns = 16 B per lane and step; an off-diagonal count
+    // above 255 is clipped and flagged (the caller redoes the build with 16-bit slabs)
+    uint8_t *prow = (uint8_t *)o.out + il * o.ld + col0;
+    bool big = false;
+    for (int q = qs + threadIdx.x * 16; q < cw; q += blockDim.x * 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        const uint32_t x = q + h < cw ? (uint32_t)acc[q + h] : 0u;
+        const bool dg = col0 + q + h == i;
+        big |= !dg && x > 0xFFu;
+        v[h] = dg ? 0u : min(x, 0xFFu);
+      }
+      uint8_t *d = prow + q;
+      if (q + 16 <= cw && (((uintptr_t)d) & 15) == 0) {
+        uint4 x;
+        x.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        x.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
+        x.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
+        x.w = v[12] | (v[13] << 8) | (v[14] << 16) | (v[15] << 24);
+        *(uint4 *)d = x;
+      } else {
+        for (int h = 0; h < 16 && q + h < cw; ++h) d[h] = (uint8_t)v[h];
+      }
+    }
+    if (big && o.ovf) atomicOr(o.ovf, 1u);
+    return;
+  }
   if (o.dtype == KMG_U16) {
     // raw counts as uint16 (multi-GPU round slabs; no normalisation here: the unpack pass
     // applies it), 8 columns = 16 B per lane and step; a count above 65535 is clipped and
@@ -282,7 +312,44 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
   const int qs = (int)max((int64_t)0, o.col_lo - col0);  // a multiple of 8 (host check)
-  if constexpr (DT == KMG_U16) {
+  if constexpr (DT == KMG_U8) {
+    // raw off-diagonal counts as uint8, diagonal column stored as 0 (see emit_row), 16
+    // columns = 16 B per lane and step from the packed 16-bit counters
+    static_assert(PACK16, "8-bit slabs need the packed accumulator");
+    uint8_t *prow = (uint8_t *)o.out + il * o.ld + col0;
+    bool big = false;
+    for (int q = qs + threadIdx.x * 16; q < cw; q += blockDim.x * 16) {
+      uint32_t v[16];
+      if (q + 16 <= cw) {
+        const uint4 a = *(const uint4 *)&acc[q >> 1], b = *(const uint4 *)&acc[(q >> 1) + 4];
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int h = 0; h < 16; ++h) v[h] = (w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+      } else {
+#pragma unroll
+        for (int h = 0; h < 16; ++h)
+          v[h] = q + h < cw ? (acc[(q + h) >> 1] >> (16 * ((q + h) & 1))) & 0xFFFFu : 0u;
+      }
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        const bool dg = col0 + q + h == i;
+        big |= !dg && v[h] > 0xFFu;
+        v[h] = dg ? 0u : min(v[h], 0xFFu);
+      }
+      uint8_t *d = prow + q;
+      if (q + 16 <= cw && (((uintptr_t)d) & 15) == 0) {
+        uint4 x;
+        x.x = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        x.y = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
+        x.z = v[8] | (v[9] << 8) | (v[10] << 16) | (v[11] << 24);
+        x.w = v[12] | (v[13] << 8) | (v[14] << 16) | (v[15] << 24);
+        *(uint4 *)d = x;
+      } else {
+        for (int h = 0; h < 16 && q + h < cw; ++h) d[h] = (uint8_t)v[h];
+      }
+    }
+    if (big && o.ovf) atomicOr(o.ovf, 1u);
+  } else if constexpr (DT == KMG_U16) {
     // raw counts as uint16 (multi-GPU round slabs, never normalised here): with PACK16 the
     // LDS words are the uint16 pairs themselves (column 2w in the low half = little-endian
     // order), 8 columns = 16 B per lane and step; P_max <= 255 bounds every count by 65025
@@ -1013,8 +1080,31 @@ __device__ __forceinline__ void store_out(TO *p, const TO (&v)[16 / sizeof(TO)])
   *(v4i *)p = x;
 }
 
-template <typename TO>
-__global__ __launch_bounds__(256) void tri_rows16_kernel(const uint16_t *__restrict__ S, int64_t w,
+// 8 slab elements of type TI (uint16 / uint8) from src, vector load when aligned
+template <typename TI>
+__device__ __forceinline__ void load8(const TI *src, int cnt, uint32_t (&v)[8]) {
+  if constexpr (sizeof(TI) == 2) {
+    if (cnt == 8 && (((uintptr_t)src) & 15) == 0) {
+      const uint4 x = *(const uint4 *)src;
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) v[h] = (xs[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+      return;
+    }
+  } else {
+    if (cnt == 8 && (((uintptr_t)src) & 7) == 0) {
+      const uint2 x = *(const uint2 *)src;
+#pragma unroll
+      for (int h = 0; h < 8; ++h) v[h] = ((h < 4 ? x.x : x.y) >> (8 * (h & 3))) & 0xFFu;
+      return;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 8; ++h) v[h] = h < cnt ? (uint32_t)src[h] : 0u;
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void tri_rows16_kernel(const TI *__restrict__ S, int64_t w,
                                                          int64_t yend, int64_t c0,
                                                          TO *__restrict__ K, int64_t ld,
                                                          int normalize,
@@ -1026,19 +1116,16 @@ __global__ __launch_bounds__(256) void tri_rows16_kernel(const uint16_t *__restr
   if (t >= per_row * yend) return;
   const bool norm = normalize && diagv[0] != 1.0;
   const int64_t y = t / per_row, j = (t - y * per_row) * 8;
-  const uint16_t *src = S + y * w + j;
+  const TI *src = S + y * w + j;
   const int64_t gr = c0 + y, gc = c0 + j;
   TO *dst = K + gr * ld + gc;
   const int cnt = (int)min((int64_t)8, w - j);
   uint32_t v[8];
-  if (cnt == 8 && (((uintptr_t)src) & 15) == 0) {
-    const uint4 x = *(const uint4 *)src;
-    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+  load8<TI>(src, cnt, v);
+  if constexpr (sizeof(TI) == 1) {  // 8-bit slabs leave the diagonal out: K_ii from diagv
 #pragma unroll
-    for (int h = 0; h < 8; ++h) v[h] = (xs[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-  } else {
-#pragma unroll
-    for (int h = 0; h < 8; ++h) v[h] = h < cnt ? (uint32_t)src[h] : 0u;
+    for (int h = 0; h < 8; ++h)
+      if (gc + h == gr) v[h] = (uint32_t)diagv[gr];
   }
   if (cnt == 8 && (((uintptr_t)dst) & 15) == 0) {
 #pragma unroll
@@ -1053,8 +1140,8 @@ __global__ __launch_bounds__(256) void tri_rows16_kernel(const uint16_t *__restr
   }
 }
 
-template <typename TO>
-__global__ __launch_bounds__(256) void tri_mirror16_kernel(const uint16_t *__restrict__ S, int64_t w,
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void tri_mirror16_kernel(const TI *__restrict__ S, int64_t w,
                                                            int64_t R, int64_t yend, int64_t c0,
                                                            TO *__restrict__ K, int64_t ld,
                                                            int normalize,
@@ -1070,15 +1157,12 @@ __global__ __launch_bounds__(256) void tri_mirror16_kernel(const uint16_t *__res
     const int r = c >> 3, q8 = (c & 7) * 8;
     const int64_t y = y0 + r, j = j0 + q8;
     uint32_t v[8];
-    const uint16_t *src = S + y * w + j;
-    if (y < yend && j + 8 <= w && (((uintptr_t)src) & 15) == 0) {
-      const uint4 x = *(const uint4 *)src;
-      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int h = 0; h < 8; ++h) v[h] = (xs[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+    const TI *src = S + y * w + j;
+    if (y < yend && j < w) {
+      load8<TI>(src, (int)min((int64_t)8, w - j), v);
     } else {
 #pragma unroll
-      for (int h = 0; h < 8; ++h) v[h] = (y < yend && j + h < w) ? (uint32_t)src[h] : 0u;
+      for (int h = 0; h < 8; ++h) v[h] = 0u;
     }
 #pragma unroll
     for (int h = 0; h < 8; ++h) tile[r][q8 + h] = v[h];
@@ -1118,11 +1202,11 @@ hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t 
   if (g2.y > 65535u || (items + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
 #define KMG_UNPACK(T)                                                                            \
   do {                                                                                           \
-    hipLaunchKernelGGL(tri_rows16_kernel<T>, g1, dim3(256), 0, s, S, w, yend, c0, (T *)K, ld,    \
-                       dt == KMG_I32 ? 0 : normalize, diagv, dsq);                               \
+    hipLaunchKernelGGL((tri_rows16_kernel<uint16_t, T>), g1, dim3(256), 0, s, S, w, yend, c0,    \
+                       (T *)K, ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);                   \
     if (mir)                                                                                     \
-      hipLaunchKernelGGL(tri_mirror16_kernel<T>, g2, dim3(256), 0, s, S, w, R, yend, c0, (T *)K, \
-                         ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);                         \
+      hipLaunchKernelGGL((tri_mirror16_kernel<uint16_t, T>), g2, dim3(256), 0, s, S, w, R, yend, \
+                         c0, (T *)K, ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);             \
   } while (0)
   if (dt == KMG_I32)
     KMG_UNPACK(int32_t);
@@ -1133,6 +1217,37 @@ hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t 
   else
     return hipErrorInvalidValue;
 #undef KMG_UNPACK
+  return hipGetLastError();
+}
+
+hipError_t launch_tri_unpack8(const uint8_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
+                              void *K, int64_t ld, int dt, int normalize, const double *diagv,
+                              const double *dsq, hipStream_t s) {
+  if (w <= 0 || R <= 0 || c0 >= n) return hipSuccess;
+  if (!diagv || (normalize && !dsq)) return hipErrorInvalidValue;
+  const int64_t yend = std::min(R, n - c0);
+  const int64_t items = ((w + 7) >> 3) * yend;
+  const dim3 g1((unsigned)((items + 255) / 256));
+  const bool mir = w > R;
+  const dim3 g2((unsigned)(mir ? (w - R + 63) / 64 : 0), (unsigned)((yend + 63) / 64));
+  if (g2.y > 65535u || (items + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+#define KMG_UNPACK8(T)                                                                           \
+  do {                                                                                           \
+    hipLaunchKernelGGL((tri_rows16_kernel<uint8_t, T>), g1, dim3(256), 0, s, S, w, yend, c0,     \
+                       (T *)K, ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);                   \
+    if (mir)                                                                                     \
+      hipLaunchKernelGGL((tri_mirror16_kernel<uint8_t, T>), g2, dim3(256), 0, s, S, w, R, yend,  \
+                         c0, (T *)K, ld, dt == KMG_I32 ? 0 : normalize, diagv, dsq);             \
+  } while (0)
+  if (dt == KMG_I32)
+    KMG_UNPACK8(int32_t);
+  else if (dt == KMG_F32)
+    KMG_UNPACK8(float);
+  else if (dt == KMG_F64)
+    KMG_UNPACK8(double);
+  else
+    return hipErrorInvalidValue;
+#undef KMG_UNPACK8
   return hipGetLastError();
 }
 
@@ -1164,10 +1279,14 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   // store policy: 0 auto (plain for a single-chunk int32 K, else non-temporal), 1 NT, 2 plain
   const bool nt = store == 1 || (store == 0 && !(o.dtype == KMG_I32 && g.nchunks == 1));
   const int64_t cmr = (order == 1 && g.nchunks > 1) ? rows : 0;
-  if (o.dtype == KMG_U16) {  // raw 16-bit round slab (kmg_gram_blocks), plain stores
+  if (o.dtype == KMG_U16 || o.dtype == KMG_U8) {  // raw round slab (kmg_gram_blocks)
     if (!pack) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U16, false>), grid, dim3(1024), lds, s, g, pk,
-                       off, ent, row0, cmr, o);
+    if (o.dtype == KMG_U16)
+      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U16, false>), grid, dim3(1024), lds, s, g, pk,
+                         off, ent, row0, cmr, o);
+    else
+      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U8, false>), grid, dim3(1024), lds, s, g, pk,
+                         off, ent, row0, cmr, o);
     return hipGetLastError();
   }
 #define KMG_SP(PK, NTV)                                                                       \

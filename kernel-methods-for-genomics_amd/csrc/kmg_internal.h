@@ -16,6 +16,10 @@
 // internal output dtype (not in the ABI): raw counts as uint16, the round slabs of the
 // multi-GPU upper-triangle assembly (kmg_gram_blocks), widened by tri_unpack16_kernel
 #define KMG_U16 16
+// ... and raw counts as uint8 with the diagonal left out (0 in the slab; the unpack takes
+// K_ii from the diagonal every rank computes itself): the spectrum's off-diagonal counts
+// are mostly < 256 where its diagonal (up to P^2) is not
+#define KMG_U8 8
 
 namespace kmg {
 
@@ -172,8 +176,9 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
   int64_t col_lo = 0;   // columns < col_lo are not written (upper-triangle multi-GPU
                         // builds; kernels that honour it: spectrum, mismatch slots / pairs)
-  uint32_t *ovf = nullptr;  // dtype KMG_U16: set to 1 when a count exceeds 65535 (the
-                            // stored value is then clipped and the caller redoes the build)
+  uint32_t *ovf = nullptr;  // dtype KMG_U16 / KMG_U8: set to 1 when a count exceeds 65535
+                            // / an off-diagonal count exceeds 255 (the stored value is then
+                            // clipped and the caller redoes the build with wider slabs)
 };
 
 // multi-GPU upper-triangle assembly (kmg_gram_blocks): round slab S (R rows x w = n - c0
@@ -188,6 +193,10 @@ hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, in
 hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
                                void *K, int64_t ld, int dt, int normalize, const double *diagv,
                                const double *dsq, hipStream_t s);
+// uint8 slab (diagonal left out): K_ii = diagv[i] (raw), normalised 1
+hipError_t launch_tri_unpack8(const uint8_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
+                              void *K, int64_t ld, int dt, int normalize, const double *diagv,
+                              const double *dsq, hipStream_t s);
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store = 0, int order = 0);

@@ -33,7 +33,7 @@ EXPORTS = (
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
-    "kmg_gram_to_host",
+    "kmg_gram_to_host", "kmg_gram_blocks_wire",
 )
 
 
@@ -110,6 +110,7 @@ def load():
             "kmg_gram_blocks": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64, I32,
                                  I32, I64, I32], ctypes.c_int),
             "kmg_reload_tuning": ([P], ctypes.c_int),
+            "kmg_gram_blocks_wire": ([P], ctypes.c_int),
             "kmg_gram_to_host": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, I64, P,
                                   I64], ctypes.c_int),
             "kmg_combine": ([P, P, I32, P, I32, I64, I64, P, I64], ctypes.c_int),
@@ -220,6 +221,10 @@ class Context:
         check(self.lib.kmg_gram_to_host(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                         out_dtype, int(slab_rows), out.ctypes.data,
                                         out.strides[0] // out.itemsize))
+
+    def blocks_wire(self):
+        """Bytes per element of the last gram_blocks call's all-gathered slabs."""
+        return int(self.lib.kmg_gram_blocks_wire(self._h))
 
     def reload_tuning(self):
         """Re-read the KMG_* environment knobs (read once at context creation)."""

@@ -106,6 +106,22 @@ def test_upper_triangle_16bit_slabs_overflow(ctx, data_repeats, case, world, blo
         assert full.max() > 65535  # the redo path really runs
     got = _run_blocks(ctx, data_repeats, params, dt, world, [0], block, gather=3)
     assert np.array_equal(got, full)
+    # spectrum: off-diagonal counts of identical homopolymer rows are 94^2 > 255 -> 16 bits;
+    # mismatch: 242172 > 65535 -> the output dtype's own width
+    assert ctx.blocks_wire() == (2 if case == 0 else np.dtype(L.DTYPES[dt]).itemsize)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_upper_triangle_8bit_slabs(ctx, data, case):
+    """Random sequences: every off-diagonal spectrum count fits 8 bits, so its slabs travel
+    as uint8 with the diagonal left out (K_ii from the locally computed diagonal); mismatch
+    slabs start at 16 bits (random 101-mers' mismatch counts pass 255)."""
+    params, dt = CASES[case]
+    codes, lens = data[0], data[1]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data, params, dt, 3, [0], 104, gather=3)
+    assert np.array_equal(got, full)
+    assert ctx.blocks_wire() == (1 if case == 0 else 2)
 
 
 def test_upper_triangle_one_rank_gather2(ctx, data):
