@@ -114,6 +114,9 @@ struct Tuning {
   int sp_order = 1;         // KMG_SP_ORDER: spectrum grid, 0 row-major, 1 chunk-major (N=100000:
                             // Gram 6.66 -> 5.85 ms, interleaved A/B profiles/r02aq_sp_order_ab.jsonl)
   int dense_sb = 0;         // KMG_DENSE_SB: dense Gram super-block edge in tiles (0: by F panel size)
+  int dense_bk = 128;       // KMG_DENSE_BK: dense Gram k-stage bytes, 64 or 128 (128: half the
+                            // barriers; MM k=7 N=20000 3.38 -> 3.13 ms, k=6 0.92 -> 0.87,
+                            // SP k=5 0.38 -> 0.367; profiles/r02ay_dense_bk_ab.jsonl)
 };
 
 int env_or(const char *name, int dflt) {
@@ -139,6 +142,7 @@ void read_tuning(Tuning &t) {
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
+  t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -607,7 +611,8 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
   return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
     const uint32_t *order = nullptr;
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
-    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream);
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
+                             c->tune.dense_bk);
   });
 }
 
@@ -652,7 +657,8 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
   return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
     const uint32_t *order = nullptr;
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
-    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream);
+    return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
+                             c->tune.dense_bk);
   });
 }
 

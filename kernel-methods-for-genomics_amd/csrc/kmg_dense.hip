@@ -107,12 +107,21 @@ __global__ __launch_bounds__(256) void dense_feat_kernel(
 // Epilogue: each wave stages one 32 x 32 sub-tile at a time in LDS and writes rows (and,
 // for SYM, columns) of it with 16-byte non-temporal stores.
 constexpr int DT_BM = 256;
-constexpr int DT_BK = 64;                         // bytes of F per stage
-constexpr int DT_STAGE = 2 * DT_BM * DT_BK;       // A + B bytes per stage (32 KB)
 constexpr int DT_EPI = 9 * 1024;                  // LDS bytes per wave for the epilogue
-constexpr int DT_LDS = 8 * DT_EPI > 2 * DT_STAGE ? 8 * DT_EPI : 2 * DT_STAGE;
+// BK = bytes of F per stage: 64 (32 KB of A + B per stage) or 128 (64 KB, half the
+// barriers per k; dp >= 1024)
+template <int BK>
+constexpr int dt_lds() { return 8 * DT_EPI > 2 * (2 * DT_BM * BK) ? 8 * DT_EPI : 2 * (2 * DT_BM * BK); }
 
-__device__ __forceinline__ int swz(int row, int c16) { return row * DT_BK + ((c16 ^ ((row >> 2) & 3)) << 4); }
+// 16-byte chunk c16 of row `row` in a stage: XOR-swizzled so the fragment reads of 16
+// consecutive rows at one chunk cover all 64 banks (BK = 64: 4 rows per 256 B, BK = 128: 2)
+template <int BK>
+__device__ __forceinline__ int swz(int row, int c16) {
+  if constexpr (BK == 64)
+    return row * BK + ((c16 ^ ((row >> 2) & 3)) << 4);
+  else
+    return row * BK + ((c16 ^ ((row >> 1) & 7)) << 4);
+}
 
 template <typename T>
 __device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
@@ -122,7 +131,7 @@ __device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
   __builtin_nontemporal_store(x, (v4i_t *)p);
 }
 
-template <int DT, bool SYM>
+template <int DT, bool SYM, int DT_BK>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
                                                             int64_t n, int64_t row0, int64_t rows,
                                                             int tiles_m, int tiles_n, int64_t ntiles,
@@ -159,13 +168,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
 
-  // global -> register staging: 2 x 16 B of A and 2 x 16 B of B per thread per stage
-  const int lr = tid >> 2, lc = tid & 3;
-  const int8_t *gA0 = F + (rbase + lr) * (int64_t)dp + lc * 16;
-  const int8_t *gA1 = gA0 + 128 * (int64_t)dp;
-  const int8_t *gB0 = F + (cbase + lr) * (int64_t)dp + lc * 16;
-  const int8_t *gB1 = gB0 + 128 * (int64_t)dp;
-  const int so0 = swz(lr, lc), so1 = swz(lr + 128, lc);
+  // global -> register staging: NR rows x 16 B of A and of B per thread per stage
+  constexpr int CPR = DT_BK / 16;          // 16-byte chunks per row and stage
+  constexpr int RSTEP = 512 / CPR;         // rows between a thread's staged rows
+  constexpr int NR = DT_BM / RSTEP;        // rows per thread and operand (2 or 4)
+  constexpr int DT_STAGE = 2 * DT_BM * DT_BK;
+  const int lr = tid / CPR, lc = tid % CPR;
+  const int8_t *gA = F + (rbase + lr) * (int64_t)dp + lc * 16;
+  const int8_t *gB = F + (cbase + lr) * (int64_t)dp + lc * 16;
+  int so[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) so[q] = swz<DT_BK>(lr + q * RSTEP, lc);
 
   v16i acc[4][2];
 #pragma unroll
@@ -174,14 +187,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (int b = 0; b < 2; ++b) acc[a][b] = (v16i){};
 
   const int nst = dp / DT_BK;
-  uint4 ra0 = *(const uint4 *)gA0, ra1 = *(const uint4 *)gA1;
-  uint4 rb0 = *(const uint4 *)gB0, rb1 = *(const uint4 *)gB1;
+  v4i ra[NR], rb[NR];  // ext-vector registers (a HIP_vector_type array stays in scratch)
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    ra[q] = *(const v4i *)(gA + (int64_t)q * RSTEP * dp);
+    rb[q] = *(const v4i *)(gB + (int64_t)q * RSTEP * dp);
+  }
   {
     uint8_t *sA = lds, *sB = lds + DT_BM * DT_BK;
-    *(uint4 *)(sA + so0) = ra0;
-    *(uint4 *)(sA + so1) = ra1;
-    *(uint4 *)(sB + so0) = rb0;
-    *(uint4 *)(sB + so1) = rb1;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      *(v4i *)(sA + so[q]) = ra[q];
+      *(v4i *)(sB + so[q]) = rb[q];
+    }
   }
   __syncthreads();
   const int fr = lane & 31, fh = lane >> 5;
@@ -190,10 +208,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const bool more = st + 1 < nst;
     if (more) {
       const int k0 = (st + 1) * DT_BK;
-      ra0 = *(const uint4 *)(gA0 + k0);
-      ra1 = *(const uint4 *)(gA1 + k0);
-      rb0 = *(const uint4 *)(gB0 + k0);
-      rb1 = *(const uint4 *)(gB1 + k0);
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        ra[q] = *(const v4i *)(gA + (int64_t)q * RSTEP * dp + k0);
+        rb[q] = *(const v4i *)(gB + (int64_t)q * RSTEP * dp + k0);
+      }
     }
     const uint8_t *sA = lds + buf * DT_STAGE;
     const uint8_t *sB = sA + DT_BM * DT_BK;
@@ -202,9 +221,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int c16 = 2 * s + fh;
       v4i a[4], b[2];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) a[x] = *(const v4i *)(sA + swz(wm * 128 + x * 32 + fr, c16));
+      for (int x = 0; x < 4; ++x) a[x] = *(const v4i *)(sA + swz<DT_BK>(wm * 128 + x * 32 + fr, c16));
 #pragma unroll
-      for (int y = 0; y < 2; ++y) b[y] = *(const v4i *)(sB + swz(wn * 64 + y * 32 + fr, c16));
+      for (int y = 0; y < 2; ++y) b[y] = *(const v4i *)(sB + swz<DT_BK>(wn * 64 + y * 32 + fr, c16));
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -213,10 +232,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     if (more) {
       uint8_t *dA = lds + (buf ^ 1) * DT_STAGE, *dB = dA + DT_BM * DT_BK;
-      *(uint4 *)(dA + so0) = ra0;
-      *(uint4 *)(dA + so1) = ra1;
-      *(uint4 *)(dB + so0) = rb0;
-      *(uint4 *)(dB + so1) = rb1;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        *(v4i *)(dA + so[q]) = ra[q];
+        *(v4i *)(dB + so[q]) = rb[q];
+      }
       __syncthreads();
     }
   }
@@ -373,20 +393,26 @@ hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, i
 }
 
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
-                             const uint32_t *order, const OutSpec &o, hipStream_t s) {
+                             const uint32_t *order, const OutSpec &o, hipStream_t s, int bk) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || n <= 0) return hipSuccess;
-  if (dp & (DT_BK - 1)) return hipErrorInvalidValue;
+  if (bk != 128 || (dp & 127)) bk = 64;
+  if (dp & 63) return hipErrorInvalidValue;
   const bool sym = row0 == 0 && rows == n;
   const int tiles_m = (int)((rows + DT_BM - 1) / DT_BM);
   const int tiles_n = (int)((n + DT_BM - 1) / DT_BM);
   const int64_t total = sym ? (int64_t)tiles_n * (tiles_n + 1) / 2 : (int64_t)tiles_m * tiles_n;
   if (total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((total + 7) & ~7LL);
-  const size_t lds = DT_LDS;
 #define KMG_DENSE(DTV, SY)                                                                       \
-  hipLaunchKernelGGL((gram_dense_kernel<DTV, SY>), dim3(grid), dim3(512), lds, s, F, dp, n, row0, \
-                     rows, tiles_m, tiles_n, total, order, o)
+  do {                                                                                           \
+    if (bk == 128)                                                                               \
+      hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, 128>), dim3(grid), dim3(512), dt_lds<128>(), \
+                         s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o);            \
+    else                                                                                         \
+      hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, 64>), dim3(grid), dim3(512), dt_lds<64>(),  \
+                         s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o);            \
+  } while (0)
   switch (o.dtype) {
     case KMG_I32:
       if (sym) KMG_DENSE(KMG_I32, true); else KMG_DENSE(KMG_I32, false);
