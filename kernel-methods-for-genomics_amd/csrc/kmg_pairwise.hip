@@ -175,23 +175,25 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
   }
 }
 
-// WD on the 2-bit packed records (Packed, kmg_internal.h).  Symbol q of code word w sits
-// at bits [30-2q, 31-2q]; with v = x_w ^ y_w, bit 31-2q of v | v << 1 is set iff the
-// symbols differ, so the match mask of a pair is M_w = keep_w & ~(v | v << 1), 2 bits a
-// position and position l+1 two bits below l.  keep_w holds the positions [1, min(Lx, Ly,
+// WD on the packed records, as bit planes.  Staging turns a record's 2-bit codes (symbol q
+// of code word w at bits [30-2q, 31-2q]) into two planes of one bit per position —
+// position l at bit 31 - l%32 of word l/32, plane 1 the high code bits, plane 0 the low —
+// so the match mask of a pair is M_w = keep_w & ~((x1 ^ y1) | (x0 ^ y0)), one bit a
+// position and position l+1 one bit below l.  keep_w holds the positions [1, min(Lx, Ly,
 // L)) (kernels.py:78: l >= 1; a slice clipped by either end never equals a full one, and
-// the range is symmetric in i, j).  Then A_1 = M, A_k = A_{k-1} & (A_{k-1} << 2) (one
+// the range is symmetric in i, j).  Then A_1 = M, A_k = A_{k-1} & (A_{k-1} << 1) (one
 // funnel shift a word) and c_k = popc(A_k) = #{l in [1, L-k] : x[l:l+k] == y[l:l+k]}
 // (kernels.py:64-81); val accumulates beta_k * c_k in k order.  The k loop ends when no
 // lane of the wave has a run left: a skipped beta_k * 0 adds +0.0 (no rounding change).
-// A pair holding a non-ACGT symbol (mask bit below len) is compared byte by byte from the
-// codes (rare; exact for any alphabet).  Tile: 64 columns (one per lane, record in VGPRs)
-// x 64 rows (16 per wave, records read wave-uniform through the scalar cache).  MIRROR
-// (full square K): only tiles J >= I run; an off-diagonal tile also writes its transpose
-// from an LDS copy, 64 coalesced 512-B rows.
+// Half the words of the 2-bit form per pair (4 against 7 at L = 101): 1.8x fewer VALU
+// operations in the mask and k loop.  A pair holding a non-ACGT symbol (mask bit below
+// len) is compared byte by byte from the codes (rare; exact for any alphabet).  Tile: 64
+// columns (one per lane, planes in VGPRs) x 64 rows (16 per wave, planes read
+// wave-uniform from LDS).  MIRROR (full square K): only tiles J >= I run; an off-diagonal
+// tile also writes its transpose from an LDS copy, 64 coalesced 512-B rows.
 __device__ __forceinline__ uint32_t wd_keep(int lim, int w) {
-  const int nv = min(max(lim - 16 * w, 0), 16);
-  return nv == 0 ? 0u : (0xAAAAAAAAu & (0xFFFFFFFFu << (32 - 2 * nv)));
+  const int nv = min(max(lim - 32 * w, 0), 32);
+  return nv == 0 ? 0u : (0xFFFFFFFFu << (32 - nv));
 }
 
 __device__ __forceinline__ bool wd_has_other(const uint32_t *rec, int cw, int len) {
@@ -204,27 +206,47 @@ __device__ __forceinline__ bool wd_has_other(const uint32_t *rec, int cw, int le
   return bad;
 }
 
-template <int NC>
+// the even bits of x (bit 2i -> bit i): 16 bits in symbol order, first symbol highest
+__device__ __forceinline__ uint32_t even_bits(uint32_t x) {
+  x &= 0x55555555u;
+  x = (x | (x >> 1)) & 0x33333333u;
+  x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+  x = (x | (x >> 4)) & 0x00FF00FFu;
+  return (x | (x >> 8)) & 0x0000FFFFu;
+}
+
+// planes of a record: dst[p] (high code bits) and dst[NP + p] (low) for p < NP
+template <int NP>
+__device__ __forceinline__ void wd_planes(const uint32_t *rec, int cw, uint32_t *dst) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const uint32_t w0 = 2 * p < cw ? rec[2 * p] : 0u, w1 = 2 * p + 1 < cw ? rec[2 * p + 1] : 0u;
+    dst[p] = (even_bits(w0 >> 1) << 16) | even_bits(w1 >> 1);
+    dst[NP + p] = (even_bits(w0) << 16) | even_bits(w1);
+  }
+}
+
+template <int NP>
 __device__ __forceinline__ void wd_mask_bytes(const SeqSpec &q, int64_t a, int64_t b, int lim,
-                                              uint32_t (&M)[NC]) {
+                                              uint32_t (&M)[NP]) {
   const uint8_t *xa = q.codes + a * q.ldc, *yb = q.codes + b * q.ldc;
 #pragma unroll
-  for (int w = 0; w < NC; ++w) {
+  for (int w = 0; w < NP; ++w) {
     uint32_t m = 0;
-    for (int t = 0; t < 16; ++t) {
-      const int pos = 16 * w + t;
-      if (pos >= 1 && pos < lim && xa[pos] == yb[pos]) m |= 1u << (31 - 2 * t);
+    for (int t = 0; t < 32; ++t) {
+      const int pos = 32 * w + t;
+      if (pos >= 1 && pos < lim && xa[pos] == yb[pos]) m |= 1u << (31 - t);
     }
     M[w] = m;
   }
 }
 
-template <int NC, bool MIRROR>
+template <int NP, bool MIRROR>
 __global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int64_t row0,
                                                        int64_t row1, int d, int span, Coef cf,
                                                        OutSpec o) {
   constexpr int RB = 64;
-  constexpr int SW = NC | 1;  // odd word stride: the column reads are bank-conflict free
+  constexpr int SW = (2 * NP) | 1;  // odd word stride: the column reads are bank-conflict free
   __shared__ double tile[MIRROR ? RB : 1][MIRROR ? 65 : 1];
   __shared__ uint32_t srow[RB][SW], scol[64][SW];
   __shared__ int slen[RB];  // row length, -1 - length if the row holds a non-ACGT symbol
@@ -242,13 +264,12 @@ __global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int
     bool bad = false;
     if (t < lim) {
       const uint32_t *rec = pk.w + t * pk.ldp;
-#pragma unroll
-      for (int w = 0; w < NC; ++w) dst[lane][w] = w < pk.cw ? rec[w] : 0u;
+      wd_planes<NP>(rec, pk.cw, dst[lane]);
       len = q.lens[t];
       bad = wd_has_other(rec, pk.cw, len);
     } else {
 #pragma unroll
-      for (int w = 0; w < NC; ++w) dst[lane][w] = 0u;
+      for (int w = 0; w < 2 * NP; ++w) dst[lane][w] = 0u;
     }
     if (wave == 0) slen[lane] = bad ? -1 - len : len;
   }
@@ -258,11 +279,12 @@ __global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int
   const int64_t jj = jin ? j : 0;
   Ly = q.lens[jj];
   cbad = wd_has_other(pk.w + jj * pk.ldp, pk.cw, Ly);
-  uint32_t y[NC], ky[NC];
+  uint32_t y1[NP], y0[NP], ky[NP];
   const int Lyc = span > 0 ? min(Ly, span) : Ly;
 #pragma unroll
-  for (int w = 0; w < NC; ++w) {
-    y[w] = scol[lane][w];
+  for (int w = 0; w < NP; ++w) {
+    y1[w] = scol[lane][w];
+    y0[w] = scol[lane][NP + w];
     ky[w] = wd_keep(Lyc, w);
   }
   ky[0] &= 0x7FFFFFFFu;  // l >= 1
@@ -277,29 +299,29 @@ __global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int
     if (i == j) {
       val = __dadd_rn((double)(Lx - 1), (double)(1 - d) / 3.0);  // kernels.py:96
     } else {
-      uint32_t A[NC];
+      uint32_t A[NP];
       if (rbad || cbad) {
         const int lim = span > 0 ? min(min(Lx, Ly), span) : min(Lx, Ly);
-        wd_mask_bytes<NC>(q, i, jj, lim, A);
+        wd_mask_bytes<NP>(q, i, jj, lim, A);
       } else {
 #pragma unroll
-        for (int w = 0; w < NC; ++w) {
+        for (int w = 0; w < NP; ++w) {
           const uint32_t kx = wd_keep(Lx, w);
-          const uint32_t v = srow[r][w] ^ y[w];
-          A[w] = (kx & ky[w]) & ~(v | (v << 1));
+          const uint32_t v = (srow[r][w] ^ y1[w]) | (srow[r][NP + w] ^ y0[w]);
+          A[w] = (kx & ky[w]) & ~v;
         }
       }
       val = 0.0;
       for (int k = 1; k <= d; ++k) {
         int c = 0;
 #pragma unroll
-        for (int w = 0; w < NC; ++w) c += __popc(A[w]);
+        for (int w = 0; w < NP; ++w) c += __popc(A[w]);
         if (!__any(c != 0)) break;
         if (c) val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], (double)c));
 #pragma unroll
-        for (int w = 0; w < NC; ++w) {
-          const uint32_t nxt = (w + 1 < NC) ? A[w + 1] : 0u;
-          A[w] &= __builtin_amdgcn_alignbit(A[w], nxt, 30);  // (A_w << 2) | (A_{w+1} >> 30)
+        for (int w = 0; w < NP; ++w) {
+          const uint32_t nxt = (w + 1 < NP) ? A[w + 1] : 0u;
+          A[w] &= __builtin_amdgcn_alignbit(A[w], nxt, 31);  // (A_w << 1) | (A_{w+1} >> 31)
         }
       }
     }
@@ -786,10 +808,10 @@ hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row
       hipLaunchKernelGGL((gram_wdp_kernel<NC_, false>), grid, dim3(256), 0, s, q, pk, row0,     \
                          row1, d, span, cf, o);                                                  \
   } while (0)
-  if (need <= 4) KMG_WDP(4);
-  else if (need <= 7) KMG_WDP(7);
-  else if (need <= 8) KMG_WDP(8);
-  else if (need <= 16) KMG_WDP(16);
+  // plane words per pair: ceil(code words / 2)
+  if (need <= 4) KMG_WDP(2);
+  else if (need <= 8) KMG_WDP(4);
+  else if (need <= 16) KMG_WDP(8);
   else return hipErrorNotSupported;
 #undef KMG_WDP
   return hipGetLastError();
