@@ -105,7 +105,7 @@ struct Tuning {
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
   int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
   int idx_v2 = 1;           // KMG_IDX_V2: index build without device-scope atomics
-  int idx_seqs = 80;        // KMG_IDX_SEQS: sequences per partition block
+  int idx_seqs = 0;         // KMG_IDX_SEQS: sequences per partition block (0: auto, build_index)
   int idx_buckets = 0;      // KMG_IDX_BUCKETS: coarse buckets (0: 384 spectrum / 1024 mismatch)
   int idx_threads = 1024;   // KMG_IDX_THREADS
   int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
@@ -276,7 +276,12 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk, const uint8_t *codes
                                                        std::min<int64_t>(4096, occ / 40000));
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
-  g.seqs_per_block = std::max(1, c->tune.idx_seqs);
+  // sequences per partition block: 80; the exact (spectrum) index uses at most ~256 blocks,
+  // so the gather pass keeps every segment's items in registers (N=100000: fine 125 -> 93
+  // us with 400 sequences a block, profiles/r02bb_index_seqs.jsonl)
+  g.seqs_per_block = c->tune.idx_seqs > 0
+                         ? c->tune.idx_seqs
+                         : (int)(g.copies == 1 ? std::max<int64_t>(80, (g.n + 255) / 256) : 80);
   {  // LDS: two bucket arrays + the staged packed records
     const int64_t budget = 150 * 1024 - 8 * (g.nbins() >> g.fine_bits) - 4096;
     g.seqs_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(g.seqs_per_block, budget / (4 * pk.ldp)));
