@@ -201,3 +201,27 @@ def test_mismatch_device_rows_narrower_than_window(ctx):
     finally:
         for p in (d_out, d_codes, d_lens):
             ctx.dfree(p)
+
+
+@pytest.mark.parametrize("params,dt,wire", [
+    (P.make(L.KMG_MISMATCH, k=10, m=1, window=101, normalize=1), L.KMG_F64, 2),  # pair table
+    (P.make(L.KMG_MISMATCH, k=8, m=1, window=101, normalize=0), L.KMG_I32, 2),   # slot table
+    (P.make(L.KMG_SPECTRUM, k=12), L.KMG_I32, 1),
+    (P.make(L.KMG_SPECTRUM, k=5), L.KMG_I32, 4),  # dense path: full-width slabs
+])
+def test_upper_triangle_slabs_other_formulations(ctx, params, dt, wire):
+    """The narrow round slabs through the other posting-list kernels (drop-two pair table
+    at k = 10, slot table at k = 8, spectrum k = 12) and the full-width fallback of the
+    dense formulation: the assembled K equals the single-call K."""
+    codes, lens = E.synthetic(400, 101, seed=73)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        full = ctx.gram(params, codes, lens, dt)
+        got = _run_blocks(ctx, (codes, lens, d_codes, d_lens), params, dt, 3, [0], 48, gather=3)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    assert np.array_equal(got, full)
+    assert ctx.blocks_wire() == wire
