@@ -276,12 +276,12 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk, const uint8_t *codes
                                                        std::min<int64_t>(4096, occ / 40000));
   g.fine_bits = 8;
   while (g.fine_bits < 14 && (g.nbins() >> g.fine_bits) > target_buckets) ++g.fine_bits;
-  // sequences per partition block: 80; the exact (spectrum) index uses at most ~256 blocks,
-  // so the gather pass keeps every segment's items in registers (N=100000: fine 125 -> 93
-  // us with 400 sequences a block, profiles/r02bb_index_seqs.jsonl)
-  g.seqs_per_block = c->tune.idx_seqs > 0
-                         ? c->tune.idx_seqs
-                         : (int)(g.copies == 1 ? std::max<int64_t>(80, (g.n + 255) / 256) : 80);
+  // sequences per partition block: 80, or enough for at most ~256 blocks, so the gather
+  // pass keeps every segment's items in registers (N=100000 spectrum: fine 125 -> 93 us;
+  // N=200000 MM(9,1): place + fine 2.81 -> 2.35 ms; profiles/r02bb_index_seqs.jsonl,
+  // r02be_index_seqs_mm.jsonl)
+  g.seqs_per_block = c->tune.idx_seqs > 0 ? c->tune.idx_seqs
+                                          : (int)std::max<int64_t>(80, (g.n + 255) / 256);
   {  // LDS: two bucket arrays + the staged packed records
     const int64_t budget = 150 * 1024 - 8 * (g.nbins() >> g.fine_bits) - 4096;
     g.seqs_per_block = (int)std::max<int64_t>(1, std::min<int64_t>(g.seqs_per_block, budget / (4 * pk.ldp)));
