@@ -92,9 +92,13 @@ __global__ __launch_bounds__(256) void dense_feat_kernel(
 // ------------------------------------------------------------------ GEMM
 // K[r][c] = sum_b F[r][b] F[c][b] over a 256 x 256 output tile per workgroup: 8 waves in a
 // 2 x 4 grid, each 128 x 64 = 4 x 2 v_mfma_i32_32x32x32_i8 tiles (128 accumulator
-// registers).  The reduction runs over 64-byte stages of F staged in LDS (double
-// buffered; the 16-byte chunk of row r sits at chunk ^ ((r >> 2) & 3), so the fragment
-// reads of 16 consecutive rows hit 16 distinct bank quads).
+// registers).  The reduction runs over BK-byte stages of F, double buffered in LDS and
+// filled by LDS-DMA (global_load_lds_dwordx4, no staging registers or ds_write; the next
+// stage's DMA is in flight while this stage multiplies; MM k=7 N=20000 3.17 -> 2.77 ms,
+// k=6 0.89 -> 0.79, SP k=5 0.36 -> 0.34 with HALF; profiles/r02bk_dense_glds_ab.jsonl).
+// The 16-byte chunk c of row r sits at slot c ^ swz_x(r), so the fragment reads of 16
+// consecutive rows hit 16 distinct bank quads; the DMA writes lane-linearly, so each lane
+// fetches the chunk its slot holds.
 //
 // Both operands are rows of F, so A and B fragments are loaded by the same code:
 // whatever order the instruction sums its 32 k-values in, A and B use the same lane/
@@ -106,12 +110,23 @@ __global__ __launch_bounds__(256) void dense_feat_kernel(
 // symmetric and the fused normalisation K_ij / (d_i * d_j) is too, bit for bit).
 // Epilogue: each wave stages one 32 x 32 sub-tile at a time in LDS and writes rows (and,
 // for SYM, columns) of it with 16-byte non-temporal stores.
+//
+// HALF (dp <= 1024): the 256 x 256 tile is split over two 4-wave workgroups, each 256 x 128
+// (2 x 2 waves of the same 128 x 64), BK = 64 only (48 KB of LDS per workgroup).  The 8-wave
+// form keeps one workgroup per CU (128 accumulators + staging = 2 waves per SIMD), so a CU's
+// k loop and its epilogue stores run one after the other; with two 4-wave workgroups per
+// CU one can store while the other multiplies (the store phase is as long as the k loop:
+// 512 KB of a SYM off-diagonal tile at a CU's 1/256 share of HBM ~ 17 us, the tile's int8
+// MFMA work ~ 7 us at peak).
 constexpr int DT_BM = 256;
-constexpr int DT_EPI = 9 * 1024;                  // LDS bytes per wave for the epilogue
+constexpr int DT_EPI = 8 * 1024;                  // LDS bytes per wave for the epilogue (32 x 32 x 8 B)
 // BK = bytes of F per stage: 64 (32 KB of A + B per stage) or 128 (64 KB, half the
 // barriers per k; dp >= 1024)
-template <int BK>
-constexpr int dt_lds() { return 8 * DT_EPI > 2 * (2 * DT_BM * BK) ? 8 * DT_EPI : 2 * (2 * DT_BM * BK); }
+template <int BK, bool HALF = false>
+constexpr int dt_lds() {
+  constexpr int nw = HALF ? 4 : 8, stage = (DT_BM + (HALF ? DT_BM / 2 : DT_BM)) * BK;
+  return nw * DT_EPI > 2 * stage ? nw * DT_EPI : 2 * stage;
+}
 
 // 16-byte chunk c16 of row `row` in a stage: XOR-swizzled so the fragment reads of 16
 // consecutive rows at one chunk cover all 64 banks (BK = 64: 4 rows per 256 B, BK = 128: 2)
@@ -123,6 +138,14 @@ __device__ __forceinline__ int swz(int row, int c16) {
     return row * BK + ((c16 ^ ((row >> 1) & 7)) << 4);
 }
 
+// the XOR that swz<BK> applies to row `row`'s chunk index
+template <int BK>
+__device__ __forceinline__ int swz_x(int row) {
+  return BK == 64 ? (row >> 2) & 3 : (row >> 1) & 7;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
 template <typename T>
 __device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
   typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -131,8 +154,8 @@ __device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
   __builtin_nontemporal_store(x, (v4i_t *)p);
 }
 
-template <int DT, bool SYM, int DT_BK>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
+template <int DT, bool SYM, int DT_BK, bool HALF>
+__global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_eu(HALF ? 2 : 1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
                                                             int64_t n, int64_t row0, int64_t rows,
                                                             int tiles_m, int tiles_n, int64_t ntiles,
                                                             const uint32_t *__restrict__ order,
@@ -141,8 +164,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                       typename std::conditional<DT == KMG_F32, float, int32_t>::type>::type;
   extern __shared__ __align__(16) uint8_t lds[];
   const int64_t per_xcd = ((int64_t)gridDim.x + 7) >> 3;
-  const int64_t logical = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (logical >= ntiles) return;
+  const int64_t wlogical = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (wlogical >= (HALF ? 2 * ntiles : ntiles)) return;
+  const int64_t logical = HALF ? wlogical >> 1 : wlogical;  // both halves of a tile: one XCD
   int tm, tn;
   if (order) {  // host-built super-block order (dense_tile_order, kmg_api.cpp)
     const uint32_t t = order[logical];
@@ -161,24 +185,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     tn = (int)(logical - (int64_t)tm * tiles_n);
   }
   const int64_t rbase = row0 + (int64_t)tm * DT_BM;
-  const int64_t cbase = (int64_t)tn * DT_BM;
+  constexpr int BN = HALF ? DT_BM / 2 : DT_BM;  // columns of this workgroup's part
+  const int64_t cbase = (int64_t)tn * DT_BM + (HALF ? (wlogical & 1) * BN : 0);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = HALF ? wave >> 1 : wave >> 2, wn = HALF ? wave & 1 : wave & 3;
 
-  // global -> register staging: NR rows x 16 B of A and of B per thread per stage
+  constexpr int NT = HALF ? 256 : 512;
   constexpr int CPR = DT_BK / 16;          // 16-byte chunks per row and stage
-  constexpr int RSTEP = 512 / CPR;         // rows between a thread's staged rows
-  constexpr int NR = DT_BM / RSTEP;        // rows per thread and operand (2 or 4)
-  constexpr int DT_STAGE = 2 * DT_BM * DT_BK;
-  const int lr = tid / CPR, lc = tid % CPR;
-  const int8_t *gA = F + (rbase + lr) * (int64_t)dp + lc * 16;
-  const int8_t *gB = F + (cbase + lr) * (int64_t)dp + lc * 16;
-  int so[NR];
-#pragma unroll
-  for (int q = 0; q < NR; ++q) so[q] = swz<DT_BK>(lr + q * RSTEP, lc);
+  constexpr int DT_STAGE = (DT_BM + BN) * DT_BK;
 
   v16i acc[4][2];
 #pragma unroll
@@ -186,35 +203,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (v16i){};
 
-  const int nst = dp / DT_BK;
-  v4i ra[NR], rb[NR];  // ext-vector registers (a HIP_vector_type array stays in scratch)
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    ra[q] = *(const v4i *)(gA + (int64_t)q * RSTEP * dp);
-    rb[q] = *(const v4i *)(gB + (int64_t)q * RSTEP * dp);
-  }
-  {
-    uint8_t *sA = lds, *sB = lds + DT_BM * DT_BK;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      *(v4i *)(sA + so[q]) = ra[q];
-      *(v4i *)(sB + so[q]) = rb[q];
-    }
-  }
-  __syncthreads();
   const int fr = lane & 31, fh = lane >> 5;
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    const bool more = st + 1 < nst;
-    if (more) {
-      const int k0 = (st + 1) * DT_BK;
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        ra[q] = *(const v4i *)(gA + (int64_t)q * RSTEP * dp + k0);
-        rb[q] = *(const v4i *)(gB + (int64_t)q * RSTEP * dp + k0);
-      }
-    }
-    const uint8_t *sA = lds + buf * DT_STAGE;
+  auto mfma_stage = [&](const uint8_t *sA) {
     const uint8_t *sB = sA + DT_BM * DT_BK;
 #pragma unroll
     for (int s = 0; s < DT_BK / 32; ++s) {
@@ -230,22 +220,65 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         for (int y = 0; y < 2; ++y)
           acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[y], acc[x][y], 0, 0, 0);
     }
-    if (more) {
-      uint8_t *dA = lds + (buf ^ 1) * DT_STAGE, *dB = dA + DT_BM * DT_BK;
+  };
+  {
+    // LDS-DMA staging (global_load_lds_dwordx4): one wave-instruction fills 1 KB of the
+    // stage linearly (RPI rows), so the swizzle moves to the source: LDS slot s of row r
+    // holds chunk s ^ swz_x(r), the chunk swz<BK> put there.
+    constexpr int RPI = 1024 / DT_BK, NW = NT / 64;
+    constexpr int NIA = DT_BM / RPI / NW, NIB = BN / RPI / NW;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int lrow = lane / CPR, slot = lane % CPR;
+    const int8_t *srcA[NIA], *srcB[NIB];
 #pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        *(v4i *)(dA + so[q]) = ra[q];
-        *(v4i *)(dB + so[q]) = rb[q];
+    for (int q = 0; q < NIA; ++q) {
+      const int row = (wv * NIA + q) * RPI + lrow;
+      srcA[q] = F + (rbase + row) * (int64_t)dp + ((slot ^ swz_x<DT_BK>(row)) << 4);
+    }
+#pragma unroll
+    for (int q = 0; q < NIB; ++q) {
+      const int row = (wv * NIB + q) * RPI + lrow;
+      srcB[q] = F + (cbase + row) * (int64_t)dp + ((slot ^ swz_x<DT_BK>(row)) << 4);
+    }
+    auto issue = [&](uint8_t *dst, int k0) {
+#pragma unroll
+      for (int q = 0; q < NIA; ++q)
+        __builtin_amdgcn_global_load_lds((const void *)(srcA[q] + k0),
+                                         (lds_void *)(dst + (wv * NIA + q) * 1024), 16, 0, 0);
+#pragma unroll
+      for (int q = 0; q < NIB; ++q)
+        __builtin_amdgcn_global_load_lds((const void *)(srcB[q] + k0),
+                                         (lds_void *)(dst + DT_BM * DT_BK + (wv * NIB + q) * 1024),
+                                         16, 0, 0);
+    };
+    const int nst = dp / DT_BK;
+    issue(lds, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA has landed
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      const int buf = st & 1;
+      const bool more = st + 1 < nst;
+      if (more) issue(lds + (buf ^ 1) * DT_STAGE, (st + 1) * DT_BK);  // read in stage st-1
+      mfma_stage(lds + buf * DT_STAGE);
+      if (more) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
   __syncthreads();  // staging buffers are reused by the epilogue
 
   const bool norm = DT != KMG_I32 && o.normalize && o.diagv[0] != 1.0;
   const int64_t rend = row0 + rows;
-  constexpr int PITCH = sizeof(T) == 8 ? 34 : 36;  // elements per LDS tile row (16-B aligned)
+
+  // 32 x 32 sub-tile, row r's column c at r * 32 + ecol(r, c): the XOR keeps every 16-B
+  // group of V columns together (row reads stay ds_read_b128) and spreads the column
+  // reads of the mirror over all banks (4-way conflicts with a padded pitch instead)
+  constexpr int PITCH = 32;
   constexpr int V = 16 / (int)sizeof(T);                                       // per 16 B
+  auto ecol = [](int r, int c) {
+    return sizeof(T) == 8 ? c ^ (2 * ((r >> 1) & 15)) : c ^ (4 * ((r >> 2) & 7));
+  };
   T *tile = (T *)(lds + wave * DT_EPI);
   const bool mirror = SYM && tm != tn;
   const bool vec_ok = ((o.ld * (int64_t)sizeof(T)) & 15) == 0 && (((uintptr_t)o.out) & 15) == 0;
@@ -270,7 +303,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
           if (norm) d = (gr == gc) ? 1.0 : (gr < rend && gc < n ? d / (o.dsq[gr] * dc) : 0.0);
           val = (T)d;
         }
-        tile[r * PITCH + fr] = val;
+        tile[r * PITCH + ecol(r, fr)] = val;
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
       __builtin_amdgcn_wave_barrier();
@@ -284,7 +317,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         if (gr >= rend) continue;
         T v[V];
 #pragma unroll
-        for (int q = 0; q < V; ++q) v[q] = tile[r * PITCH + c4 + q];
+        for (int q = 0; q < V; ++q) v[q] = tile[r * PITCH + ecol(r, c4) + q];
         T *dst = (T *)o.out + (gr - row0) * o.ld + gc;
         if (vec_ok && gc + V <= n) {
           store16(dst, v);
@@ -303,7 +336,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
           if (orow >= n) continue;
           T v[V];
 #pragma unroll
-          for (int q = 0; q < V; ++q) v[q] = tile[(r4 + q) * PITCH + c];
+          for (int q = 0; q < V; ++q) v[q] = tile[(r4 + q) * PITCH + ecol(r4 + q, c)];
           T *dst = (T *)o.out + orow * o.ld + ocol;
           if (vec_ok && ocol + V <= rend) {
             store16(dst, v);
@@ -393,25 +426,26 @@ hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, i
 }
 
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
-                             const uint32_t *order, const OutSpec &o, hipStream_t s, int bk) {
+                             const uint32_t *order, const OutSpec &o, hipStream_t s, int bk,
+                             bool half) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || n <= 0) return hipSuccess;
-  if (bk != 128 || (dp & 127)) bk = 64;
+  if (bk != 128 || (dp & 127) || half) bk = 64;
   if (dp & 63) return hipErrorInvalidValue;
   const bool sym = row0 == 0 && rows == n;
   const int tiles_m = (int)((rows + DT_BM - 1) / DT_BM);
   const int tiles_n = (int)((n + DT_BM - 1) / DT_BM);
   const int64_t total = sym ? (int64_t)tiles_n * (tiles_n + 1) / 2 : (int64_t)tiles_m * tiles_n;
   if (total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((total + 7) & ~7LL);
-#define KMG_DENSE(DTV, SY)                                                                       \
-  do {                                                                                           \
-    if (bk == 128)                                                                               \
-      hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, 128>), dim3(grid), dim3(512), dt_lds<128>(), \
-                         s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o);            \
-    else                                                                                         \
-      hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, 64>), dim3(grid), dim3(512), dt_lds<64>(),  \
-                         s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o);            \
+  const unsigned grid = (unsigned)(((half ? 2 * total : total) + 7) & ~7LL);
+#define KMG_DENSE_GO(DTV, SY, BKV, HV)                                                          \
+  hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, BKV, HV>), dim3(grid), dim3(HV ? 256 : 512),      \
+                     (dt_lds<BKV, HV>()), s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o)
+#define KMG_DENSE(DTV, SY)                                                      \
+  do {                                                                          \
+    if (half) KMG_DENSE_GO(DTV, SY, 64, true);                                  \
+    else if (bk == 128) KMG_DENSE_GO(DTV, SY, 128, false);                      \
+    else KMG_DENSE_GO(DTV, SY, 64, false);                                      \
   } while (0)
   switch (o.dtype) {
     case KMG_I32:
@@ -425,6 +459,7 @@ hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, i
       break;
   }
 #undef KMG_DENSE
+#undef KMG_DENSE_GO
   return hipGetLastError();
 }
 

@@ -15,9 +15,11 @@ from kmgram import params as P
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def dense(tune):
-    tune(KMG_ALGO=1)
+@pytest.fixture(params=[0, 1], ids=["wg8", "half"])
+def dense(tune, request):
+    """The dense path, with each tile on one 8-wave workgroup or split over two 4-wave ones
+    (KMG_DENSE_HALF; auto: half when the feature width is <= 1024)."""
+    tune(KMG_ALGO=1, KMG_DENSE_HALF=request.param)
 
 
 @pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Dense Gram split over two 4-wave workgroups per tile (KMG_DENSE_HALF): parity, then an
+# interleaved one-process A/B against the 8-wave tile.
+set -u
+OUT=gpurun_out/r2bh
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_dense.py tests/test_gpu_learners.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.txt" 2>&1 || { tail -30 $OUT/pytest.txt; exit 1; }
+tail -n 1 $OUT/pytest.txt
+: > "$OUT/ab.jsonl"
+for cfg in '{"kind": "sp", "k": 5, "n": 20000, "reps": 3, "steps": 10}' \
+           '{"kind": "mm", "k": 6, "n": 20000, "norm": 0, "reps": 3, "steps": 10, "seed": 3}' \
+           '{"kind": "mm", "k": 7, "n": 20000, "norm": 0, "reps": 2, "steps": 3, "seed": 3}' \
+           '{"kind": "mm", "k": 5, "n": 9000, "norm": 1, "reps": 3, "steps": 10, "seed": 3}'; do
+  timeout -k 10 200 python3 -u tools/ab_env.py "$cfg" '[{"KMG_ALGO": 1}, {"KMG_ALGO": 1, "KMG_DENSE_HALF": 1}]' >> "$OUT/ab.jsonl" 2>> "$OUT/ab.err" || { echo "ab failed"; tail -20 $OUT/ab.err; exit 1; }
+done
+python3 - "$OUT/ab.jsonl" <<'PY'
+import json, sys, collections
+d = collections.defaultdict(list)
+for l in open(sys.argv[1]):
+    r = json.loads(l); d[(json.dumps(r["cfg"]), json.dumps(r["env"]))].append(r["gram_ms"])
+for k, v in d.items(): print(k[0][:60], k[1], "min %.4f med %.4f" % (min(v), sorted(v)[len(v)//2]))
+PY
