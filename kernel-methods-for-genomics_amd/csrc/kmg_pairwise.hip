@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void gram_wd_kernel(SeqSpec q, int64_t row0, i
 // operations in the mask and k loop.  A pair holding a non-ACGT symbol (mask bit below
 // len) is compared byte by byte from the codes (rare; exact for any alphabet).  Tile: 64
 // columns (one per lane, planes in VGPRs) x 64 rows (16 per wave, planes read
-// wave-uniform from LDS).  MIRROR (full square K): only tiles J >= I run; an off-diagonal
+// wave-uniform from LDS, four rows a pass so a lane runs four independent chains).  MIRROR (full square K): only tiles J >= I run; an off-diagonal
 // tile also writes its transpose from an LDS copy, 64 coalesced 512-B rows.
 __device__ __forceinline__ uint32_t wd_keep(int lim, int w) {
   const int nv = min(max(lim - 32 * w, 0), 32);
@@ -289,44 +289,76 @@ __global__ __launch_bounds__(256) void gram_wdp_kernel(SeqSpec q, Packed pk, int
   }
   ky[0] &= 0x7FFFFFFFu;  // l >= 1
   const bool diag_tile = MIRROR && blockIdx.x == blockIdx.y;
-  for (int r = wave; r < RB; r += 4) {
-    const int64_t i = rbase + r;
-    if (i >= row1) break;
+  // match mask of (row r, this lane's column): A[w] (A_1 of the k recursion)
+  auto row_mask = [&](int r, int64_t i, uint32_t (&A)[NP]) {
     const int sl = __builtin_amdgcn_readfirstlane(slen[r]);
     const bool rbad = sl < 0;
     const int Lx = rbad ? -1 - sl : sl;
-    double val;
-    if (i == j) {
-      val = __dadd_rn((double)(Lx - 1), (double)(1 - d) / 3.0);  // kernels.py:96
+    if (rbad || cbad) {
+      const int lim = span > 0 ? min(min(Lx, Ly), span) : min(Lx, Ly);
+      wd_mask_bytes<NP>(q, i, jj, lim, A);
     } else {
-      uint32_t A[NP];
-      if (rbad || cbad) {
-        const int lim = span > 0 ? min(min(Lx, Ly), span) : min(Lx, Ly);
-        wd_mask_bytes<NP>(q, i, jj, lim, A);
-      } else {
 #pragma unroll
-        for (int w = 0; w < NP; ++w) {
-          const uint32_t kx = wd_keep(Lx, w);
-          const uint32_t v = (srow[r][w] ^ y1[w]) | (srow[r][NP + w] ^ y0[w]);
-          A[w] = (kx & ky[w]) & ~v;
-        }
-      }
-      val = 0.0;
-      for (int k = 1; k <= d; ++k) {
-        int c = 0;
-#pragma unroll
-        for (int w = 0; w < NP; ++w) c += __popc(A[w]);
-        if (!__any(c != 0)) break;
-        if (c) val = __dadd_rn(val, __dmul_rn(cf.a[k - 1], (double)c));
-#pragma unroll
-        for (int w = 0; w < NP; ++w) {
-          const uint32_t nxt = (w + 1 < NP) ? A[w + 1] : 0u;
-          A[w] &= __builtin_amdgcn_alignbit(A[w], nxt, 31);  // (A_w << 1) | (A_{w+1} >> 31)
-        }
+      for (int w = 0; w < NP; ++w) {
+        const uint32_t kx = wd_keep(Lx, w);
+        const uint32_t v = (srow[r][w] ^ y1[w]) | (srow[r][NP + w] ^ y0[w]);
+        A[w] = (kx & ky[w]) & ~v;
       }
     }
-    if (jin) store_f(o, i - row0, j, val);
-    if (MIRROR) tile[r][lane] = val;
+    return Lx;
+  };
+  {
+    // RP rows (r, r + 4, ...) per pass: RP independent shift / popcount / fp64 chains a lane
+    // (one row a pass: N=9000 d=4/5/10 0.221/0.234/0.270 -> 0.190/0.204/0.239 ms;
+    // profiles/r02bp_wd_rows_per_pass_ab.jsonl)
+    constexpr int RP = 4;
+    for (int r = wave; r < RB; r += 4 * RP) {
+      if (rbase + r >= row1) break;
+      uint32_t A[RP][NP];
+      int Lx[RP];
+      double val[RP];
+#pragma unroll
+      for (int u = 0; u < RP; ++u) {
+        const int64_t i = rbase + r + 4 * u;
+        val[u] = 0.0;
+        Lx[u] = 0;
+        if (i < row1) {
+          Lx[u] = row_mask(r + 4 * u, i, A[u]);
+        } else {
+#pragma unroll
+          for (int w = 0; w < NP; ++w) A[u][w] = 0u;
+        }
+      }
+      for (int k = 1; k <= d; ++k) {
+        int c[RP], any = 0;
+#pragma unroll
+        for (int u = 0; u < RP; ++u) {
+          c[u] = 0;
+#pragma unroll
+          for (int w = 0; w < NP; ++w) c[u] += __popc(A[u][w]);
+          any |= c[u];
+        }
+        if (!__any(any != 0)) break;
+        // a zero count adds +0.0: no rounding change
+#pragma unroll
+        for (int u = 0; u < RP; ++u) val[u] = __dadd_rn(val[u], __dmul_rn(cf.a[k - 1], (double)c[u]));
+#pragma unroll
+        for (int u = 0; u < RP; ++u)
+#pragma unroll
+          for (int w = 0; w < NP; ++w) {
+            const uint32_t nxt = (w + 1 < NP) ? A[u][w + 1] : 0u;
+            A[u][w] &= __builtin_amdgcn_alignbit(A[u][w], nxt, 31);  // (A_w << 1) | (A_{w+1} >> 31)
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < RP; ++u) {
+        const int64_t i = rbase + r + 4 * u;
+        if (i >= row1) break;
+        if (i == j) val[u] = __dadd_rn((double)(Lx[u] - 1), (double)(1 - d) / 3.0);  // kernels.py:96
+        if (jin) store_f(o, i - row0, j, val[u]);
+        if (MIRROR) tile[r + 4 * u][lane] = val[u];
+      }
+    }
   }
   if (MIRROR && !diag_tile) {
     __syncthreads();

@@ -20,6 +20,8 @@ def main():
     codes, lens = E.synthetic(n, 101, seed=cfg.get("seed", 2))
     if kind == "sp":
         p, dt = P.make(L.KMG_SPECTRUM, k=cfg.get("k", 8)), L.KMG_I32
+    elif kind == "wd":
+        p, dt = P.make(L.KMG_WD, d=cfg.get("d", 5)), L.KMG_F64
     else:
         norm = cfg.get("norm", 1)
         p = P.make(L.KMG_MISMATCH, k=cfg.get("k", 9), m=1, window=101, normalize=norm)
