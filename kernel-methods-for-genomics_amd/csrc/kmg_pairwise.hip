@@ -590,6 +590,14 @@ struct LaCoef {
   double inv_beta; // 1 / beta (the reference's (1/beta) * log(...))
 };
 
+// v from lane l - 1 (lanes 1..63; lane 0 gets 0): DPP wave_shr:1 on both halves, a VALU
+// move instead of the LDS-routed ds_bpermute that __shfl_up becomes
+__device__ __forceinline__ double wave_shr1(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 template <bool SMITH>
 __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, int64_t row1,
                                                       LaCoef cf, int mirror, OutSpec o) {
@@ -623,8 +631,8 @@ __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, i
     const bool store_row = (lane == 63) && (s0 + 64 <= nx);
     for (int st = 0; st <= ny + 63; ++st) {
       const int c = st - lane;
-      double uM = __shfl_up(lM, 1, 64), uX = __shfl_up(lX, 1, 64);
-      double uY = __shfl_up(lY, 1, 64), uX2 = __shfl_up(lX2, 1, 64);
+      double uM = wave_shr1(lM), uX = wave_shr1(lX);
+      double uY = wave_shr1(lY), uX2 = wave_shr1(lX2);
       if (lane == 0) {
         const bool rb = s0 > 0 && c >= 0 && c <= ny;
         uM = rb ? rowbuf[c] : 0.0;
