@@ -465,6 +465,14 @@ __global__ __launch_bounds__(256) void gram_wds_kernel(SeqSpec q, int64_t row0, 
   }
 }
 
+// v from lane l - 1 (lanes 1..63; lane 0 gets 0): DPP wave_shr:1 on both halves, a VALU
+// move instead of the LDS-routed ds_bpermute that __shfl_up becomes
+__device__ __forceinline__ double wave_shr1(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 // ------------------------------------------------------------------ SS (substring)
 // One wave per pair.  Bottom-up B_t(r, j) = B_t(x[:r], y[:j]) for t = 1..k-1 over an
 // anti-diagonal sweep: lane l of a 64-row strip owns row r, at step st it computes
@@ -516,7 +524,7 @@ __global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, i
         double up[KMAX - 1];
 #pragma unroll
         for (int t = 0; t < KMAX - 1; ++t) {
-          const double fromleft = __shfl_up(last[t], 1, 64);
+          const double fromleft = wave_shr1(last[t]);
           double u = fromleft;
           if (lane == 0) u = (s0 == 0 || jc < 0 || jc > ny) ? 0.0 : rowbuf[t * (ML + 1) + jc];
           up[t] = u;
@@ -589,14 +597,6 @@ struct LaCoef {
   double eo, ee;   // exp(-beta e), exp(-beta d)
   double inv_beta; // 1 / beta (the reference's (1/beta) * log(...))
 };
-
-// v from lane l - 1 (lanes 1..63; lane 0 gets 0): DPP wave_shr:1 on both halves, a VALU
-// move instead of the LDS-routed ds_bpermute that __shfl_up becomes
-__device__ __forceinline__ double wave_shr1(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
 
 template <bool SMITH>
 __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, int64_t row1,

@@ -20,6 +20,11 @@ def main():
     codes, lens = E.synthetic(n, 101, seed=cfg.get("seed", 2))
     if kind == "sp":
         p, dt = P.make(L.KMG_SPECTRUM, k=cfg.get("k", 8)), L.KMG_I32
+    elif kind == "ss":
+        p, dt = P.make(L.KMG_SUBSTRING, k=cfg.get("k", 5), lbda=cfg.get("lbda", 0.5)), L.KMG_F64
+    elif kind == "la":
+        p, dt = P.make(L.KMG_LOCALALIGN, smith=cfg.get("smith", 0), la_mode=L.KMG_LA_INTENDED,
+                       la_e=11, la_d=1, la_beta=0.5), L.KMG_F64
     elif kind == "wd":
         p, dt = P.make(L.KMG_WD, d=cfg.get("d", 5)), L.KMG_F64
     else:
