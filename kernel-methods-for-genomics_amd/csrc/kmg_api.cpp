@@ -99,7 +99,9 @@ enum {
 struct Tuning {
   int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
   int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
-  int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table
+  int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table,
+                            // 3 drop-two pair lines (kmg_pairs.hip)
+  int pl_depth = 4;         // KMG_PL_D: pair-lines Gram, ring steps in flight per wave (4/6/8)
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
@@ -141,6 +143,7 @@ void read_tuning(Tuning &t) {
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
+  t.pl_depth = env_or("KMG_PL_D", d.pl_depth);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
@@ -399,6 +402,26 @@ int diag_hamming(kmg_ctx *c, const IndexGeom &g, const Packed &pk) {
   return KMG_OK;
 }
 
+// Max symbol code and min length over the device-resident rows (one small kernel and a
+// stream sync; only the kernels that need it call this).
+int row_stats(kmg_ctx *c, const uint8_t *d_codes, const int32_t *d_lens, int64_t n, int64_t ldc,
+              uint32_t &max_code, uint32_t &min_len) {
+  max_code = 0;
+  min_len = 0;
+  if (n <= 0) return KMG_OK;
+  KMG_TRY(c->ovf.ensure(4 * sizeof(uint32_t)));
+  const uint32_t init[2] = {0u, 0xFFFFFFFFu};
+  KMG_HIP(hipMemcpyAsync(c->ovf.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+  SeqSpec q{d_codes, d_lens, n, ldc, 0};
+  KMG_HIP(launch_row_stats(q, c->ovf.as<uint32_t>(), c->stream));
+  uint32_t st[2];
+  KMG_HIP(hipMemcpyAsync(st, c->ovf.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  max_code = st[0];
+  min_len = st[1];
+  return KMG_OK;
+}
+
 // ----------------------------------------------------------------- dense formulation
 // xor masks of every k-mer within Hamming distance m of a k-mer (2-bit letters; a
 // non-zero xor of a letter is one of the 3 other letters): sum_{t<=m} C(k,t) 3^t masks.
@@ -466,6 +489,46 @@ int pair_chunk(int64_t n, int pmax, int k, int cap) {
     }
   }
   return (int)std::max<int64_t>(8, (best + 7) & ~7LL);
+}
+
+// Columns per chunk of the pair-lines table (kmg_pairs.hip): the fewest expected 128-byte
+// lines per row window, nch x (uniform pairs E[ceil(X / 64)] + k correction pairs
+// E[ceil((8 + X) / 64)]), X ~ Poisson(chunk * pmax / 4^(k-2)), over the chunkings whose
+// int32 LDS accumulator fits beside the kernel's wave queues and whose per-chunk table
+// stays Infinity-Cache sized (<= 192 MB: the chunk-major grid reads one chunk's table at a
+// time, and the K rows stream past it).
+int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
+  const double keys = (double)pow4(k - 2);
+  const int np = k * (k - 1) / 2;
+  int64_t max_chunk = (160 * 1024 / 4 - 66 - pmax - ldp - KMG_PAIRS_MAX - 16 * KMG_PL_WAVE_WORDS) & ~7LL;
+  max_chunk = std::min<int64_t>(max_chunk, 65536 - 64);
+  if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
+  if (max_chunk < 8) return 8;
+  const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
+  int64_t best = std::min<int64_t>(std::max<int64_t>(n, 8), max_chunk);
+  double best_lines = 1e300;
+  for (int64_t nch = nch0; nch <= nch0 + 64; ++nch) {
+    const int64_t ch = ((n + nch - 1) / nch + 7) & ~7LL;
+    if (ch > max_chunk) continue;
+    const double mean = (double)ch * pmax / keys;
+    double eu = 0.0, ec = 0.0, pr = std::exp(-mean), cdf = 0.0;
+    for (int x = 0; x < 4000 && cdf < 1.0 - 1e-12; ++x) {
+      if (x > 0) pr *= mean / x;
+      cdf += pr;
+      if (x > 0) {
+        eu += pr * std::ceil(x / 64.0);
+        ec += pr * std::ceil((8.0 + x) / 64.0);
+      }
+    }
+    const double per = (np - k) * eu + k * ec;  // lines per window and chunk
+    const double table = per * keys * 128.0;      // bytes of one chunk's table
+    if (table > 192e6 && nch < nch0 + 64) continue;
+    if (nch * per < best_lines - 1e-9) {
+      best_lines = nch * per;
+      best = ch;
+    }
+  }
+  return (int)std::max<int64_t>(8, best);
 }
 
 // Columns per chunk of the drop-one slot table.  A row reads one 128-byte line per
@@ -676,7 +739,7 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 // ----------------------------------------------------------------- dispatch
 // Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
 // kmg_gram_blocks' choice of the round-slab format).
-enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS };
+enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL };
 SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
@@ -687,9 +750,11 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax) {
   // profiles/r02_mm_pmc.txt); at k = 12 the 66 x 4^10 pair groups cost more to build.
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
-  const bool use_pairs = s1 && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
-  const bool use_slots = s1 && !use_pairs && k >= 8 && k <= 12 && form != 2;
-  const bool use_index = (exact && k <= 12) || use_slots || use_pairs;
+  const bool use_pl = s1 && form == 3 && k >= 3 && k <= 12;
+  const bool use_pairs =
+      s1 && !use_pl && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
+  const bool use_slots = s1 && !use_pairs && !use_pl && k >= 8 && k <= 12 && form != 2;
+  const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_pl;
   // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
   // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
   // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
@@ -700,6 +765,7 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax) {
     return SM_DENSE;  // (algo 1 without dense_ok: gram_device reports it)
   if (!use_index) return SM_HAMMING;
   if (use_pairs) return SM_PAIRS;
+  if (use_pl) return SM_PL;
   return exact ? SM_POSTING : SM_SLOTS;
 }
 
@@ -756,8 +822,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const SmPath path = sm_path(c->tune, p, g.pmax);
-      const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
-      const bool use_index = path == SM_POSTING || use_slots || use_pairs;
+      const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS, use_pl = path == SM_PL;
+      const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl;
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       const int mm_eff = mm ? std::min(p->m, k) : 0;
@@ -861,6 +927,63 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                              r1, (int)w[0], (int)w[1], (int)w[2], oq, c->stream);
         }, true);
       }
+      if (use_pl) {
+        // exact k-mer index over the mismatch window (kernels.py:171), then the pair-lines
+        // table assembled from it (kmg_pairs.hip): uniform pairs first, then the k
+        // correction pairs G(r) = {r-1, r} (r >= 1) and {0, k-1} (outer letter k-1)
+        g.copies = 1;
+        g.nkeys = (uint32_t)pow4(k);
+        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk));
+        KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
+        PairGeom pg{};
+        pg.k = k;
+        pg.nchunks = g.nchunks;
+        pg.chunk = g.chunk;
+        pg.nkeys2 = (uint32_t)pow4(k - 2);
+        auto is_corr = [k](int pp, int qq) { return qq == pp + 1 || (pp == 0 && qq == k - 1); };
+        for (int pp = 0; pp < k; ++pp)
+          for (int qq = pp + 1; qq < k; ++qq)
+            if (!is_corr(pp, qq)) pg.pq[pg.npairs++] = (uint16_t)(pp | (qq << 8));
+        pg.corr0 = pg.npairs;
+        pg.pq[pg.npairs++] = (uint16_t)(0 | ((k - 1) << 8) | KMG_PL_OUTER_Q);  // r = 0
+        for (int r = 1; r < k; ++r) pg.pq[pg.npairs++] = (uint16_t)((r - 1) | (r << 8));
+        const int64_t nrec = pg.nrec();
+        const int64_t nlines = pl_lines_bound(pg, n * g.pmax);
+        if (nlines * 128 >= 0xFFFFFFF0LL || nlines >= (1LL << 28))
+          return fail(KMG_EUNSUPPORTED, "pair-lines table too large for 32-bit offsets");
+        KMG_TRY(c->pr_summary.ensure(sizeof(uint32_t) * 8 * (size_t)nrec));
+        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
+        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nrec)));
+        KMG_TRY(c->pr_lines.ensure((size_t)nlines * 128));
+        {
+          StageTimer t(c, ST_SLOTS);
+          KMG_HIP(launch_pl_count(pg, c->off.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
+                                  c->pr_rtot.as<uint32_t>(), c->stream));
+          KMG_HIP(launch_scan(c->pr_rtot.as<uint32_t>(), c->pr_rbase.as<uint32_t>(),
+                              c->pr_cursor.as<uint32_t>(), nrec, c->partials.as<uint32_t>(),
+                              c->stream));
+          KMG_HIP(launch_pl_pack(pg, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                 c->pr_rbase.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
+                                 c->pr_lines.as<uint4>(), c->stream));
+        }
+        if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
+          KMG_TRY(upload_wtab(c, w));
+          KMG_TRY(diag_hamming(c, g, pkd));
+          if (p->normalize) {
+            o.normalize = 1;
+            o.diagv = c->diagv.as<double>();
+            o.dsq = c->dsq.as<double>();
+          }
+        }
+        return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          return launch_gram_mismatch1_pl(pg, g, pkd, c->pr_summary.as<uint32_t>(),
+                                          c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
+                                          c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
+                                          (int)w[2], oq, c->stream, c->tune.pl_depth);
+        }, true);
+      }
       if (exact) {
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
@@ -904,6 +1027,16 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
       if (p->span < 0) return fail(KMG_EINVAL, "span < 0");
+      if (p->span > 0) {
+        // the kernels count positions below min(len_x, len_y, span): a span past a row's
+        // end would miss the reference's clipped-slice matches (kernels.py:75-80, 127-134)
+        uint32_t mc = 0, ml = 0;
+        KMG_TRY(row_stats(c, d_codes, d_lens, n, ldc, mc, ml));
+        const int64_t need = (int64_t)p->span + (p->kind == KMG_WDS ? p->S : 0);
+        if (n > 0 && need > (int64_t)ml)
+          return fail(KMG_EUNSUPPORTED, "WD/WDS: span %d%s exceeds the shortest row (%u); pad the rows",
+                      p->span, p->kind == KMG_WDS ? " + S" : "", ml);
+      }
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
       Packed pkd{nullptr, 0, 0};
       const bool packed_wd = p->kind == KMG_WD && c->tune.wd_form == 0 && maxlen <= 256 &&
@@ -961,6 +1094,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // bounds and gap signs fixed; gram_la_kernel): parity unpinned
         if (!(p->la_beta > 0.0)) return fail(KMG_EINVAL, "LA: beta must be > 0");
         if (maxlen > 1024) return fail(KMG_EUNSUPPORTED, "LA: sequences longer than 1024");
+        {  // the substitution matrix S covers A, C, G, T only (kernels.py:223)
+          uint32_t mc = 0, ml = 0;
+          KMG_TRY(row_stats(c, d_codes, d_lens, n, ldc, mc, ml));
+          if (mc > 3) return fail(KMG_EINVAL, "LA: symbol other than A/C/G/T (code %u)", mc);
+        }
         SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
         bool unsupported = false;
         const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
@@ -1185,10 +1323,17 @@ int kmg_gram_to_host(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     }
     return KMG_OK;
   };
-  KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, n, after));
-  KMG_TRY(copy_out(ranges.size() - 1));
-  KMG_HIP(hipStreamSynchronize(c->d2h_stream));
-  KMG_HIP(hipStreamSynchronize(c->stream));
+  const int rc = [&]() -> int {
+    KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, out_dtype, n, after));
+    return copy_out(ranges.size() - 1);
+  }();
+  // on every exit path: no slab copy into the caller's buffer may still be running when
+  // this returns (a failed call's caller may unmap the buffer right away)
+  const hipError_t e_d2h = hipStreamSynchronize(c->d2h_stream);
+  const hipError_t e_ctx = hipStreamSynchronize(c->stream);
+  if (rc != KMG_OK) return rc;
+  KMG_HIP(e_d2h);
+  KMG_HIP(e_ctx);
   return KMG_OK;
 }
 

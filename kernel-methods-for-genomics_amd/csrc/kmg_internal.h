@@ -129,7 +129,8 @@ struct PairGeom {
   int nchunks;
   int chunk;
   uint32_t nkeys2;                 // 4^(k-2)
-  uint16_t pq[KMG_PAIRS_MAX];      // p | q << 8
+  uint16_t pq[KMG_PAIRS_MAX];      // p | q << 8 (pair lines: | KMG_PL_OUTER_Q, see below)
+  int corr0 = 0;                   // pair lines: first correction pair (kmg_pairs.hip)
   __host__ __device__ int64_t ngroups() const { return (int64_t)npairs * nchunks * nkeys2; }
   __host__ __device__ int64_t nrec() const { return (ngroups() + 31) / 32; }
 };
@@ -164,6 +165,30 @@ inline int64_t pair_lines_bound(const PairGeom &pg, int64_t occurrences) {
   const int64_t entries = (int64_t)pg.npairs * occurrences;
   const int64_t nonempty = pg.ngroups() < entries ? pg.ngroups() : entries;
   return nonempty + nonempty / 8 + 2 * entries / 128 + 64;
+}
+
+// ---------------------------------------------------------------- pair lines (kmg_pairs.hip)
+// Drop-two table, second layout.  Pairs are ordered "uniform" first, then the k
+// correction pairs (index corr0 + r for r = 0..k-1): pair {r-1, r} with outer letter r-1
+// (r >= 1) and pair {0, k-1} with outer letter k-1 (r = 0, flag KMG_PL_OUTER_Q).
+//   uniform group: n uint16 columns, no header, padded to nl = ceil(n / 64) lines with
+//     dummy columns (64 LDS words past the accumulator); every entry weighs w2.
+//   correction group: 16-byte header of sub-bin ends (bytes, sub-bin = z_outer * 4 +
+//     z_inner), then the entries in sub-bin order, nl = ceil((8 + n) / 64) lines.
+// Summary record per 32 groups (8 dwords): w0 base line, w1..w4 4-bit line counts,
+// w5 "wide" bits (group too large for lines: read from the exact index instead).
+#define KMG_PL_OUTER_Q 0x80
+#define KMG_PL_MAXNL 14
+#define KMG_PL_WAVE_WORDS 1024  // LDS words of one wave's line ring (gram_pl_kernel)
+hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
+                           uint32_t *rtot, hipStream_t s);
+hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
+                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, hipStream_t s);
+// upper bound of the line count of the pair-lines table
+inline int64_t pl_lines_bound(const PairGeom &pg, int64_t occurrences) {
+  const int64_t entries = (int64_t)pg.npairs * occurrences;
+  const int64_t nonempty = pg.ngroups() < entries ? pg.ngroups() : entries;
+  return nonempty + entries / 64 + 65;  // + the dummy line 0
 }
 
 // ---------------------------------------------------------------- Gram kernels
@@ -211,6 +236,12 @@ hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, c
                                        int64_t nlines, const uint32_t *xoff, const uint16_t *xent,
                                        int64_t row0, int64_t row1, int w0, int w1, int w2,
                                        const OutSpec &o, hipStream_t s);
+// mismatch (k, 1), 3 <= k <= 12, on the pair-lines table; xoff / xent = exact index
+hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, const Packed &pk,
+                                    const uint32_t *summary, const uint4 *lines, int64_t nlines,
+                                    const uint32_t *xoff, const uint16_t *xent, int64_t row0,
+                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                    hipStream_t s, int depth = 4);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
@@ -237,6 +268,9 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
 // LA kernel, intended semantics (KMG_LA_INTENDED): five-array affine-gap DP per pair
 hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
                           double beta, int smith, int mirror, const OutSpec &o, hipStream_t s);
+// stats[0] = max code over every row's first len symbols, stats[1] = min len (preset to 0 /
+// UINT_MAX by the caller)
+hipError_t launch_row_stats(const SeqSpec &q, uint32_t *stats, hipStream_t s);
 hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int window,
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);

@@ -1,0 +1,663 @@
+// kmg_pairs.hip — mismatch (k, 1) Gram through the drop-two "pair lines" table, gfx950.
+//
+// Reference hot loops replaced (afiliot/Kernel-Methods-For-Genomics kernels.py):
+//   get_phi_km (kernels.py:161-175) + the get_mismatch_K pair loop (kernels.py:211-215)
+//   + normalize_K (kernels.py:398-415, fused epilogue).
+// Closed form: K(x, y) = sum_{a,b} w[ham(x_a, y_b)], w = (1 + 3k, 4, 2, 0, ...).
+//
+// Table.  For a pair of positions {p, q} and a k-mer z, key_pq(z) = z without letters p and
+// q.  The group (pair, column chunk, key) lists every occurrence that agrees with the key:
+// for a row k-mer u, group (pq, key_pq(u)) holds every Hamming <= 2 neighbour of u whose
+// differences lie inside {p, q}.  Weights (an inclusion-exclusion that leaves most groups
+// with ONE weight for every entry, so they need no per-entry test and no header):
+//   every entry of every group: w2.  A Hamming-2 neighbour at {a, b} lies in group {a, b}
+//     only; a Hamming-1 neighbour at r in the k-1 groups holding r; u itself in all
+//     k(k-1)/2 groups.
+//   correction groups (k of them, one per position r): group G(r) = {r-1, r} (r >= 1) or
+//     {0, k-1} (r = 0), its sub-bins sorted by the OTHER ("outer") letter first.  The row
+//     z_outer = u_outer of G(r) is u's exact bin plus the Hamming-1 neighbours at r:
+//       Hamming-1 entries there get c = w1 - (k-1) w2 on top of w2,
+//       the exact bin gets h0 = w0 - k(k-1)/2 w2 in G(1) only (0 elsewhere).
+//   Net: w[ham] for every Hamming <= 2 neighbour (checked against the oracle bit for bit).
+// Uniform groups are n columns padded to whole 128-byte lines with dummy columns (64 LDS
+// words past the accumulator); correction groups carry a 16-byte header of sub-bin ends.
+//
+// Gram kernel.  One 1024-thread workgroup per (row, column chunk), int32 LDS accumulator.
+// Each wave turns batches of 64 lists (one per lane: pair, row window) into a ring of line
+// entries in LDS (group line ranges from the L2-resident summary, prefetched one batch
+// ahead; a wave prefix sum places them) and streams the ring 8 lines per wave-instruction:
+// lane j of an 8-lane group loads 16-byte piece j of its line and adds w2 for its 8 columns
+// (SDWA address + ds_add each); steps holding correction lines take the per-halfword
+// weights; oversized groups a per-lane path.
+#include "kmg_internal.h"
+#include "kmg_rowacc.h"
+
+namespace kmg {
+
+namespace {
+
+constexpr uint32_t PL_WIDE = 0xFFFFFFFFu;
+
+// lines of a group of n entries; PL_WIDE: read from the exact index instead
+__host__ __device__ __forceinline__ uint32_t pl_lines(uint32_t n, bool corr) {
+  if (n == 0) return 0;
+  if (corr) return n > 255u ? PL_WIDE : (8u + n + 63u) / 64u;
+  const uint32_t l = (n + 63u) / 64u;
+  return l > (uint32_t)KMG_PL_MAXNL ? PL_WIDE : l;
+}
+
+__device__ __forceinline__ void pl_decode_group(const PairGeom &pg, int64_t g, int &pi, int &p,
+                                                int &q, int &c, uint32_t &key) {
+  key = (uint32_t)(g % pg.nkeys2);
+  const int64_t pc = g / pg.nkeys2;  // pair * nchunks + chunk
+  c = (int)(pc % pg.nchunks);
+  pi = (int)(pc / pg.nchunks);
+  p = pg.pq[pi] & 0xF;
+  q = (pg.pq[pi] >> 8) & 0xF;
+}
+
+// (z_p, z_q) of sub-bin b of a group: outer letter first for correction groups
+__device__ __forceinline__ void pl_subbin(int b, bool corr, bool outer_q, uint32_t &zp,
+                                          uint32_t &zq) {
+  const uint32_t hi = (uint32_t)b >> 2, lo = (uint32_t)b & 3u;
+  if (corr && outer_q) {
+    zq = hi;
+    zp = lo;
+  } else {
+    zp = hi;
+    zq = lo;
+  }
+}
+
+__device__ __forceinline__ uint32_t nib_sum(uint32_t x) {
+  const uint32_t y = (x & 0x0F0F0F0Fu) + ((x >> 4) & 0x0F0F0F0Fu);
+  return (y * 0x01010101u) >> 24;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ table build
+// one thread per 8 groups (one nibble word of a summary record); 4 threads per record
+__global__ __launch_bounds__(256) void pl_count_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
+                                                       uint32_t *__restrict__ summary,
+                                                       uint32_t *__restrict__ rtot) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nrec = pg.nrec();
+  const bool live = t < nrec * 4;
+  uint32_t word = 0, tot = 0, wide = 0;
+  if (live) {
+    const int64_t g0 = (t >> 2) * 32 + (t & 3) * 8;
+    for (int r = 0; r < 8; ++r) {
+      const int64_t g = g0 + r;
+      if (g >= pg.ngroups()) break;
+      int pi, p, q, c;
+      uint32_t key;
+      pl_decode_group(pg, g, pi, p, q, c, key);
+      const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
+      uint32_t n = 0;
+      for (uint32_t b = 0; b < 16; ++b) {
+        const uint32_t z = pair_insert(key, pg.k, p, q, b >> 2, b & 3u);
+        n += xo[z + 1] - xo[z];
+      }
+      const uint32_t nl = pl_lines(n, pi >= pg.corr0);
+      if (nl == PL_WIDE) {
+        wide |= 1u << (8 * (t & 3) + r);
+      } else {
+        word |= nl << (4 * r);
+        tot += nl;
+      }
+    }
+    summary[(t >> 2) * 8 + 1 + (t & 3)] = word;
+  }
+  // record totals and wide bits over its 4 threads (adjacent lanes)
+  tot += __shfl_xor(tot, 1, 64);
+  tot += __shfl_xor(tot, 2, 64);
+  wide |= __shfl_xor(wide, 1, 64);
+  wide |= __shfl_xor(wide, 2, 64);
+  if (live && (t & 3) == 0) {
+    rtot[t >> 2] = tot;
+    summary[(t >> 2) * 8 + 5] = wide;
+  }
+}
+
+// Bank-sorted lines.  A line's dword d holds two columns of LDS bank pl_bank(d) (column mod
+// 32 with the accumulator at LDS offset 0).  The Gram kernel's lane j of 8-lane group s
+// (s = 0..3 inside each half-wave) adds, at instruction v, the columns of dword
+// 4 j + ((v / 2 + s) mod 4) of its line, i.e. bank 8 ((v / 2 + s) mod 4) + j: the 32 lanes
+// of a half-wave hit 32 distinct banks, so the ds_add of uniform lines runs without bank
+// conflicts.  A group's columns beyond two per bank and line (Poisson tail) fill the free
+// slots of other banks; unused slots hold a dummy column of the slot's bank.
+__host__ __device__ __forceinline__ uint32_t pl_bank(uint32_t d) { return 8u * (d & 3u) + (d >> 2); }
+__host__ __device__ __forceinline__ uint32_t pl_dword(uint32_t bank) {
+  return 4u * (bank & 7u) + (bank >> 3);
+}
+// dummy column of bank `bank` (two per bank: half h = 0, 1) in the 64 words past the accumulator
+__device__ __forceinline__ uint32_t pl_dummy(uint32_t dcol, uint32_t bank, uint32_t h) {
+  return dcol + ((bank - dcol) & 31u) + 32u * h;
+}
+
+// 16 lanes per group (lane b = sub-bin b), 16 groups per block.  The group's lines are
+// assembled in an LDS image and written with 16-byte stores.  Correction groups: header
+// bytes, then the entries in sub-bin order.  Uniform groups: bank-sorted in two passes
+// (every lane issues PL_PACK_U entry loads before using any): pass 1 counts the columns per
+// bank; the free slots per bank (two per line) are prefix-summed; pass 2 puts a column of
+// rank < 2 nl into its bank's slot and the Poisson tail into the free slots of other banks,
+// in bank order.
+constexpr int PL_PACK_GROUPS = 16;
+constexpr int PL_IMG_WORDS = KMG_PL_MAXNL * 32;
+constexpr int PL_PACK_U = 8;  // entry loads in flight per lane
+__global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
+                                                      const uint16_t *__restrict__ xent,
+                                                      const uint32_t *__restrict__ rbase,
+                                                      uint32_t *__restrict__ summary,
+                                                      uint4 *__restrict__ lines) {
+  __shared__ __align__(16) uint32_t img[PL_PACK_GROUPS][PL_IMG_WORDS];
+  __shared__ uint32_t hist[PL_PACK_GROUPS][32];   // columns per bank (pass 1)
+  __shared__ uint32_t rank[PL_PACK_GROUPS][32];   // running rank per bank (pass 2)
+  __shared__ uint32_t freeb[PL_PACK_GROUPS][33];  // exclusive prefix of the free slots per bank
+  __shared__ uint32_t novf[PL_PACK_GROUPS];       // columns placed into other banks' slots
+  const int lg = threadIdx.x >> 4, b = threadIdx.x & 15;
+  const int64_t g = (int64_t)blockIdx.x * PL_PACK_GROUPS + lg;
+  const bool live = g < pg.ngroups();
+  // line 0 is the dummy line (read for empty ring entries): group bases start at 1
+  if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5] + 1u;
+  const uint32_t dcol = (uint32_t)(((pg.chunk + 3) >> 2) << 2);
+  uint32_t s0 = 0, cnt = 0;
+  bool corr = false;
+  if (live) {
+    int pi, p, q, c;
+    uint32_t key;
+    pl_decode_group(pg, g, pi, p, q, c, key);
+    corr = pi >= pg.corr0;
+    uint32_t zp, zq;
+    pl_subbin(b, corr, (pg.pq[pi] & KMG_PL_OUTER_Q) != 0, zp, zq);
+    const uint32_t z = pair_insert(key, pg.k, p, q, zp, zq);
+    const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
+    s0 = xo[z];
+    cnt = xo[z + 1] - s0;
+  }
+  uint32_t end = cnt;  // inclusive scan of the 16 sub-bin counts
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const uint32_t v = __shfl_up(end, d, 16);
+    if (b >= d) end += v;
+  }
+  const uint32_t n = __shfl(end, 15, 16);
+  const uint32_t nl = live ? pl_lines(n, corr) : 0u;
+  const bool pack = live && nl != PL_WIDE && n > 0;
+  hist[lg][b] = 0;
+  hist[lg][b + 16] = 0;
+  rank[lg][b] = 0;
+  rank[lg][b + 16] = 0;
+  if (b == 0) novf[lg] = 0;
+  for (int w = b; w < (int)(pack ? nl * 32 : 0); w += 16) {
+    const uint32_t bk = pl_bank((uint32_t)w & 31u);
+    img[lg][w] = pl_dummy(dcol, bk, 0) | (pl_dummy(dcol, bk, 1) << 16);
+  }
+  uint32_t base = 0;
+  if (live) {
+    const int64_t rec = g >> 5;
+    const int r = (int)(g & 31);
+    base = rbase[rec] + 1u;
+    for (int j = 0; j < r; ++j) base += (summary[rec * 8 + 1 + (j >> 3)] >> (4 * (j & 7))) & 15u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
+    uint32_t w[4];
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t bk = pl_bank(4u * threadIdx.x + q);
+      w[q] = pl_dummy(dcol, bk, 0) | (pl_dummy(dcol, bk, 1) << 16);
+    }
+    lines[threadIdx.x] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __syncthreads();
+  uint16_t *im16 = (uint16_t *)img[lg];
+  const uint32_t cap = 2u * nl;  // slots per bank and group
+  auto slot = [&](uint32_t bk, uint32_t rk) { return 64u * (rk >> 1) + 2u * pl_dword(bk) + (rk & 1u); };
+  // this lane's run: entries [s0, s0 + cnt) of the exact index, group positions end - cnt + e
+  auto for_run = [&](auto &&f) {
+    for (uint32_t e0 = 0; e0 < cnt; e0 += PL_PACK_U) {
+      uint32_t col[PL_PACK_U];
+#pragma unroll
+      for (int u = 0; u < PL_PACK_U; ++u)
+        col[u] = e0 + u < cnt ? (uint32_t)xent[s0 + e0 + u] : 0xFFFFFFFFu;
+#pragma unroll
+      for (int u = 0; u < PL_PACK_U; ++u)
+        if (col[u] != 0xFFFFFFFFu) f(end - cnt + e0 + u, col[u]);
+    }
+  };
+  if (pack && corr) {
+    ((uint8_t *)img[lg])[b] = (uint8_t)end;
+    for_run([&](uint32_t pos, uint32_t col) { im16[8u + pos] = (uint16_t)col; });
+  }
+  if (pack && !corr) for_run([&](uint32_t, uint32_t col) { atomicAdd(&hist[lg][col & 31u], 1u); });
+  __syncthreads();
+  if (pack && !corr) {  // free slots per bank, exclusive prefix in bank order
+    const uint32_t flo = cap - min(hist[lg][b], cap), fhi = cap - min(hist[lg][b + 16], cap);
+    uint32_t ilo = flo, ihi = fhi;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint32_t vl = __shfl_up(ilo, d, 16), vh = __shfl_up(ihi, d, 16);
+      if (b >= d) {
+        ilo += vl;
+        ihi += vh;
+      }
+    }
+    const uint32_t tlo = __shfl(ilo, 15, 16);
+    freeb[lg][b] = ilo - flo;
+    freeb[lg][b + 16] = tlo + ihi - fhi;
+    if (b == 15) freeb[lg][32] = tlo + ihi;
+  }
+  __syncthreads();
+  if (pack && !corr)
+    for_run([&](uint32_t, uint32_t col) {
+      const uint32_t bk = col & 31u;
+      const uint32_t rk = atomicAdd(&rank[lg][bk], 1u);
+      if (rk < cap) {
+        im16[slot(bk, rk)] = (uint16_t)col;
+        return;
+      }
+      // the o-th column past its bank's slots takes the o-th free slot
+      const uint32_t o = atomicAdd(&novf[lg], 1u);
+      uint32_t lo = 0;
+#pragma unroll
+      for (int t = 16; t >= 1; t >>= 1)
+        if (lo + t < 32u && freeb[lg][lo + t] <= o) lo += t;
+      im16[slot(lo, min(hist[lg][lo], cap) + (o - freeb[lg][lo]))] = (uint16_t)col;
+    });
+  __syncthreads();
+  if (pack)
+    for (uint32_t w = b; w < nl * 8; w += 16) lines[(size_t)base * 8 + w] = ((const uint4 *)img[lg])[w];
+}
+
+hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
+                           uint32_t *rtot, hipStream_t s) {
+  const int64_t threads = pg.nrec() * 4;
+  if (threads == 0) return hipSuccess;
+  hipLaunchKernelGGL(pl_count_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, pg,
+                     xoff, summary, rtot);
+  return hipGetLastError();
+}
+
+hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
+                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, hipStream_t s) {
+  const int64_t blocks = (pg.ngroups() + PL_PACK_GROUPS - 1) / PL_PACK_GROUPS;
+  if (blocks == 0) return hipSuccess;
+  if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
+  hipLaunchKernelGGL(pl_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent, rbase,
+                     summary, lines);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ Gram kernel
+namespace {
+constexpr int PL_QU = 3;  // lines of a uniform list through the ring (more: per-lane path)
+constexpr int PL_QC = 4;  // ... of a correction list
+constexpr int PL_RING = KMG_PL_WAVE_WORDS / 2;  // ring entries (uint2) per wave
+// ring entry: x = line index | flags, y = correction ranges (4 bytes, halfwords of the line)
+constexpr uint32_t RE_EMPTY = 0x80000000u, RE_CORR = 0x40000000u, RE_HDR = 0x20000000u,
+                   RE_DESIG = 0x10000000u, RE_LINE = 0x0FFFFFFFu;
+
+__device__ __forceinline__ void lds_add(uint32_t ad, int w) {
+  __hip_atomic_fetch_add((__attribute__((address_space(3))) int32_t *)(uintptr_t)ad, w,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// 8 columns (one 16-byte piece) + weight w each
+__device__ __forceinline__ void add_piece(const uint4 &x, int w) {
+  lds_add(col_addr_sdwa<0>(x.x), w);
+  lds_add(col_addr_sdwa<1>(x.x), w);
+  lds_add(col_addr_sdwa<0>(x.y), w);
+  lds_add(col_addr_sdwa<1>(x.y), w);
+  lds_add(col_addr_sdwa<0>(x.z), w);
+  lds_add(col_addr_sdwa<1>(x.z), w);
+  lds_add(col_addr_sdwa<0>(x.w), w);
+  lds_add(col_addr_sdwa<1>(x.w), w);
+}
+__device__ __forceinline__ uint32_t hdr_byte(const uint4 &h, int b) {
+  const int q = b >> 2;
+  const uint32_t w = q == 0 ? h.x : q == 1 ? h.y : q == 2 ? h.z : h.w;
+  return (w >> (8 * (b & 3))) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t hdr_start(const uint4 &h, int b) {
+  return b == 0 ? 0u : hdr_byte(h, b - 1);
+}
+__device__ __forceinline__ uint4 load_piece(__amdgpu_buffer_rsrc_t rl, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rl, off, 0, 0));
+}
+__device__ __forceinline__ uint32_t clamp64(int x) { return (uint32_t)min(64, max(0, x)); }
+// the dwords of a piece rotated by s (lane slot inside its half-wave): x'[q] = x[(q + s) mod 4]
+__device__ __forceinline__ uint4 rot4(const uint4 &x, bool s1, bool s2) {
+  const uint4 a = s1 ? make_uint4(x.y, x.z, x.w, x.x) : x;
+  return s2 ? make_uint4(a.z, a.w, a.x, a.y) : a;
+}
+}  // namespace
+
+// Per wave: a ring of line entries in LDS.  produce() turns the next batch of 64 lists
+// (one per lane) into ring entries: the group's line range from the summary record loaded
+// one batch earlier, a wave prefix sum of the line counts, one entry per line; a
+// correction list's header (sub-bin ends) is loaded at one call and its lines entered at
+// the next, with the halfword ranges of the row z_outer = u_outer and of the exact bin.
+// The consumer keeps PL_D steps of 8 lines in flight (lane j of 8-lane group g loads
+// 16-byte piece j of the step's line g) and adds w2 per column, or the per-halfword
+// weight when the step holds correction lines.
+template <int K, int PL_D>
+__global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g, Packed pk,
+                                                       const uint32_t *__restrict__ summary,
+                                                       const uint4 *__restrict__ lines,
+                                                       uint32_t line_bytes,
+                                                       const uint32_t *__restrict__ xoff,
+                                                       const uint16_t *__restrict__ xent,
+                                                       int64_t row0, int64_t rows, int w0, int w1,
+                                                       int w2, OutSpec o) {
+  constexpr int NP = K * (K - 1) / 2;
+  constexpr uint32_t NK2 = 1u << (2 * (K - 2));
+  // one dynamic LDS block, accumulator first (col_addr_sdwa: acc at LDS offset 0)
+  extern __shared__ __align__(16) uint32_t smem[];
+  const int c = (int)(blockIdx.x / rows);
+  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  const int64_t i = row0 + il;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;          // [accw] + 64 dummy words
+  uint32_t *rowk = smem + accw + 64;       // [P] row k-mers (KMG_INVALID: skipped)
+  uint32_t *srec = rowk + P;               // packed row record
+  uint32_t *spq = srec + pk.ldp;           // [NP] pair descriptors
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
+  // this wave's ring (8-byte aligned: the block's word count before it is even)
+  const int ring_off = (accw + 64 + P + (int)pk.ldp + KMG_PAIRS_MAX + 1) & ~1;
+  uint2 *ring = (uint2 *)(smem + ring_off) + wave * PL_RING;
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2) + 16; w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  stage_record(pk, i, srec);
+  if (threadIdx.x < NP) spq[threadIdx.x] = pg.pq[threadIdx.x];
+  __syncthreads();
+  for (int a = threadIdx.x; a < P; a += blockDim.x) rowk[a] = pk_window(srec, pk.cw, a, K);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void *)lines, (short)0, (int)line_bytes, 0x00020000);
+  const int total = NP * P;
+  const int nbatch = (total + 63) / 64;
+  const uint32_t chunk_base = (uint32_t)c * NK2;
+  const uint32_t pair_stride = (uint32_t)g.nchunks * NK2;
+  const int cc = w1 - (K - 1) * w2;  // Hamming 1, on top of the w2 of its K-1 groups
+  const int h0 = w0 - NP * w2;       // Hamming 0, on top of the w2 of all NP groups
+  const int g8 = lane >> 3, j8 = lane & 7;
+  const uint32_t dcol = (uint32_t)accw;  // first dummy column
+
+  // list L = batch * 64 + lane -> group index and meta: bit 0 valid, bit 1 correction,
+  // bits 2-3 u_outer, bits 4-5 u_inner, bit 6 designated (G(1): Hamming-0 weight),
+  // bits 8-11 p, bits 12-15 q, bit 16 outer = q
+  auto describe = [&](int batch, uint32_t &gidx, uint32_t &meta) {
+    const int L = batch * 64 + lane;
+    const bool in = L < total;
+    const int pi = in ? L / P : 0;
+    const int a = in ? L - pi * P : 0;
+    const uint32_t pq = spq[pi];
+    const int p = pq & 0xF, q = (pq >> 8) & 0xF;
+    const bool oq = (pq & KMG_PL_OUTER_Q) != 0;
+    const uint32_t u = rowk[a];
+    const bool valid = in && u != KMG_INVALID;
+    const uint32_t uu = valid ? u : 0u;
+    const uint32_t up = (uu >> (2 * (K - 1 - p))) & 3u, uq = (uu >> (2 * (K - 1 - q))) & 3u;
+    const bool corr = pi >= pg.corr0;
+    gidx = (uint32_t)pi * pair_stride + chunk_base + pair_key(uu, K, p, q);
+    meta = (valid ? 1u : 0u) | (corr ? 2u : 0u) | ((oq ? uq : up) << 2) | ((oq ? up : uq) << 4) |
+           ((pi == pg.corr0 + 1) ? 64u : 0u) | ((uint32_t)p << 8) | ((uint32_t)q << 12) |
+           (oq ? 0x10000u : 0u);
+  };
+  auto load_summary = [&](uint32_t gidx, uint4 &sa, uint2 &sb) {
+    const uint32_t *rec = summary + (size_t)(gidx >> 5) * 8;
+    sa = *(const uint4 *)rec;
+    sb = *(const uint2 *)(rec + 4);
+  };
+  // base line and line count of the group (PL_WIDE: exact-index path)
+  auto decode = [&](const uint4 &sa, const uint2 &sb, uint32_t gidx, uint32_t &base,
+                    uint32_t &nl) {
+    const int r = (int)(gidx & 31u);
+    const int wsel = r >> 3, sh = 4 * (r & 7);
+    const uint32_t wd[4] = {sa.y, sa.z, sa.w, sb.x};
+    uint32_t sum = sa.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t m = q < wsel ? 0xFFFFFFFFu : (q == wsel ? ((1u << sh) - 1u) : 0u);
+      sum += nib_sum(wd[q] & m);
+    }
+    const uint32_t own = wsel == 0 ? wd[0] : wsel == 1 ? wd[1] : wsel == 2 ? wd[2] : wd[3];
+    base = sum;
+    nl = ((sb.y >> r) & 1u) ? PL_WIDE : ((own >> sh) & 15u);
+  };
+  // weight of sub-bin (outer zo, inner zi) of a correction group
+  auto corr_w = [&](uint32_t meta, uint32_t zo, uint32_t zi) -> int {
+    if (zo != ((meta >> 2) & 3u)) return w2;
+    if (zi == ((meta >> 4) & 3u)) return w2 + ((meta & 64u) ? h0 : 0);
+    return w2 + cc;
+  };
+  // groups past the ring: a lane walks the group on its own (rare)
+  auto slow_list = [&](uint32_t gidx, uint32_t meta, uint32_t base, uint32_t nl) {
+    const bool corr = (meta & 2u) != 0;
+    if (nl == PL_WIDE) {  // straight from the exact index, sub-bin by sub-bin
+      const uint32_t key = gidx & (NK2 - 1u);
+      const int p = (meta >> 8) & 0xF, q = (meta >> 12) & 0xF;
+      const uint32_t *xo = xoff + (size_t)c * ((size_t)NK2 << 4);
+      for (int b = 0; b < 16; ++b) {
+        uint32_t zp, zq;
+        pl_subbin(b, corr, (meta & 0x10000u) != 0, zp, zq);
+        const int w = corr ? corr_w(meta, (uint32_t)b >> 2, (uint32_t)b & 3u) : w2;
+        if (!w) continue;
+        const uint32_t z = pair_insert(key, K, p, q, zp, zq);
+        const uint32_t e1 = xo[z + 1];
+        for (uint32_t e = xo[z]; e < e1; ++e) atomicAdd(&acc[xent[e]], w);
+      }
+      return;
+    }
+    uint4 hd = make_uint4(0, 0, 0, 0);
+    if (corr) hd = load_piece(rl, base * 128u);
+    const uint32_t n = corr ? hdr_byte(hd, 15) : nl * 64u;
+    const uint32_t e0 = corr ? 8u : 0u;  // first entry halfword
+    const uint16_t *hw = (const uint16_t *)(lines + (size_t)base * 8);
+    for (uint32_t t = 0; t < n; ++t) {
+      int w = w2;
+      if (corr) {
+        uint32_t b = 0;
+        while (b < 15 && hdr_byte(hd, (int)b) <= t) ++b;
+        w = corr_w(meta, b >> 2, b & 3u);
+      }
+      if (w) atomicAdd(&acc[hw[e0 + t]], w);
+    }
+  };
+
+  // producer state: summary of batch b (loaded one call ahead), correction lists whose
+  // headers are in flight (entered at the next call)
+  int b = wave;
+  uint32_t gid = 0, met = 0;
+  uint4 sa = make_uint4(0, 0, 0, 0);
+  uint2 sb = make_uint2(0, 0);
+  if (b < nbatch) {
+    describe(b, gid, met);
+    load_summary(gid, sa, sb);
+  }
+  bool pc_on = false;
+  uint32_t pc_base = 0, pc_nl = 0, pc_meta = 0;
+  uint4 pc_h = make_uint4(0, 0, 0, 0);
+  uint32_t tail = 0, issue = 0;  // ring positions (wave-uniform)
+
+  auto produce = [&]() {
+    const bool have = b < nbatch;
+    uint32_t base = 0, nl = 0, meta = 0, gcur = 0;
+    if (have) {
+      decode(sa, sb, gid, base, nl);
+      meta = met;
+      gcur = gid;
+    }
+    const int bn = b + nwv;
+    if (bn < nbatch) {  // prefetch the summary records of the batch after
+      describe(bn, gid, met);
+      load_summary(gid, sa, sb);
+    }
+    b = bn;
+    const bool valid = have && (meta & 1u) != 0;
+    const bool corr = (meta & 2u) != 0;
+    const bool wide = nl == PL_WIDE;
+    const uint32_t cu = (valid && !corr && !wide && nl <= (uint32_t)PL_QU) ? nl : 0u;
+    const uint32_t cn = pc_on ? pc_nl : 0u;
+    const uint32_t cnt = cu + cn;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = (uint32_t)__shfl_up((int)incl, d, 64);
+      if (lane >= d) incl += v;
+    }
+    const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
+    const uint32_t Tp = (T + 7u) & ~7u;
+    uint32_t pos = tail + incl - cnt;
+    for (uint32_t e = 0; e < cu; ++e) ring[(pos + e) & (PL_RING - 1)] = make_uint2(base + e, 0u);
+    pos += cu;
+    if (pc_on) {
+      const int uo = (int)((pc_meta >> 2) & 3u), ui = (int)((pc_meta >> 4) & 3u);
+      const int rs = (int)hdr_start(pc_h, 4 * uo), re = (int)hdr_byte(pc_h, 4 * uo + 3);
+      const int es = (int)hdr_start(pc_h, 4 * uo + ui), ee = (int)hdr_byte(pc_h, 4 * uo + ui);
+      const uint32_t fl = RE_CORR | ((pc_meta & 64u) ? RE_DESIG : 0u);
+      for (uint32_t s = 0; s < pc_nl; ++s) {
+        // halfword h of line s holds entry 64 s + h - 8
+        const int sh = 8 - 64 * (int)s;
+        const uint32_t y = clamp64(rs + sh) | (clamp64(re + sh) << 8) | (clamp64(es + sh) << 16) |
+                           (clamp64(ee + sh) << 24);
+        ring[(pos + s) & (PL_RING - 1)] = make_uint2((pc_base + s) | fl | (s == 0 ? RE_HDR : 0u), y);
+      }
+    }
+    if ((uint32_t)lane < Tp - T) ring[(tail + T + lane) & (PL_RING - 1)] = make_uint2(RE_EMPTY, 0u);
+    tail += Tp;
+    // this batch's correction lists: headers now, lines at the next call
+    pc_on = valid && corr && !wide && nl > 0 && nl <= (uint32_t)PL_QC;
+    if (pc_on) {
+      pc_base = base;
+      pc_nl = nl;
+      pc_meta = meta;
+      pc_h = load_piece(rl, base * 128u);
+    }
+    if (valid && nl > 0 && (wide || nl > (corr ? (uint32_t)PL_QC : (uint32_t)PL_QU)))
+      slow_list(gcur, meta, base, nl);
+  };
+  // add the 8 columns of a loaded piece: w2 each, or (steps with correction lines) the
+  // per-halfword weight.  Every path issues exactly 8 ds_add (header halfwords go to a
+  // dummy column), so the compiler's LDS / memory wait counts stay static in the loop.
+  const int slot = g8 & 3;  // lane group inside its half-wave (bank-sorted lines)
+  const bool rs1 = (slot & 1) != 0, rs2 = (slot & 2) != 0;
+  auto consume = [&](const uint4 &xr, const uint2 &e) {
+    const uint4 x = rot4(xr, rs1, rs2);
+    if (!__any((e.x & RE_CORR) != 0)) {
+      add_piece(x, w2);
+      return;
+    }
+    const uint32_t rlo = e.y & 0xFFu, rhi = (e.y >> 8) & 0xFFu;
+    const uint32_t elo = (e.y >> 16) & 0xFFu, ehi = e.y >> 24;
+    const uint32_t vlo = (e.x & RE_HDR) ? 8u : 0u;
+    const int wx = (e.x & RE_DESIG) ? h0 : 0;
+    const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      // halfword of the line this instruction adds (rotated dwords)
+      const uint32_t h = 8u * (uint32_t)j8 + 2u * (((uint32_t)(v >> 1) + (uint32_t)slot) & 3u) +
+                         (uint32_t)(v & 1);
+      const int w = (h - rlo < rhi - rlo) ? ((h - elo < ehi - elo) ? w2 + wx : w2 + cc) : w2;
+      const uint32_t ad = (v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]);
+      lds_add(h < vlo ? 4u * (dcol + h) : ad, w);
+    }
+  };
+  // next ring entry of this lane's 8-lane group (the dummy line 0 when the ring is empty)
+  auto next_entry = [&]() -> uint2 {
+    uint2 x = make_uint2(RE_EMPTY, 0u);
+    if (issue < tail) {
+      x = ring[(issue + (uint32_t)g8) & (PL_RING - 1)];
+      issue += 8;
+    }
+    return x;
+  };
+  auto piece_off = [&](const uint2 &x) -> uint32_t {
+    return ((x.x & RE_EMPTY) ? 0u : (x.x & RE_LINE) * 128u) + 16u * (uint32_t)j8;
+  };
+
+  // Two stages per slot: a ring entry read into one of two register sets, then its piece
+  // loaded into v, then consumed.  The sets swap roles every half-iteration (no register
+  // copies, which would wait on the LDS reads); the wave-uniform masks m0 / m1 say which
+  // slots hold real entries, so the exit test never waits on a value just read.
+  while (tail == issue && (b < nbatch || __any(pc_on))) produce();
+  uint4 v[PL_D];
+  uint2 s0[PL_D], s1[PL_D];
+  uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+  for (int r = 0; r < PL_D; ++r) {
+    if (issue < tail) m0 |= 1u << r;
+    s0[r] = next_entry();
+    v[r] = load_piece(rl, piece_off(s0[r]));
+  }
+#pragma unroll
+  for (int r = 0; r < PL_D; ++r) {
+    if (issue < tail) m1 |= 1u << r;
+    s1[r] = next_entry();
+  }
+  // half-step: consume the pieces of set `cur`, load those of set `nxt`, refill `cur`
+  auto half = [&](uint2 (&cur)[PL_D], uint2 (&nxt)[PL_D], uint32_t &mc) {
+#pragma unroll
+    for (int r = 0; r < PL_D; ++r) {
+      consume(v[r], cur[r]);
+      v[r] = load_piece(rl, piece_off(nxt[r]));
+      mc &= ~(1u << r);
+      if (issue < tail) mc |= 1u << r;
+      cur[r] = next_entry();
+    }
+  };
+  auto more = [&]() { return b < nbatch || __any(pc_on); };
+  for (;;) {
+    if (tail - issue < 8u * (PL_D + 1) && more()) produce();
+    if (!(m0 | m1) && issue >= tail && !more()) break;
+    half(s0, s1, m0);
+    if (tail - issue < 8u * (PL_D + 1) && more()) produce();
+    if (!(m0 | m1) && issue >= tail && !more()) break;
+    half(s1, s0, m1);
+  }
+  __syncthreads();
+
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  emit_row<true>(o, il, i, col0, cw, (const int32_t *)acc, norm);
+}
+
+hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, const Packed &pk,
+                                    const uint32_t *summary, const uint4 *lines, int64_t nlines,
+                                    const uint32_t *xoff, const uint16_t *xent, int64_t row0,
+                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                    hipStream_t s, int depth) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || g.n == 0) return hipSuccess;
+  if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
+  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (nlines * 128 >= 0xFFFFFFF0LL || nlines >= (1LL << 28)) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(((((((g.chunk + 3) >> 2) << 2) + 64 + g.pmax + pk.ldp + KMG_PAIRS_MAX + 1) & ~1) +
+                               16 * KMG_PL_WAVE_WORDS)) * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(rows * g.nchunks));
+  const uint32_t lb = (uint32_t)(nlines * 128);
+  switch (pg.k) {
+#define KMG_PL(KK)                                                                                 \
+  case KK:                                                                                         \
+    if (depth >= 8)                                                                                \
+      hipLaunchKernelGGL((gram_pl_kernel<KK, 8>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+    else if (depth >= 6)                                                                           \
+      hipLaunchKernelGGL((gram_pl_kernel<KK, 6>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+    else                                                                                           \
+      hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+    break;
+    KMG_PL(3) KMG_PL(4) KMG_PL(5) KMG_PL(6) KMG_PL(7) KMG_PL(8) KMG_PL(9) KMG_PL(10) KMG_PL(11)
+    KMG_PL(12)
+#undef KMG_PL
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kmg

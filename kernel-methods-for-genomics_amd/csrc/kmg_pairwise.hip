@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, i
       if (live && c >= 0 && c <= ny) {
         double M = 0.0, X = 0.0, Y = 0.0, X2 = 0.0, Y2 = 0.0;
         if (r >= 1 && c >= 1) {
-          const double sub = cf.es[xr * 4 + yb[c - 1]];
+          const double sub = cf.es[(xr & 3u) * 4 + (yb[c - 1] & 3u)];  // ACGT (host-checked)
           if (SMITH) {
             M = __dmul_rn(sub, fmax(fmax(fmax(1.0, dX), dY), dM));
             X = fmax(__dmul_rn(eo, uM), __dmul_rn(ee, uX));
@@ -700,6 +700,31 @@ hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e
     hipLaunchKernelGGL((gram_la_kernel<true>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
   else
     hipLaunchKernelGGL((gram_la_kernel<false>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ argument checks
+// stats[0] = max symbol code over every row's first len symbols, stats[1] = min len (both
+// must be preset by the caller to 0 / INT_MAX): the C ABI's alphabet / length checks on
+// device-resident rows (kmgram.h: KMG_EINVAL for alphabet errors)
+__global__ __launch_bounds__(256) void row_stats_kernel(SeqSpec q, uint32_t *stats) {
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= q.n) return;
+  const int len = min(max(q.lens[j], 0), (int)q.ldc);
+  uint32_t mx = 0;
+  for (int t = lane; t < len; t += 64) mx = max(mx, (uint32_t)q.codes[j * q.ldc + t]);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+  if (lane == 0) {
+    atomicMax(&stats[0], mx);
+    atomicMin(&stats[1], (uint32_t)len);
+  }
+}
+
+hipError_t launch_row_stats(const SeqSpec &q, uint32_t *stats, hipStream_t s) {
+  if (q.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(row_stats_kernel, dim3((unsigned)((q.n + 3) / 4)), dim3(256), 0, s, q, stats);
   return hipGetLastError();
 }
 

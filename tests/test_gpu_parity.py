@@ -150,8 +150,11 @@ def test_spectrum_long_sequences_unpacked(ctx):
     assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 5))
 
 
-def test_mismatch_k9_n20000(ctx):
-    """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows."""
+@pytest.mark.parametrize("form", ["0", "3"])
+def test_mismatch_k9_n20000(ctx, tune, form):
+    """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows
+    (default formulation and the pair-lines table)."""
+    tune(KMG_MM_FORM=form)
     codes, lens = E.synthetic(20000, 101, seed=3)
     K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
                  L.KMG_F64)
@@ -193,13 +196,15 @@ def test_mismatch_slots_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
+@pytest.mark.parametrize("form", ["2", "3"])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
-def test_mismatch_pairs_k_range(ctx, tune, k):
-    """Drop-two pair table (default for 9 <= k <= 12, forced below) at every compiled k,
-    raw and normalised, over several column chunkings (chunk = columns per group table)."""
+def test_mismatch_pairs_k_range(ctx, tune, k, form):
+    """Drop-two tables (2: pair table with per-group headers, 3: pair lines) at every
+    compiled k, raw and normalised, over several column chunkings (chunk = columns per
+    group table)."""
     codes, lens = E.synthetic(500, 101, seed=80 + k)
     ref = cref.mismatch_raw(codes, lens, k, 1)
-    tune(KMG_MM_FORM=2)
+    tune(KMG_MM_FORM=form)
     for chunk in (("40", "168", "20480") if k <= 9 else ("168", "20480") if k == 10 else ("20480",)):
         tune(KMG_MM_CHUNK=chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
@@ -210,7 +215,7 @@ def test_mismatch_pairs_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["1", "2"])
+@pytest.mark.parametrize("form", ["1", "2", "3"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
     >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
@@ -229,7 +234,7 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     assert np.array_equal(raw, raw.T)
 
 
-@pytest.mark.parametrize("form", ["1", "2"])
+@pytest.mark.parametrize("form", ["1", "2", "3"])
 def test_mismatch_stress_repeats(ctx, tune, form):
     tune(KMG_MM_FORM=form)
     codes, lens = E.synthetic(40, 101, seed=12)
@@ -299,6 +304,20 @@ def test_wd_wds_pair_any_L(engine):
         for span in (0, 1, 2, 5, len(x) - 3, len(x), len(y), len(x) + 4, max(len(x), len(y)) + 9):
             assert engine.wd_pair(x, y, 5, span) == cpu_ref.wd_pair(x, y, 5, span)
             assert engine.wds_pair(x, y, 4, 3, span) == cpu_ref.wds_pair(x, y, 4, 3, span)
+
+
+def test_wd_span_past_shortest_row_rejected(ctx):
+    """A full-K call with span > 0 counts positions below min(len_x, len_y, span): a span past
+    a row's end would miss the reference's clipped-slice matches, so the C ABI refuses it
+    (KMG_EUNSUPPORTED) unless the rows are padded to span (+ S), as engine.wd_pair does."""
+    codes, lens = E.synthetic(6, 60, seed=14)
+    lens[3] = 40
+    for kind, extra in ((L.KMG_WD, {}), (L.KMG_WDS, {"S": 3})):
+        with pytest.raises(L.KmgUnsupported):
+            ctx.gram(P.make(kind, d=4, span=45, **extra), codes, lens, L.KMG_F64)
+    ctx.gram(P.make(L.KMG_WD, d=4, span=40), codes, lens, L.KMG_F64)  # = min len: accepted
+    with pytest.raises(L.KmgUnsupported):
+        ctx.gram(P.make(L.KMG_WDS, d=4, S=3, span=38), codes, lens, L.KMG_F64)  # 38 + 3 > 40
 
 
 @pytest.mark.parametrize("d,S", [(1, 0), (3, 1), (5, 3), (10, 5), (8, 7), (4, 12)])

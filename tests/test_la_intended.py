@@ -111,3 +111,35 @@ def test_gpu_la_intended_rows(engine, ctx):
         for x in (d_codes, d_lens, d_out):
             ctx.dfree(x)
     assert np.array_equal(rows, full[9:22])
+
+
+@pytest.mark.gpu
+def test_gpu_la_intended_rejects_non_acgt(ctx):
+    """The substitution matrix covers A/C/G/T only (kernels.py:223): a row holding another
+    symbol is KMG_EINVAL through the C ABI (host and device-resident rows), not a read past
+    the 16-entry table."""
+    from kmgram import _lib as L
+    from kmgram import params as P
+    codes, lens = E.synthetic(9, 101, seed=33)
+    codes[4, 50] = 4  # 'N'
+    p = P.make(L.KMG_LOCALALIGN, smith=0, la_mode=L.KMG_LA_INTENDED, la_e=11, la_d=1,
+               la_beta=0.5)
+    with pytest.raises(L.KmgError) as ei:
+        ctx.gram(p, codes, lens, L.KMG_F64)
+    assert ei.value.status == L.KMG_EINVAL
+    n, ldc = codes.shape
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(n * n * 8)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        with pytest.raises(L.KmgError) as ei:
+            ctx.gram_device(p, d_codes, d_lens, n, ldc, 0, n, L.KMG_F64, d_out, n)
+        assert ei.value.status == L.KMG_EINVAL
+        lens[4] = 50  # the N is past the row's length: accepted
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device(p, d_codes, d_lens, n, ldc, 0, n, L.KMG_F64, d_out, n)
+        ctx.synchronize()
+    finally:
+        for x in (d_codes, d_lens, d_out):
+            ctx.dfree(x)

@@ -3,7 +3,8 @@
 # Every step runs under its own time limit; the session stops at the first failing step.
 #
 # usage: bash tools/gpu_run.sh <tag> <step> [<step> ...]
-#   tests [pytest args]     GPU test suite (tools/gpu_tests.sh), log gpurun_out/<tag>/pytest.txt
+#   tests[=EXPR]            GPU test suite (tools/gpu_tests.sh; EXPR: pytest -k expression),
+#                           log gpurun_out/<tag>/pytest.txt
 #   smoke                   __graft_entry__.smoke()
 #   bench[:ARGS]            python bench.py ARGS (colon-separated, e.g. bench:--steps:10)
 #   prof:WL[,WL...]         rocprofv3 kernel trace + PMC passes (profiles/run_profiles_r02.sh)
@@ -21,8 +22,11 @@ for STEP in "$@"; do
   n=$((n + 1))
   case "$STEP" in
     tests*)
-      ARGS=${STEP#tests}
-      bash tools/gpu_tests.sh "$TAG" $ARGS > /dev/null || { echo "tests failed"; tail -40 "$OUT/pytest.txt"; exit 1; }
+      if [ "$STEP" = "tests" ]; then
+        bash tools/gpu_tests.sh "$TAG" > /dev/null || { echo "tests failed"; tail -40 "$OUT/pytest.txt"; exit 1; }
+      else
+        bash tools/gpu_tests.sh "$TAG" -k "${STEP#tests=}" > /dev/null || { echo "tests failed"; tail -40 "$OUT/pytest.txt"; exit 1; }
+      fi
       tail -n 1 "$OUT/pytest.txt"
       ;;
     smoke)
