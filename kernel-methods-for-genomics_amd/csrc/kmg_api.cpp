@@ -102,6 +102,9 @@ struct Tuning {
   int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table,
                             // 3 drop-two pair lines (kmg_pairs.hip)
   int pl_depth = 4;         // KMG_PL_D: pair-lines Gram, ring steps in flight per wave (4/6/8)
+  int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
+  int pl_dbg = 0;           // KMG_PL_DBG: diagnostics only (wrong results): 1 no correction
+                            // weights, 2 no bank rotation
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
@@ -144,6 +147,8 @@ void read_tuning(Tuning &t) {
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
   t.pl_depth = env_or("KMG_PL_D", d.pl_depth);
+  t.pl_dbg = env_or("KMG_PL_DBG", d.pl_dbg);
+  t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
@@ -168,6 +173,8 @@ struct kmg_ctx {
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
   DevBuf tri_stage, tri_scratch;  // upper-triangle multi-GPU build: round slabs, full rows
   DevBuf ovf;                     // 16-bit round slabs: count-overflow flag
+  DevBuf esc, esc_all, esc_cnt;   // uint8 round slabs: escape list, all-gathered lists, counts
+  uint32_t esc_cap = 0;           // entries of `esc` in use by the current build (0: none)
   int64_t cur_n = 0;              // columns of the current Gram call
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   Tuning tune;
@@ -785,6 +792,11 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     KMG_TRY(c->ovf.ensure(sizeof(uint32_t)));
     KMG_HIP(hipMemsetAsync(c->ovf.p, 0, sizeof(uint32_t), c->stream));
     o.ovf = c->ovf.as<uint32_t>();
+    if (dt == KMG_U8 && c->esc_cap > 0) {  // escapes (kmg_gram_blocks sets the list up)
+      o.esc = c->esc.as<uint4>();
+      o.esc_n = c->esc_cnt.as<uint32_t>();
+      o.esc_cap = c->esc_cap;
+    }
   }
   if (c->tune.poison && n > 0)  // testing: no stale output can pass
     for (const RowRange &r : ranges)
@@ -981,7 +993,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           return launch_gram_mismatch1_pl(pg, g, pkd, c->pr_summary.as<uint32_t>(),
                                           c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
                                           c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, c->tune.pl_depth);
+                                          (int)w[2], oq, c->stream, c->tune.pl_depth, c->tune.pl_dbg);
         }, true);
       }
       if (exact) {
@@ -1378,6 +1390,41 @@ int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
 int kmg_gram_blocks_wire(kmg_ctx *c) { return c ? c->last_wire_bytes : 0; }
 
 namespace {
+// Escapes of uint8 round slabs (counts >= 255): the ranks all-gather their lists (the
+// per-rank counts first, then max-count entries from every rank) and every rank patches
+// them into its K after the unpacks (context stream, which already waits for them).
+int patch_escapes(kmg_ctx *c, const kmg_params *p, int64_t n, void *d_out, int64_t ld_out,
+                  int32_t out_dtype, int32_t nranks, int32_t rank, bool rccl) {
+  uint32_t *cnt = c->esc_cnt.as<uint32_t>();  // [0] this process's count, [1..] gathered
+  const double *diagv = c->diagv.as<double>(), *dsq = c->dsq.as<double>();
+  if (!rccl || nranks == 1) {
+    KMG_HIP(launch_tri_patch8(c->esc.as<uint4>(), cnt, 1, c->esc_cap, c->esc_cap, d_out, ld_out,
+                              out_dtype, p->normalize, diagv, dsq, c->stream));
+    return KMG_OK;
+  }
+  KMG_HIP(hipMemcpyAsync(cnt + 1 + rank, cnt, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+  KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+  KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+  ncclResult_t r = ncclAllGather(cnt + 1 + rank, cnt + 1, 1, ncclUint32, c->comm, c->comm_stream);
+  if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather (escape counts): %s", ncclGetErrorString(r));
+  std::vector<uint32_t> counts((size_t)nranks);
+  KMG_HIP(hipMemcpyAsync(counts.data(), cnt + 1, sizeof(uint32_t) * nranks, hipMemcpyDeviceToHost,
+                         c->comm_stream));
+  KMG_HIP(hipStreamSynchronize(c->comm_stream));
+  uint32_t maxc = 0;
+  for (uint32_t v : counts) maxc = std::max(maxc, std::min(v, c->esc_cap));
+  if (maxc == 0) return KMG_OK;
+  KMG_TRY(c->esc_all.ensure(sizeof(uint4) * (size_t)maxc * nranks));
+  r = ncclAllGather(c->esc.p, c->esc_all.p, sizeof(uint4) * (size_t)maxc, ncclChar, c->comm,
+                    c->comm_stream);
+  if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather (escapes): %s", ncclGetErrorString(r));
+  KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
+  KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+  KMG_HIP(launch_tri_patch8(c->esc_all.as<uint4>(), cnt + 1, nranks, maxc, maxc, d_out, ld_out,
+                            out_dtype, p->normalize, diagv, dsq, c->stream));
+  return KMG_OK;
+}
+
 int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
                      void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
@@ -1412,13 +1459,16 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     const int L = mm ? (p->window > 0 ? p->window : 101) : (int)ldc;  // gram_device's maxlen
     const int pmax = std::max(1, L - p->k + 1);
     const SmPath path = sm_path(c->tune, p, pmax);
-    // 8 bits only for spectrum-shaped counts: their off-diagonal entries stay far below 256
-    // unless sequences repeat k-mers, where mismatch counts of random 101-mers pass 255
-    // (a shared 12-mer already contributes 4 exact 9-mer windows x 28)
-    if (narrow_bits == 8 && path != SM_POSTING) return KMG_RETRY_WIDE;
-    if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS) {
+    // 8-bit slabs for every posting-list path: an off-diagonal count >= 255 (a pair sharing
+    // a long k-mer; ~1e-4 of random 101-mer pairs for MM(9,1)) travels in an escape list
+    // that is all-gathered after the slabs and patched into K; a full list redoes the
+    // build with 16-bit slabs
+    if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS ||
+        path == SM_PL) {
       wire = narrow_bits == 8 ? KMG_U8 : KMG_U16;
       check16 = wire == KMG_U8 || path != SM_POSTING;  // spectrum counts <= P^2 < 65536
+    } else if (narrow_bits == 8) {
+      return KMG_RETRY_WIDE;
     }
   }
   const size_t wsz = dtype_size(wire);
@@ -1526,6 +1576,19 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
       return KMG_OK;
     };
   }
+  c->esc_cap = 0;
+  if (wire == KMG_U8 && n > 0) {
+    // escape list sized for ~1/512 of this process's upper-triangle pairs (random 101-mers:
+    // ~1e-4 of MM(9,1) pairs reach 255), at least 65536 entries
+    const double pairs = 0.5 * (double)n * (double)n / (gather == 3 ? 1.0 : (double)nranks);
+    const int64_t cap = c->tune.esc_cap > 0
+                            ? (int64_t)c->tune.esc_cap
+                            : std::min<int64_t>(1 << 24, std::max<int64_t>(65536, (int64_t)(pairs / 512.0)));
+    KMG_TRY(c->esc.ensure(sizeof(uint4) * (size_t)cap));
+    KMG_TRY(c->esc_cnt.ensure(sizeof(uint32_t) * (size_t)(1 + nranks)));
+    KMG_HIP(hipMemsetAsync(c->esc_cnt.p, 0, sizeof(uint32_t), c->stream));
+    c->esc_cap = (uint32_t)cap;
+  }
   KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, ranges, tri ? wire : out_dtype,
                       ld_out, after));
   if (rccl) {  // stream order: later work on the context stream sees the full K
@@ -1552,6 +1615,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     KMG_HIP(hipStreamSynchronize(c->stream));
     if (flag) return KMG_RETRY_WIDE;
   }
+  if (c->esc_cap > 0) KMG_TRY(patch_escapes(c, p, n, d_out, ld_out, out_dtype, nranks, rank, rccl));
   return KMG_OK;
 }
 }  // namespace

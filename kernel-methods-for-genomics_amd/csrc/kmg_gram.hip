@@ -150,8 +150,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
 #pragma unroll
       for (int h = 0; h < 16; ++h) {
         const bool dg = col0 + q + h == i;
-        big |= !dg && v[h] > 0xFFu;
-        v[h] = dg ? 0u : min(v[h], 0xFFu);
+        v[h] = (dg || q + h >= cw) ? 0u : u8_slab_entry(o, i, col0 + q + h, v[h], big);
       }
       uint8_t *d = prow + q;
       if (q + 16 <= cw && (((uintptr_t)d) & 15) == 0) {
@@ -1016,6 +1015,47 @@ hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t 
   else
     return hipErrorInvalidValue;
 #undef KMG_UNPACK
+  return hipGetLastError();
+}
+
+// escapes of uint8 round slabs: one thread per (list, entry); K[r][c] and its mirror
+// K[c][r] get the count widened exactly as tri_rows16_kernel / tri_mirror16_kernel widen
+// slab values (normalize_K's formula for normalised output)
+template <typename TO>
+__global__ __launch_bounds__(256) void tri_patch8_kernel(const uint4 *__restrict__ esc,
+                                                         const uint32_t *__restrict__ counts,
+                                                         int64_t stride, int64_t max_count,
+                                                         TO *__restrict__ K, int64_t ld,
+                                                         int normalize,
+                                                         const double *__restrict__ diagv,
+                                                         const double *__restrict__ dsq) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int set = (int)blockIdx.y;
+  const int64_t cnt = min((int64_t)counts[set], min(stride, max_count));
+  if (t >= cnt) return;
+  const bool norm = normalize && diagv[0] != 1.0;
+  const uint4 e = esc[(int64_t)set * stride + t];
+  const int64_t r = e.x, c = e.y;
+  K[r * ld + c] = widen16<TO>(e.z, r, c, norm, dsq);
+  K[c * ld + r] = widen16<TO>(e.z, c, r, norm, dsq);
+}
+
+hipError_t launch_tri_patch8(const uint4 *esc, const uint32_t *counts, int nsets, int64_t stride,
+                             int64_t max_count, void *K, int64_t ld, int dt, int normalize,
+                             const double *diagv, const double *dsq, hipStream_t s) {
+  const int64_t m = std::min(stride, max_count);
+  if (nsets <= 0 || m <= 0) return hipSuccess;
+  if (!diagv || (normalize && !dsq) || nsets > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((m + 255) / 256), (unsigned)nsets);
+  if (dt == KMG_I32)
+    hipLaunchKernelGGL((tri_patch8_kernel<int32_t>), grid, dim3(256), 0, s, esc, counts, stride,
+                       max_count, (int32_t *)K, ld, 0, diagv, dsq);
+  else if (dt == KMG_F32)
+    hipLaunchKernelGGL((tri_patch8_kernel<float>), grid, dim3(256), 0, s, esc, counts, stride,
+                       max_count, (float *)K, ld, normalize, diagv, dsq);
+  else
+    hipLaunchKernelGGL((tri_patch8_kernel<double>), grid, dim3(256), 0, s, esc, counts, stride,
+                       max_count, (double *)K, ld, normalize, diagv, dsq);
   return hipGetLastError();
 }
 

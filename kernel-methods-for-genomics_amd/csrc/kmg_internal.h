@@ -204,7 +204,28 @@ struct OutSpec {
   uint32_t *ovf = nullptr;  // dtype KMG_U16 / KMG_U8: set to 1 when a count exceeds 65535
                             // / an off-diagonal count exceeds 255 (the stored value is then
                             // clipped and the caller redoes the build with wider slabs)
+  // dtype KMG_U8 with an escape list: an off-diagonal count >= 255 is stored as the escape
+  // byte 255 and appended as (row, column, count, 0) to esc[*esc_n] (esc_n counts every
+  // attempt; past esc_cap the overflow flag is raised instead)
+  uint4 *esc = nullptr;
+  uint32_t *esc_n = nullptr;
+  uint32_t esc_cap = 0;
 };
+
+// uint8 round-slab byte of the off-diagonal count x at (row i, column col)
+__device__ __forceinline__ uint32_t u8_slab_entry(const OutSpec &o, int64_t i, int64_t col,
+                                                  uint32_t x, bool &big) {
+  if (x < 255u) return x;
+  if (o.esc) {
+    const uint32_t k = atomicAdd(o.esc_n, 1u);
+    if (k < o.esc_cap) {
+      o.esc[k] = make_uint4((uint32_t)i, (uint32_t)col, x, 0u);
+      return 255u;
+    }
+  }
+  big = true;
+  return 255u;
+}
 
 // multi-GPU upper-triangle assembly (kmg_gram_blocks): round slab S (R rows x w = n - c0
 // columns, row-major: rows c0 .. c0 + R of K restricted to columns >= c0) -> K's rows
@@ -222,6 +243,11 @@ hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t 
 hipError_t launch_tri_unpack8(const uint8_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
                               void *K, int64_t ld, int dt, int normalize, const double *diagv,
                               const double *dsq, hipStream_t s);
+// escapes of uint8 slabs: nsets lists of stride entries, list s holding counts[s] entries
+// (row, column, count, 0); writes K[row][col] and K[col][row] as the unpack would have
+hipError_t launch_tri_patch8(const uint4 *esc, const uint32_t *counts, int nsets, int64_t stride,
+                             int64_t max_count, void *K, int64_t ld, int dt, int normalize,
+                             const double *diagv, const double *dsq, hipStream_t s);
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store = 0, int order = 0);
@@ -241,7 +267,7 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
                                     const uint32_t *summary, const uint4 *lines, int64_t nlines,
                                     const uint32_t *xoff, const uint16_t *xent, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int depth = 4);
+                                    hipStream_t s, int depth = 4, int dbg = 0);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -347,7 +347,7 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
                                                        const uint32_t *__restrict__ xoff,
                                                        const uint16_t *__restrict__ xent,
                                                        int64_t row0, int64_t rows, int w0, int w1,
-                                                       int w2, OutSpec o) {
+                                                       int w2, OutSpec o, int dbg) {
   constexpr int NP = K * (K - 1) / 2;
   constexpr uint32_t NK2 = 1u << (2 * (K - 2));
   // one dynamic LDS block, accumulator first (col_addr_sdwa: acc at LDS offset 0)
@@ -546,9 +546,14 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
   // dummy column), so the compiler's LDS / memory wait counts stay static in the loop.
   const int slot = g8 & 3;  // lane group inside its half-wave (bank-sorted lines)
   const bool rs1 = (slot & 1) != 0, rs2 = (slot & 2) != 0;
+  uint32_t sink = 0;
   auto consume = [&](const uint4 &xr, const uint2 &e) {
-    const uint4 x = rot4(xr, rs1, rs2);
-    if (!__any((e.x & RE_CORR) != 0)) {
+    const uint4 x = (dbg & 2) ? xr : rot4(xr, rs1, rs2);
+    if (dbg & 4) {  // diagnostics: no LDS adds
+      sink += x.x ^ x.y ^ x.z ^ x.w;
+      return;
+    }
+    if ((dbg & 1) || !__any((e.x & RE_CORR) != 0)) {
       add_piece(x, w2);
       return;
     }
@@ -619,6 +624,7 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
     if (!(m0 | m1) && issue >= tail && !more()) break;
     half(s1, s0, m1);
   }
+  if (sink == 0x9E3779B9u) acc[0] = 1;  // keeps the diagnostic loads live
   __syncthreads();
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
@@ -629,7 +635,7 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
                                     const uint32_t *summary, const uint4 *lines, int64_t nlines,
                                     const uint32_t *xoff, const uint16_t *xent, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int depth) {
+                                    hipStream_t s, int depth, int dbg) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
@@ -645,13 +651,13 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
   case KK:                                                                                         \
     if (depth >= 8)                                                                                \
       hipLaunchKernelGGL((gram_pl_kernel<KK, 8>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
     else if (depth >= 6)                                                                           \
       hipLaunchKernelGGL((gram_pl_kernel<KK, 6>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
     else                                                                                           \
       hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o);                        \
+                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
     break;
     KMG_PL(3) KMG_PL(4) KMG_PL(5) KMG_PL(6) KMG_PL(7) KMG_PL(8) KMG_PL(9) KMG_PL(10) KMG_PL(11)
     KMG_PL(12)

@@ -89,7 +89,8 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
   if (o.dtype == KMG_U8) {
     // raw off-diagonal counts as uint8 (the diagonal column is stored as 0: the unpack takes
     // K_ii from the diagonal), 16 columns = 16 B per lane and step; an off-diagonal count
-    // above 255 is clipped and flagged (the caller redoes the build with 16-bit slabs)
+    // >= 255 goes to the escape list (or, with none / a full one, is flagged and the caller
+    // redoes the build with 16-bit slabs)
     uint8_t *prow = (uint8_t *)o.out + il * o.ld + col0;
     bool big = false;
     for (int q = qs + threadIdx.x * 16; q < cw; q += blockDim.x * 16) {
@@ -98,8 +99,7 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
       for (int h = 0; h < 16; ++h) {
         const uint32_t x = q + h < cw ? (uint32_t)acc[q + h] : 0u;
         const bool dg = col0 + q + h == i;
-        big |= !dg && x > 0xFFu;
-        v[h] = dg ? 0u : min(x, 0xFFu);
+        v[h] = (dg || q + h >= cw) ? 0u : u8_slab_entry(o, i, col0 + q + h, x, big);
       }
       uint8_t *d = prow + q;
       if (q + 16 <= cw && (((uintptr_t)d) & 15) == 0) {

@@ -97,3 +97,29 @@ def assemble_upper_triangle(slabs, n, world, block, dtype):
         if c0 + r < n:
             K[c0 + r:, c0:c0 + r] = S[:r, r:w].T
     return K
+
+
+def u8_slab_escapes(counts, row0, col0):
+    """Restatement of the uint8 round-slab form the Gram kernels write (kmg_rowacc.h
+    emit_row, KMG_U8, with an escape list): `counts` holds rows row0.. at columns col0..;
+    the diagonal column is stored as 0 (the unpack takes K_ii from the locally computed
+    diagonal) and an off-diagonal count >= 255 is stored as the escape byte 255 plus a
+    (row, column, count) entry.  Returns (slab uint8, escapes int64 [m, 3])."""
+    import numpy as np
+    c = np.asarray(counts, dtype=np.int64)
+    rows = np.arange(c.shape[0])[:, None] + row0
+    cols = np.arange(c.shape[1])[None, :] + col0
+    diag = rows == cols
+    esc = (c >= 255) & ~diag
+    slab = np.where(diag, 0, np.minimum(c, 255)).astype(np.uint8)
+    r, q = np.nonzero(esc)
+    return slab, np.stack([r + row0, q + col0, c[r, q]], axis=1).astype(np.int64)
+
+
+def patch_escapes(K, escapes):
+    """Escape entries (row, column, count) into K and its mirror (kmg_gram.hip
+    tri_patch8_kernel)."""
+    for r, c, v in escapes:
+        K[r, c] = v
+        K[c, r] = v
+    return K

@@ -189,6 +189,83 @@ def test_gloo_upper_triangle_assembly(tmp_path, world):
     assert d["sent"] < 0.65 * d["full_rows_sent"]
 
 
+ESCAPE_WORKER = r"""
+import os, sys, json
+for p in ("kernel-methods-for-genomics_amd", "oracle"):
+    sys.path.insert(0, os.path.join(os.environ["ROOT"], p))
+import numpy as np
+import torch, torch.distributed as dist
+import cref
+from kmgram import encode as E
+from kmgram.shard import assemble_upper_triangle, patch_escapes, triangle_rounds, u8_slab_escapes
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+n, block = 301, 24
+codes, lens = E.synthetic(n, 101, seed=23)
+rng = np.random.default_rng(24)
+motif = rng.integers(0, 4, size=30, dtype=np.uint8)
+for _ in range(12):  # row pairs sharing a 30-mer: raw MM(9,1) counts far past 255
+    i, j = rng.choice(n, size=2, replace=False)
+    codes[i, 5:35] = motif
+    codes[j, 60:90] = motif
+full = cref.mismatch_raw(codes, lens, 9, 1)
+R = w * block
+slabs, escapes = [], []
+for c0, width in triangle_rounds(n, w, block):
+    S = torch.zeros((R, width), dtype=torch.uint8)
+    a, b = min(n, c0 + r * block), min(n, c0 + r * block + block)
+    mine = np.zeros((0, 3), dtype=np.int64)
+    if b > a:
+        sl, mine = u8_slab_escapes(cref.mismatch_raw(codes, lens, 9, 1, rows=(a, b))[:, c0:], a, c0)
+        S[a - c0:b - c0] = torch.from_numpy(sl)
+    parts = list(S.split(block))
+    dist.all_gather(parts, parts[r].clone())
+    slabs.append(S.numpy().astype(np.int64))
+    escapes.append(mine)
+# the escape lists after the slabs: counts first, then max-count entries from every rank
+mine = np.concatenate(escapes) if escapes else np.zeros((0, 3), dtype=np.int64)
+cnt = [torch.zeros(1, dtype=torch.int64) for _ in range(w)]
+dist.all_gather(cnt, torch.tensor([len(mine)], dtype=torch.int64))
+m = int(max(c.item() for c in cnt))
+pad = torch.zeros((m, 3), dtype=torch.int64)
+pad[:len(mine)] = torch.from_numpy(mine)
+lists = [torch.zeros((m, 3), dtype=torch.int64) for _ in range(w)]
+dist.all_gather(lists, pad)
+K = assemble_upper_triangle(slabs, n, w, block, np.int64)
+K[np.arange(n), np.arange(n)] = np.diag(full)  # K_ii from the locally computed diagonal
+for q in range(w):
+    patch_escapes(K, lists[q][:cnt[q].item()].numpy())
+ok = bool(np.array_equal(K, full))
+flag = torch.tensor([1 if ok else 0])
+dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+if r == 0:
+    print(json.dumps({"assembled_equal": int(flag.item()),
+                      "escapes": int(sum(c.item() for c in cnt))}))
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_upper_triangle_u8_escapes(tmp_path, world):
+    """uint8 round slabs with escape lists (the kmg_gram_blocks mismatch wire format): raw
+    MM(9,1) counts >= 255 of row pairs sharing a 30-mer travel as (row, column, count)
+    entries all-gathered after the slabs; assembly + diagonal + escape patch rebuild the
+    1-rank K byte for byte."""
+    pytest.importorskip("torch")
+    script = tmp_path / "e.py"
+    script.write_text(ESCAPE_WORKER)
+    env = dict(os.environ, ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), str(script)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["assembled_equal"] == 1
+    assert d["escapes"] >= 12
+
+
 @pytest.mark.parametrize("n,world,block", [(0, 2, 8), (1, 8, 4), (701, 2, 64), (20000, 8, 128),
                                            (200000, 8, 3125), (99, 3, 7)])
 def test_block_cyclic_cover(n, world, block):

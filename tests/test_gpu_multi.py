@@ -95,33 +95,72 @@ def data_repeats(ctx):
 
 @pytest.mark.parametrize("case", [0, 1, 2])
 @pytest.mark.parametrize("world,block", [(2, 128), (3, 64)])
-def test_upper_triangle_16bit_slabs_overflow(ctx, data_repeats, case, world, block):
-    """Round slabs travel as raw uint16 counts (spectrum: always; mismatch: until a count
-    passes 65535, then the whole build is redone with 32-bit slabs): the assembled K equals
-    the single-call K with homopolymer rows in the input."""
+def test_upper_triangle_8bit_slabs_escapes(ctx, data_repeats, case, world, block):
+    """Round slabs travel as uint8 counts; an off-diagonal count >= 255 (homopolymer pairs:
+    94^2 spectrum, 242172 raw mismatch) goes to the escape list, which is patched into K
+    after the unpack: the assembled K equals the single-call K."""
     params, dt = CASES[case]
     codes, lens = data_repeats[0], data_repeats[1]
     full = ctx.gram(params, codes, lens, dt)
     if case == 2:
-        assert full.max() > 65535  # the redo path really runs
+        assert full.max() > 65535
     got = _run_blocks(ctx, data_repeats, params, dt, world, [0], block, gather=3)
     assert np.array_equal(got, full)
-    # spectrum: off-diagonal counts of identical homopolymer rows are 94^2 > 255 -> 16 bits;
-    # mismatch: 242172 > 65535 -> the output dtype's own width
+    assert ctx.blocks_wire() == 1
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_upper_triangle_escape_list_full_ladder(ctx, tune, data_repeats, case):
+    """An escape list too small for the build (KMG_ESC_CAP=4) raises the overflow flag and
+    the build is redone one width up: spectrum at 16 bits (its counts <= 94^2), raw mismatch
+    at the output dtype's width (242172 > 65535).  The K is exact either way."""
+    tune(KMG_ESC_CAP=4)
+    params, dt = CASES[case]
+    codes, lens = data_repeats[0], data_repeats[1]
+    full = ctx.gram(params, codes, lens, dt)
+    got = _run_blocks(ctx, data_repeats, params, dt, 2, [0], 128, gather=3)
+    assert np.array_equal(got, full)
     assert ctx.blocks_wire() == (2 if case == 0 else np.dtype(L.DTYPES[dt]).itemsize)
+
+
+@pytest.mark.parametrize("form", ["0", "3"])
+def test_upper_triangle_escapes_n20000(ctx, tune, form):
+    """N=20000 MM(9,1), normalised float64 K, uint8 round slabs of 8 ranks rehearsed on one
+    GPU: 40 row pairs share an injected 30-mer (counts far past 255, so escapes are taken on
+    top of the random pairs' own); the assembled K equals the one-call K byte for byte."""
+    tune(KMG_MM_FORM=form)
+    codes, lens = E.synthetic(20000, 101, seed=74)
+    rng = np.random.default_rng(75)
+    motif = rng.integers(0, 4, size=30, dtype=np.uint8)
+    for _ in range(40):
+        i, j = rng.choice(20000, size=2, replace=False)
+        codes[i, 10:40] = motif
+        codes[j, 50:80] = motif
+    params = P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1)
+    full = ctx.gram(params, codes, lens, L.KMG_F64)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        got = _run_blocks(ctx, (codes, lens, d_codes, d_lens), params, L.KMG_F64, 8, [0], 1024,
+                          gather=3)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    assert ctx.blocks_wire() == 1
+    assert np.array_equal(got, full)
 
 
 @pytest.mark.parametrize("case", [0, 1, 2])
 def test_upper_triangle_8bit_slabs(ctx, data, case):
-    """Random sequences: every off-diagonal spectrum count fits 8 bits, so its slabs travel
-    as uint8 with the diagonal left out (K_ii from the locally computed diagonal); mismatch
-    slabs start at 16 bits (random 101-mers' mismatch counts pass 255)."""
+    """Random sequences: round slabs of spectrum and mismatch counts travel as uint8 with the
+    diagonal left out (K_ii from the locally computed diagonal)."""
     params, dt = CASES[case]
     codes, lens = data[0], data[1]
     full = ctx.gram(params, codes, lens, dt)
     got = _run_blocks(ctx, data, params, dt, 3, [0], 104, gather=3)
     assert np.array_equal(got, full)
-    assert ctx.blocks_wire() == (1 if case == 0 else 2)
+    assert ctx.blocks_wire() == 1
 
 
 def test_upper_triangle_one_rank_gather2(ctx, data):
@@ -204,8 +243,8 @@ def test_mismatch_device_rows_narrower_than_window(ctx):
 
 
 @pytest.mark.parametrize("params,dt,wire", [
-    (P.make(L.KMG_MISMATCH, k=10, m=1, window=101, normalize=1), L.KMG_F64, 2),  # pair table
-    (P.make(L.KMG_MISMATCH, k=8, m=1, window=101, normalize=0), L.KMG_I32, 2),   # slot table
+    (P.make(L.KMG_MISMATCH, k=10, m=1, window=101, normalize=1), L.KMG_F64, 1),  # pair table
+    (P.make(L.KMG_MISMATCH, k=8, m=1, window=101, normalize=0), L.KMG_I32, 1),   # slot table
     (P.make(L.KMG_SPECTRUM, k=12), L.KMG_I32, 1),
     (P.make(L.KMG_SPECTRUM, k=5), L.KMG_I32, 4),  # dense path: full-width slabs
 ])
