@@ -17,6 +17,7 @@
 #include <cstring>
 #include <algorithm>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -87,11 +88,11 @@ struct DevBuf {
 // "gather" = the RCCL row all-gather (kmg_allgather_rows)
 const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
                              "gram",    "extract",  "pack",  "features", "combine",
-                             "solve",   "slots",    "memset", "gather"};
-constexpr int kNumStages = 14;
+                             "solve",   "slots",    "memset", "gather", "unpack"};
+constexpr int kNumStages = 15;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
-  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER
+  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK
 };
 
 // Tuning knobs: read from the environment once per context (kmg_create) and again only on
@@ -109,7 +110,6 @@ struct Tuning {
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
   int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
-  int idx_v2 = 1;           // KMG_IDX_V2: index build without device-scope atomics
   int idx_seqs = 0;         // KMG_IDX_SEQS: sequences per partition block (0: auto, build_index)
   int idx_buckets = 0;      // KMG_IDX_BUCKETS: coarse buckets (0: 384 spectrum / 1024 mismatch)
   int idx_threads = 1024;   // KMG_IDX_THREADS
@@ -139,7 +139,6 @@ void read_tuning(Tuning &t) {
   t.algo = env_or("KMG_ALGO", d.algo);
   t.dense_kmax_sp = env_or("KMG_DENSE_KMAX_SP", d.dense_kmax_sp);
   t.dense_kmax_mm = env_or("KMG_DENSE_KMAX_MM", d.dense_kmax_mm);
-  t.idx_v2 = env_or("KMG_IDX_V2", d.idx_v2);
   t.idx_seqs = env_or("KMG_IDX_SEQS", d.idx_seqs);
   t.idx_buckets = env_or("KMG_IDX_BUCKETS", d.idx_buckets);
   t.idx_threads = env_or("KMG_IDX_THREADS", d.idx_threads);
@@ -164,7 +163,7 @@ struct kmg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf kmers, bcount, boff, bcursor, partials, tmp, off, ent, diagv, dsq, wtab;
+  DevBuf kmers, partials, tmp, off, ent, diagv, dsq, wtab;
   DevBuf hcnt, hstart;            // index build v2: per-(bucket, block) counts / local starts
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
   DevBuf dense_tiles;             // dense Gram tile order (dense_tile_order)
@@ -193,7 +192,6 @@ struct kmg_ctx {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_log;
   size_t ev_used = 0;
   int last_call_first = 0;
-  bool index_dirty = false;
   int64_t wtab_host[33] = {};
   bool wtab_valid = false;
   ncclComm_t comm = nullptr;
@@ -221,7 +219,8 @@ struct StageTimer {
   kmg_ctx *c;
   hipEvent_t end = nullptr;
   StageTimer(kmg_ctx *c_, int i) : c(c_) {
-    if (c->timing == 1 || (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET))) {
+    if (c->timing == 1 ||
+        (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET || i == ST_UNPACK))) {
       hipEvent_t b = pool_event(c);
       end = pool_event(c);
       (void)hipEventRecord(b, c->stream);
@@ -310,64 +309,29 @@ int build_index(kmg_ctx *c, IndexGeom &g, const Packed &pk, const uint8_t *codes
     return fail(KMG_EUNSUPPORTED, "too many k-mer occurrences for 32-bit offsets");
   const int64_t nblk = (g.n + g.seqs_per_block - 1) / g.seqs_per_block;
   const int64_t cap = (int64_t)g.seqs_per_block * g.pmax * g.copies;
-  const bool v2 = c->tune.idx_v2 && g.n > 0 && index_gather_lds(g, nblk) <= 150 * 1024 &&
-                  nblk * cap < ((int64_t)1 << 34);
-  if (codes && !v2) {
-    StageTimer t(c, ST_PACK);
-    KMG_HIP(launch_pack(codes, lens, g.n, ldc, g.window, const_cast<uint32_t *>(pk.w), c->stream));
-  }
-  if (v2) {
-    KMG_TRY(c->hcnt.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
-    KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
-    KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(nblk * cap)));
-    KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
-    KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 512)));  // + pad: whole-piece reads
-    {
-      StageTimer t(c, ST_PLACE);
-      KMG_HIP(launch_index_local(g, pk, codes, lens, ldc, (int)nblk, (uint32_t)cap,
-                                 c->hcnt.as<uint32_t>(), c->hstart.as<uint32_t>(),
-                                 c->tmp.as<uint32_t>(), c->stream));
-    }
-    {
-      StageTimer t(c, ST_FINE);
-      KMG_HIP(launch_index_gather(g, (int)nblk, (uint32_t)cap, c->hcnt.as<uint32_t>(),
-                                  c->hstart.as<uint32_t>(), c->tmp.as<uint32_t>(),
-                                  c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
-    }
-    return KMG_OK;
-  }
-  const bool realloc = c->bcount.bytes < sizeof(uint32_t) * (size_t)nbk ||
-                       c->bcursor.bytes < sizeof(uint32_t) * (size_t)nbk;
-  KMG_TRY(c->bcount.ensure(sizeof(uint32_t) * (size_t)nbk));
-  KMG_TRY(c->boff.ensure(sizeof(uint32_t) * (size_t)(nbk + 1)));
-  KMG_TRY(c->bcursor.ensure(sizeof(uint32_t) * (size_t)nbk));
-  KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(items > 0 ? items : 1)));
+  if (g.n == 0) return KMG_OK;
+  // the partition build (two launches, no device-scope atomics): its gather pass holds one
+  // fine histogram and two words per partition block in LDS
+  if (index_gather_lds(g, nblk) > 150 * 1024 || nblk * cap >= ((int64_t)1 << 34))
+    return fail(KMG_EUNSUPPORTED, "index build: %lld partition blocks exceed the LDS budget",
+                (long long)nblk);
+  KMG_TRY(c->hcnt.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
+  KMG_TRY(c->hstart.ensure(sizeof(uint32_t) * (size_t)(nbk * nblk)));
+  KMG_TRY(c->tmp.ensure(sizeof(uint32_t) * (size_t)(nblk * cap)));
   KMG_TRY(c->off.ensure(sizeof(uint32_t) * (size_t)(nb + 1)));
   KMG_TRY(c->ent.ensure(sizeof(uint16_t) * (size_t)(items + 512)));  // + pad: whole-piece reads
-  // bucket counters are zero between calls (the fine pass re-zeroes them); only a fresh
-  // allocation or an interrupted previous build needs an explicit clear
-  if (realloc || c->index_dirty) {
-    KMG_HIP(hipMemsetAsync(c->bcount.p, 0, c->bcount.bytes, c->stream));
-    KMG_HIP(hipMemsetAsync(c->bcursor.p, 0, c->bcursor.bytes, c->stream));
-  }
-  c->index_dirty = true;
-  {
-    StageTimer t(c, ST_COUNT);
-    KMG_HIP(launch_index_count(g, pk, c->bcount.as<uint32_t>(), c->stream));
-  }
   {
     StageTimer t(c, ST_PLACE);
-    KMG_HIP(launch_index_place(g, pk, c->bcount.as<uint32_t>(),
-                               c->bcursor.as<uint32_t>(), c->boff.as<uint32_t>(),
+    KMG_HIP(launch_index_local(g, pk, codes, lens, ldc, (int)nblk, (uint32_t)cap,
+                               c->hcnt.as<uint32_t>(), c->hstart.as<uint32_t>(),
                                c->tmp.as<uint32_t>(), c->stream));
   }
   {
     StageTimer t(c, ST_FINE);
-    KMG_HIP(launch_index_fine(g, c->boff.as<uint32_t>(), c->tmp.as<uint32_t>(),
-                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
-                              c->bcount.as<uint32_t>(), c->bcursor.as<uint32_t>(), c->stream));
+    KMG_HIP(launch_index_gather(g, (int)nblk, (uint32_t)cap, c->hcnt.as<uint32_t>(),
+                                c->hstart.as<uint32_t>(), c->tmp.as<uint32_t>(),
+                                c->off.as<uint32_t>(), c->ent.as<uint16_t>(), c->stream));
   }
-  c->index_dirty = false;
   return KMG_OK;
 }
 
@@ -1219,7 +1183,7 @@ int kmg_destroy(kmg_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->blas) rocblas_destroy_handle(c->blas);
-  DevBuf *bufs[] = {&c->kmers, &c->bcount, &c->boff,  &c->bcursor, &c->partials, &c->tmp,
+  DevBuf *bufs[] = {&c->kmers, &c->partials, &c->tmp, &c->esc, &c->esc_all, &c->esc_cnt,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
                     &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
@@ -1562,6 +1526,9 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
         KMG_HIP(hipEventRecord(c->ev_gath[t & 1], c->comm_stream));
         KMG_HIP(hipStreamWaitEvent(post, c->ev_gath[t & 1], 0));
       }
+      // unpack / mirror: timed when it runs on the context stream (no RCCL; the one-GPU
+      // rehearsal the bench's multi-GPU projection reads)
+      std::unique_ptr<StageTimer> ut(post == c->stream ? new StageTimer(c, ST_UNPACK) : nullptr);
       if (wire == KMG_U8)
         KMG_HIP(launch_tri_unpack8((const uint8_t *)S, w, round, c0, n, d_out, ld_out, out_dtype,
                                    p->normalize, c->diagv.as<double>(), c->dsq.as<double>(), post));
@@ -1570,6 +1537,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                                     p->normalize, c->diagv.as<double>(), c->dsq.as<double>(), post));
       else
         KMG_HIP(launch_tri_unpack(S, w, round, c0, n, d_out, ld_out, (int)esz, post));
+      ut.reset();
       KMG_HIP(hipEventRecord(c->ev_tri[t & 1], post));
       // the next Gram launch (round t + 1) writes the slab round t - 1 used
       if (t >= 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_tri[(t - 1) & 1], 0));

@@ -12,13 +12,9 @@
 // the dropped position << 14 (MM).  Order inside a bin is unspecified (the Gram is
 // an integer sum, so results do not depend on it).
 //
-// Build = two-pass MSD partition with LDS histograms (no per-occurrence global
-// atomics): (1) count occurrences per coarse bucket (bins >> fine_bits), LDS
-// histogram per block, one global add per (block, bucket); (2) exclusive scan of the
-// bucket counts; (3) per block, reserve a range per bucket (one returning global add
-// per (block, bucket)) and place items in the bucket arrays with LDS cursors;
-// (4) one block per bucket: LDS histogram + scan of its fine bins -> off[], then
-// place the items with LDS cursors into ent[].
+// Build = two-launch MSD partition with LDS histograms, no global atomics (see
+// "index build" below): per-block local sort by coarse bucket, then one block per bucket
+// places its fine bins.
 #include "kmg_internal.h"
 
 namespace kmg {
@@ -115,21 +111,6 @@ __device__ __forceinline__ void for_items(const IndexGeom &g, const Packed &pk, 
   }
 }
 
-__global__ __launch_bounds__(IDX_THREADS) void bucket_count_kernel(IndexGeom g, Packed pk, uint32_t *__restrict__ bcount) {
-  extern __shared__ __align__(16) uint32_t sm[];
-  const int nbk = (int)g.nbuckets();
-  uint32_t *hist = sm;
-  uint32_t *srec = hist + nbk;
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x) hist[b] = 0;
-  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
-  const int ns = stage_rows(g, pk, srec, j0);
-  const int fb = g.fine_bits;
-  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
-  __syncthreads();
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x)
-    if (hist[b]) atomicAdd(&bcount[b], hist[b]);
-}
-
 // block-wide exclusive scan over an LDS array of length len (in place); returns total
 __device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
   const int nt = blockDim.x, t = threadIdx.x;
@@ -162,89 +143,9 @@ __device__ uint32_t lds_excl_scan(uint32_t *a, int len, uint32_t *wtmp) {
   return total;
 }
 
-// Every block recomputes the exclusive scan of the bucket totals (nbuckets <= 16384,
-// cheap) so no separate scan launch is needed; block 0 publishes it as boff[] for the
-// fine pass.  Positions inside a bucket: base + one returning add per (block, bucket)
-// on the relative cursor bcursor[] (zero on entry; re-zeroed by the fine pass).
-__global__ __launch_bounds__(IDX_THREADS) void bucket_place_kernel(IndexGeom g, Packed pk, const uint32_t *__restrict__ bcount,
-                                                                   uint32_t *__restrict__ bcursor,
-                                                                   uint32_t *__restrict__ boff,
-                                                                   uint32_t *__restrict__ tmp) {
-  extern __shared__ __align__(16) uint32_t sm[];
-  __shared__ uint32_t wtmp[IDX_THREADS / 64];
-  const int nbk = (int)g.nbuckets();
-  uint32_t *hist = sm;
-  uint32_t *base = hist + nbk;
-  uint32_t *srec = base + nbk;
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
-    hist[b] = 0;
-    base[b] = bcount[b];
-  }
-  __syncthreads();
-  const uint32_t total = lds_excl_scan(base, nbk, wtmp);
-  if (blockIdx.x == 0) {
-    for (int b = threadIdx.x; b < nbk; b += blockDim.x) boff[b] = base[b];
-    if (threadIdx.x == 0) boff[nbk] = total;
-  }
-  const int64_t j0 = (int64_t)blockIdx.x * g.seqs_per_block;
-  const int ns = stage_rows(g, pk, srec, j0);
-  const int fb = g.fine_bits;
-  const uint32_t fmask = (1u << fb) - 1u;
-  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t) { atomicAdd(&hist[bin >> fb], 1u); });
-  __syncthreads();
-  // reserve this block's range inside every bucket it touches
-  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
-    const uint32_t c = hist[b];
-    if (c) hist[b] = base[b] + atomicAdd(&bcursor[b], c);
-  }
-  __syncthreads();
-  for_items(g, pk, srec, ns, j0, [&](uint32_t bin, uint32_t val) {
-    const uint32_t pos = atomicAdd(&hist[bin >> fb], 1u);
-    tmp[pos] = ((bin & fmask) << 16) | val;
-  });
-}
-
-// one block per coarse bucket: fine histogram -> off[], then place values into ent[]
-__global__ __launch_bounds__(FINE_THREADS) void bucket_fine_kernel(IndexGeom g, const uint32_t *__restrict__ boff,
-                                                                  const uint32_t *__restrict__ tmp,
-                                                                  uint32_t *__restrict__ off,
-                                                                  uint16_t *__restrict__ ent,
-                                                                  uint32_t *__restrict__ bcount,
-                                                                  uint32_t *__restrict__ bcursor) {
-  extern __shared__ __align__(16) uint32_t sm[];
-  __shared__ uint32_t wtmp[FINE_THREADS / 64];
-  const int fb = g.fine_bits;
-  const int nf = 1 << fb;
-  uint32_t *fh = sm;
-  const int b = blockIdx.x;
-  const uint32_t s0 = boff[b], s1 = boff[b + 1];
-  if (threadIdx.x == 0) {  // leave the counters zero for the next call (no memset launch)
-    bcount[b] = 0;
-    bcursor[b] = 0;
-  }
-  for (int f = threadIdx.x; f < nf; f += blockDim.x) fh[f] = 0;
-  __syncthreads();
-  for (uint32_t t = s0 + threadIdx.x; t < s1; t += blockDim.x) atomicAdd(&fh[tmp[t] >> 16], 1u);
-  __syncthreads();
-  lds_excl_scan(fh, nf, wtmp);
-  const int64_t nb = g.nbins();
-  const int64_t bin0 = (int64_t)b << fb;
-  for (int f = threadIdx.x; f < nf; f += blockDim.x) {
-    const int64_t bin = bin0 + f;
-    if (bin < nb) off[bin] = s0 + fh[f];
-  }
-  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) off[nb] = s1;
-  __syncthreads();
-  for (uint32_t t = s0 + threadIdx.x; t < s1; t += blockDim.x) {
-    const uint32_t it = tmp[t];
-    const uint32_t pos = atomicAdd(&fh[it >> 16], 1u);
-    ent[s0 + pos] = (uint16_t)(it & 0xFFFFu);
-  }
-}
-
-// ------------------------------------------------------------------ index build, v2
+// ------------------------------------------------------------------ index build
 // Two launches, no device-scope atomics and no communication between the workgroups of
-// a launch (v1's count/place passes each pay one device-scope atomic per (block, coarse
+// a launch (an earlier atomics-based build paid one device-scope atomic per (block, coarse
 // bucket) on a few hundred hot words, serialised at the memory-side atomic unit):
 //  (1) part_local_kernel: block q stages its sequences, builds the LDS histogram over the
 //      coarse buckets, scans it, and writes its items bucket-sorted into its own region
@@ -763,34 +664,6 @@ hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, in
 // ------------------------------------------------------------------ launchers
 static size_t part_lds(const IndexGeom &g, const Packed &pk, int arrays) {
   return sizeof(uint32_t) * ((size_t)g.nbuckets() * arrays + (size_t)g.seqs_per_block * pk.ldp) + 16;
-}
-
-hipError_t launch_index_count(const IndexGeom &g, const Packed &pk, uint32_t *bcount,
-                              hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_count_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, pk, 1), s,
-                     g, pk, bcount);
-  return hipGetLastError();
-}
-
-hipError_t launch_index_place(const IndexGeom &g, const Packed &pk, const uint32_t *bcount,
-                              uint32_t *bcursor, uint32_t *boff, uint32_t *tmp, hipStream_t s) {
-  if (g.n == 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((g.n + g.seqs_per_block - 1) / g.seqs_per_block);
-  hipLaunchKernelGGL(bucket_place_kernel, dim3(blocks), dim3(g.part_threads), part_lds(g, pk, 2), s,
-                     g, pk, bcount, bcursor, boff, tmp);
-  return hipGetLastError();
-}
-
-hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
-                             uint32_t *off, uint16_t *ent, uint32_t *bcount, uint32_t *bcursor,
-                             hipStream_t s) {
-  const int64_t nbk = g.nbuckets();
-  const size_t lds = sizeof(uint32_t) * ((size_t)1 << g.fine_bits);
-  hipLaunchKernelGGL(bucket_fine_kernel, dim3((unsigned)nbk), dim3(FINE_THREADS), lds, s, g, boff,
-                     tmp, off, ent, bcount, bcursor);
-  return hipGetLastError();
 }
 
 size_t index_gather_lds(const IndexGeom &g, int64_t nblk) {

@@ -82,21 +82,12 @@ __device__ __forceinline__ uint32_t pk_window(const uint32_t *rec, int cw, int a
 hipError_t launch_pack(const uint8_t *codes, const int32_t *lens, int64_t n, int64_t ldc,
                        int window, uint32_t *packed, hipStream_t s);
 
-hipError_t launch_index_count(const IndexGeom &g, const Packed &pk, uint32_t *bcount,
-                              hipStream_t s);
 // exclusive scan of hist[0..nb) into off[0..nb] (off[nb] = total); cursor = off[0..nb)
 hipError_t launch_scan(const uint32_t *hist, uint32_t *off, uint32_t *cursor, int64_t nb,
                        uint32_t *partials, hipStream_t s);
 size_t scan_partials_words(int64_t nb);
-// place: every block scans the bucket totals itself (block 0 publishes boff[])
-hipError_t launch_index_place(const IndexGeom &g, const Packed &pk, const uint32_t *bcount,
-                              uint32_t *bcursor, uint32_t *boff, uint32_t *tmp, hipStream_t s);
-// fine: per-bucket fine histogram -> off[], ent[]; re-zeroes bcount[]/bcursor[]
-hipError_t launch_index_fine(const IndexGeom &g, const uint32_t *boff, const uint32_t *tmp,
-                             uint32_t *off, uint16_t *ent, uint32_t *bcount, uint32_t *bcursor,
-                             hipStream_t s);
 hipError_t launch_extract(const IndexGeom &g, const Packed &pk, uint32_t *kmers, hipStream_t s);
-// index build v2 (no device-scope atomics): per-block local sort, then per-bucket gather.
+// index build (no device-scope atomics): per-block local sort, then per-bucket gather.
 // hcnt/hstart: nbuckets x nblk (bucket-major); tmp: nblk x cap items.  codes != nullptr:
 // the local pass also packs the sequences into pk (launch_pack fused into the first pass).
 size_t index_gather_lds(const IndexGeom &g, int64_t nblk);

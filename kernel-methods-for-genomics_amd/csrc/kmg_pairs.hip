@@ -77,46 +77,51 @@ __device__ __forceinline__ uint32_t nib_sum(uint32_t x) {
 }  // namespace
 
 // ------------------------------------------------------------------ table build
-// one thread per 8 groups (one nibble word of a summary record); 4 threads per record
+// one thread per group (its 16 sub-bins' counts from the exact index, all loads issued
+// together); 32 adjacent lanes = one summary record: nibble words, line total and wide bits
+// by lane reductions
 __global__ __launch_bounds__(256) void pl_count_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
                                                        uint32_t *__restrict__ summary,
                                                        uint32_t *__restrict__ rtot) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nrec = pg.nrec();
-  const bool live = t < nrec * 4;
-  uint32_t word = 0, tot = 0, wide = 0;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool live = g < pg.ngroups();
+  uint32_t nl = 0;
+  bool wide = false;
   if (live) {
-    const int64_t g0 = (t >> 2) * 32 + (t & 3) * 8;
-    for (int r = 0; r < 8; ++r) {
-      const int64_t g = g0 + r;
-      if (g >= pg.ngroups()) break;
-      int pi, p, q, c;
-      uint32_t key;
-      pl_decode_group(pg, g, pi, p, q, c, key);
-      const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
-      uint32_t n = 0;
-      for (uint32_t b = 0; b < 16; ++b) {
-        const uint32_t z = pair_insert(key, pg.k, p, q, b >> 2, b & 3u);
-        n += xo[z + 1] - xo[z];
-      }
-      const uint32_t nl = pl_lines(n, pi >= pg.corr0);
-      if (nl == PL_WIDE) {
-        wide |= 1u << (8 * (t & 3) + r);
-      } else {
-        word |= nl << (4 * r);
-        tot += nl;
-      }
+    int pi, p, q, c;
+    uint32_t key;
+    pl_decode_group(pg, g, pi, p, q, c, key);
+    const uint32_t *xo = xoff + (size_t)c * ((size_t)pg.nkeys2 << 4);
+    uint32_t lo[16], hi[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const uint32_t z = pair_insert(key, pg.k, p, q, (uint32_t)b >> 2, (uint32_t)b & 3u);
+      lo[b] = xo[z];
+      hi[b] = xo[z + 1];
     }
-    summary[(t >> 2) * 8 + 1 + (t & 3)] = word;
+    uint32_t n = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) n += hi[b] - lo[b];
+    const uint32_t l = pl_lines(n, pi >= pg.corr0);
+    wide = l == PL_WIDE;
+    nl = wide ? 0u : l;
   }
-  // record totals and wide bits over its 4 threads (adjacent lanes)
-  tot += __shfl_xor(tot, 1, 64);
-  tot += __shfl_xor(tot, 2, 64);
-  wide |= __shfl_xor(wide, 1, 64);
-  wide |= __shfl_xor(wide, 2, 64);
-  if (live && (t & 3) == 0) {
-    rtot[t >> 2] = tot;
-    summary[(t >> 2) * 8 + 5] = wide;
+  // nibble word of lanes 8w..8w+7 (group r of the record at bits 4 (r & 7))
+  uint32_t word = nl << (4 * (lane & 7));
+  word |= (uint32_t)__shfl_xor((int)word, 1, 64);
+  word |= (uint32_t)__shfl_xor((int)word, 2, 64);
+  word |= (uint32_t)__shfl_xor((int)word, 4, 64);
+  uint32_t tot = nl;
+  uint64_t wb = __ballot(wide);
+  const uint32_t wbits = (uint32_t)(wb >> (lane & 32));
+#pragma unroll
+  for (int d = 1; d < 32; d <<= 1) tot += (uint32_t)__shfl_xor((int)tot, d, 64);
+  const int64_t rec = g >> 5;
+  if (live && (lane & 7) == 0) summary[rec * 8 + 1 + ((lane >> 3) & 3)] = word;
+  if (live && (lane & 31) == 0) {
+    rtot[rec] = tot;
+    summary[rec * 8 + 5] = wbits;
   }
 }
 
@@ -195,11 +200,15 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
     img[lg][w] = pl_dummy(dcol, bk, 0) | (pl_dummy(dcol, bk, 1) << 16);
   }
   uint32_t base = 0;
-  if (live) {
+  if (live) {  // record base + the line counts of the record's earlier groups (nibbles)
     const int64_t rec = g >> 5;
-    const int r = (int)(g & 31);
+    const int r = (int)(g & 31), wsel = r >> 3, sh = 4 * (r & 7);
+    const uint32_t *sw = summary + rec * 8 + 1;  // nibble words 1..4
+    const uint32_t wd[4] = {sw[0], sw[1], sw[2], sw[3]};
     base = rbase[rec] + 1u;
-    for (int j = 0; j < r; ++j) base += (summary[rec * 8 + 1 + (j >> 3)] >> (4 * (j & 7))) & 15u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      base += nib_sum(wd[q] & (q < wsel ? 0xFFFFFFFFu : (q == wsel ? ((1u << sh) - 1u) : 0u)));
   }
   if (blockIdx.x == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
     uint32_t w[4];
@@ -271,7 +280,7 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
 
 hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
                            uint32_t *rtot, hipStream_t s) {
-  const int64_t threads = pg.nrec() * 4;
+  const int64_t threads = pg.nrec() * 32;
   if (threads == 0) return hipSuccess;
   hipLaunchKernelGGL(pl_count_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, pg,
                      xoff, summary, rtot);

@@ -11,7 +11,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libkmgram.so")
+# KMGRAM_LIB: another build of the same ABI (the host-ASan build, tools/asan_tests.sh)
+LIB_PATH = os.environ.get("KMGRAM_LIB") or os.path.join(os.path.dirname(_HERE), "libkmgram.so")
 
 (KMG_OK, KMG_EINVAL, KMG_EUNSUPPORTED, KMG_EHIP, KMG_ENOMEM, KMG_ERCCL, KMG_ENODEV,
  KMG_ESINGULAR) = range(8)

@@ -123,11 +123,10 @@ def test_spectrum_ragged_and_chunks(ctx, tune):
         assert np.array_equal(K.astype(np.int64), ref), chunk
 
 
-@pytest.mark.parametrize("v2", ["0", "1"])
-def test_index_builds(ctx, tune, v2):
-    """Both posting-index builds (v1: atomics-based MSD partition; v2: per-block local
-    sort + per-bucket gather) give bit-identical Grams, over chunkings and block sizes."""
-    tune(KMG_IDX_V2=v2, KMG_ALGO=2)
+def test_index_builds(ctx, tune):
+    """The posting-index build (per-block local sort + per-bucket gather) gives bit-identical
+    Grams over chunkings and partition block sizes."""
+    tune(KMG_ALGO=2)
     codes, lens = E.synthetic(2500, 101, seed=91)
     codes[3] = 0
     ref = cref.spectrum(codes, lens, 8)

@@ -32,7 +32,7 @@ DEFAULT = {
 }
 KNOBS = ("KMG_ALGO", "KMG_MM_SLOTV", "KMG_SP_PERSIST", "KMG_MM_TRI", "KMG_MM_PORDER", "KMG_SP_NT", "KMG_SP_CHUNK", "KMG_MM_G", "KMG_MM_U", "KMG_MM_V", "KMG_MM_D", "KMG_MM_THREADS",
          "KMG_MM_CHUNK", "KMG_IDX_SEQS", "KMG_IDX_THREADS", "KMG_IDX_BUCKETS", "KMG_MM_VARIANT",
-         "KMG_IDX_V2", "KMG_SP_G", "KMG_DIAG_SMALL")
+         "KMG_SP_G", "KMG_DIAG_SMALL")
 
 
 def main():
