@@ -40,7 +40,8 @@ import numpy as np  # noqa: E402
 from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
-from kmgram.shard import block_cyclic_ranges, default_block, rows_padded, triangle_rounds  # noqa: E402
+from kmgram.shard import (block_cyclic_ranges, default_block, rows_padded,  # noqa: E402
+                          scaling_projection, triangle_rounds)
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_MODE = 2  # G > 1: upper-triangle round slabs + local mirror (--gather-mode 1: full rows)
@@ -232,7 +233,7 @@ def _rows_product(ab):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(name, n, budget_s, workers=None):
+def cpu_baseline(name, n, budget_s, seed, workers=None):
     """The strongest CPU restatement of the reference we have, on this box's host cores:
     scipy-sparse Phi Phi^T (oracle/cpu_ref.py spectrum_phi / mismatch_phi = the reference's
     own feature maps get_phi_u / get_phi_km, kernels.py:12-25, 161-175, and its np.dot pair
@@ -244,8 +245,7 @@ def cpu_baseline(name, n, budget_s, workers=None):
     import cpu_ref
     global _F, _FT
     workers = workers or min(16, os.cpu_count() or 1)
-    seed = 2 if name == "spectrum_k8" else 3
-    codes, lens = E.synthetic(n, 101, seed=seed)
+    codes, lens = E.synthetic(n, 101, seed=seed)  # the timed workload's own input
     t0 = time.perf_counter()
     _F = (cpu_ref.spectrum_phi(codes, lens, 8) if name == "spectrum_k8"
           else cpu_ref.mismatch_phi(codes, lens, 9, 1))
@@ -276,7 +276,8 @@ def cpu_baseline(name, n, budget_s, workers=None):
             "sample": f"scipy-sparse Phi Phi^T (oracle/cpu_ref.py {label}): Phi of all {n} "
                       f"sequences {t_phi:.2f} s (1 process) + rows 0..{rows} x {n} over "
                       f"{len(blocks)} forked processes in {t_rows:.2f} s wall, whole job "
-                      f"extrapolated to {t_job:.1f} s",
+                      + (f"{t_job:.1f} s (every row computed)" if rows >= n else
+                         f"extrapolated to {t_job:.1f} s"),
             "one_process": {"value": n * n / t_job1, "cores": 1,
                             "sample": f"{r} rows in {t:.2f} s, whole job {t_job1:.1f} s"}}
 
@@ -373,6 +374,67 @@ def extras(ctx, cpu_rates, steps4):
     del K
     out["run_py_kernels_n9000"] = run_py_workload(ctx)
     out["downstream"] = downstream(ctx)
+    return out
+
+
+def _hip():
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def host_path_config4(ctx, n=100000, slab_rows=2500, f64=True):
+    """SURVEY §8d's host legs at BASELINE configs[3] (get_spectrum_K returns the host array,
+    kernels.py:47): H2D of the codes, then kmg_gram_to_host — device row slabs of one index
+    build, each slab's D2H (second stream) overlapping the next slab's Gram — into a pinned
+    host buffer, int32 (40 GB, exact counts) and float64 (80 GB, what the reference
+    materialises).  Never `value`: PCIe-bound."""
+    hip = _hip()
+    codes, lens = E.synthetic(n, 101, seed=4)
+    ldc = codes.shape[1]
+    out = {"N": n, "slab_rows": slab_rows}
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.synchronize()
+        out["h2d_codes_ms"] = (time.perf_counter() - t0) * 1e3
+        out["h2d_bytes"] = codes.nbytes + lens.nbytes
+        p8 = P.make(L.KMG_SPECTRUM, k=8)
+        for dt, name in ((L.KMG_I32, "int32"), (L.KMG_F64, "float64")):
+            if dt == L.KMG_F64 and not f64:
+                continue
+            esz = np.dtype(L.DTYPES[dt]).itemsize
+            nbytes = n * n * esz
+            hp = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            rc = hip.hipHostMalloc(ctypes.byref(hp), ctypes.c_size_t(nbytes), 0)
+            t_alloc = time.perf_counter() - t0
+            if rc != 0 or not hp.value:
+                out[name] = {"error": f"hipHostMalloc({nbytes}) = {rc}"}
+                continue
+            try:
+                buf = (ctypes.c_char * nbytes).from_address(hp.value)
+                K = np.frombuffer(buf, dtype=L.DTYPES[dt]).reshape(n, n)
+                ctx.gram_to_host(p8, d_codes, d_lens, n, ldc, dt, slab_rows, K)  # warm (index, slabs)
+                t0 = time.perf_counter()
+                ctx.gram_to_host(p8, d_codes, d_lens, n, ldc, dt, slab_rows, K)
+                t = time.perf_counter() - t0
+                import cref
+                r = n // 2
+                ok = bool(np.array_equal(K[r].astype(np.int64),
+                                         cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0]))
+                out[name] = {"ms": t * 1e3, "bytes": nbytes, "d2h_GBps": nbytes / t / 1e9,
+                             "pairs_per_s": n * n / t, "pinned_alloc_s": t_alloc,
+                             "spot_check_row": r, "spot_check": ok}
+                del K, buf
+            finally:
+                hip.hipHostFree(hp)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    out["note"] = ("kmg_gram_to_host into hipHostMalloc'd memory; the device build alone is "
+                   "the headline ms_per_step (inputs resident)")
     return out
 
 
@@ -547,6 +609,40 @@ def gather_roofline(res, world, esz):
             "frac": recv / t / XGMI_IN_PEAK}
 
 
+def _chunked(n, max_chunk):
+    """Column chunk width of a posting-list build: n split evenly into ceil(n / max_chunk)."""
+    nch = -(-n // max_chunk)
+    return -(-n // nch)
+
+
+def projection(sp, n, extra):
+    """G = 2/4/8 predictions for configs 4 and 5 from THIS run's one-GPU stage times
+    (kmgram.shard.scaling_projection): index and Gram device times, the measured
+    fill rate, uint8 round slabs (spectrum: diagonal from each rank; mismatch: escape list),
+    xGMI at 76.5 GB/s per link and direction with no efficiency loss (an upper bound)."""
+    fill = sp.get("write_ceiling_GBps") or 6000.0
+    st = sp["stages_ms"]
+    t_index = sum(v for k, v in st.items() if k in ("count", "scan", "place", "fine", "pack"))
+    out = {"model": "kmgram.shard.scaling_projection (DESIGN.md §5); not measured on >1 GPU",
+           "assumptions": {"xgmi_link_GBps": XGMI_IN_PEAK / 7 / 1e9, "link_eff": 1.0,
+                           "fill_GBps": fill, "wire_bytes": 1}}
+    out["config4_spectrum_k8_n%d" % n] = {
+        str(g): v for g, v in scaling_projection(
+            n, sp["ms_per_step"], t_index, st["gram"], fill, 4, 1,
+            chunk=_chunked(n, 24576)).items()}
+    c5 = (extra or {}).get("config5_mismatch_k9_n200000_full_1gpu")
+    if c5:
+        s5 = c5["stages_ms"]
+        t5_index = sum(v for k, v in s5.items() if k in ("count", "scan", "place", "fine", "pack",
+                                                         "slots"))
+        n5 = c5["N"]
+        out["config5_mismatch_k9_n200000_raw_int32"] = {
+            str(g): v for g, v in scaling_projection(
+                n5, c5["ms_per_step"], t5_index, s5["gram"], fill, 4, 1,
+                chunk=_chunked(n5, 28572)).items()}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -580,8 +676,9 @@ def main():
         ctx.comm_init(uid, dist.world, dist.rank)
     n = args.n
 
+    sp_seed = 4 if n == 100000 else 2
     sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
-                   4 if n == 100000 else 2, args.steps, args.warmup, check_spectrum)
+                   sp_seed, args.steps, args.warmup, check_spectrum)
     mm = None
     if not args.no_mismatch:
         mm = run_build(ctx, dist, "mismatch_k9_m1",
@@ -595,9 +692,9 @@ def main():
                        200000, 5, 2, 1, check_mismatch_raw)
     cpu = {}
     if dist.world == 1 and not args.no_cpu:
-        cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget)
+        cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget, sp_seed)
         if mm:
-            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", args.mm_n, args.cpu_budget / 2)
+            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", args.mm_n, args.cpu_budget / 2, 3)
     extra = None
     if dist.world == 1 and not args.no_extra:
         extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(20, args.steps))
@@ -681,6 +778,8 @@ def main():
             line["secondary"]["cpu_baseline"] = cpu["mismatch_k9_m1"]
     if extra:
         line["configs"] = extra
+    if dist.world == 1:
+        line["projection"] = projection(sp, n, extra)
     if dist.rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     dist.close()

@@ -238,11 +238,13 @@ int kmg_stream(kmg_ctx *ctx, void **hip_stream);
 
 /* Per-stage device timings from HIP events recorded on the context stream around
  * every launch while timing is enabled (kmg_set_timing(ctx,1); kmg_set_timing(ctx,2)
- * times only the "gram", "gather" and "memset" stages, 2 events per Gram launch instead
- * of 2 per stage); nothing is synchronised until a stage time is read.  Stage names: "count", "scan",
- * "place", "fine", "diag", "gram", "extract", "features", "pack" (2-bit packing of the
- * input), "slots" (mismatch slot table), "combine", "solve", "memset", "gather" (the RCCL
- * all-gathers of kmg_gram_blocks, timed on their own stream).
+ * times only the "gram", "gather", "unpack", "mirror" and "memset" stages, 2 events per
+ * Gram launch instead of 2 per stage); nothing is synchronised until a stage time is read.
+ * Stage names: "count", "scan", "place", "fine", "diag", "gram", "extract", "features",
+ * "pack" (2-bit packing of the input), "slots" (mismatch slot / pair tables), "combine",
+ * "solve", "memset", "gather" (the RCCL all-gathers of kmg_gram_blocks, timed on their own
+ * stream), "unpack" (round-slab assembly), "mirror" (lower block triangle of a full square
+ * mismatch K built by its upper block triangle).
  *   kmg_stage_ms:    that stage in the last call (-1 if it did not run)
  *   kmg_stage_stats: sum and count over every call since kmg_timing_reset */
 int kmg_set_timing(kmg_ctx *ctx, int32_t enable);

@@ -88,11 +88,12 @@ struct DevBuf {
 // "gather" = the RCCL row all-gather (kmg_allgather_rows)
 const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
                              "gram",    "extract",  "pack",  "features", "combine",
-                             "solve",   "slots",    "memset", "gather", "unpack"};
-constexpr int kNumStages = 15;
+                             "solve",   "slots",    "memset", "gather", "unpack",
+                             "mirror"};
+constexpr int kNumStages = 16;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
-  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK
+  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK, ST_MIRROR
 };
 
 // Tuning knobs: read from the environment once per context (kmg_create) and again only on
@@ -102,7 +103,8 @@ struct Tuning {
   int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
   int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table,
                             // 3 drop-two pair lines (kmg_pairs.hip)
-  int pl_depth = 4;         // KMG_PL_D: pair-lines Gram, ring steps in flight per wave (4/6/8)
+  int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
+                            // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
   int pl_dbg = 0;           // KMG_PL_DBG: diagnostics only (wrong results): 1 no correction
                             // weights, 2 no bank rotation
@@ -145,9 +147,9 @@ void read_tuning(Tuning &t) {
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
-  t.pl_depth = env_or("KMG_PL_D", d.pl_depth);
   t.pl_dbg = env_or("KMG_PL_DBG", d.pl_dbg);
   t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
+  t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
@@ -220,7 +222,8 @@ struct StageTimer {
   hipEvent_t end = nullptr;
   StageTimer(kmg_ctx *c_, int i) : c(c_) {
     if (c->timing == 1 ||
-        (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET || i == ST_UNPACK))) {
+        (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET || i == ST_UNPACK ||
+                            i == ST_MIRROR))) {
       hipEvent_t b = pool_event(c);
       end = pool_event(c);
       (void)hipEventRecord(b, c->stream);
@@ -468,7 +471,18 @@ int pair_chunk(int64_t n, int pmax, int k, int cap) {
 // int32 LDS accumulator fits beside the kernel's wave queues and whose per-chunk table
 // stays Infinity-Cache sized (<= 192 MB: the chunk-major grid reads one chunk's table at a
 // time, and the K rows stream past it).
-int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
+// tri_esz > 0 (a full square K by its upper block triangle, OutSpec::tri): a row reads
+// (nch + 1) / 2 chunks on average and the mirror moves 2 tri_esz (nch - 1) / (2 nch) n^2
+// bytes; lines are priced at the measured random-line rate of the Infinity Cache (54 G
+// lines/s), the mirror at 5.5 TB/s.
+double tri_cost(int64_t n, int pmax, double lines_per_window_chunk, int64_t nch, int tri_esz) {
+  if (tri_esz <= 0) return (double)nch * lines_per_window_chunk;
+  const double lines = (double)n * pmax * lines_per_window_chunk * (double)(nch + 1) / 2.0;
+  const double mirror = 2.0 * tri_esz * (double)n * n * (double)(nch - 1) / (2.0 * nch);
+  return lines / 54e9 + mirror / 5.5e12;
+}
+
+int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
   const double keys = (double)pow4(k - 2);
   const int np = k * (k - 1) / 2;
   int64_t max_chunk = (160 * 1024 / 4 - 66 - pmax - ldp - KMG_PAIRS_MAX - 16 * KMG_PL_WAVE_WORDS) & ~7LL;
@@ -494,8 +508,14 @@ int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
     const double per = (np - k) * eu + k * ec;  // lines per window and chunk
     const double table = per * keys * 128.0;      // bytes of one chunk's table
     if (table > 192e6 && nch < nch0 + 64) continue;
-    if (nch * per < best_lines - 1e-9) {
-      best_lines = nch * per;
+    if ((double)nch * (double)pow4(k) > (double)(1 << 28)) continue;  // exact index bins
+    if ((double)np * nch * keys * 16.0 >= 4294967296.0) continue;      // pl_pack work-items
+    // + a quarter line per list for its summary record and decode, which every (window,
+    // pair, chunk) pays however small the group (without it, tiny groups at large k would
+    // make every extra chunk look free)
+    const double cost = tri_cost(n, pmax, per + 0.25 * np, nch, tri_esz);
+    if (cost < best_lines * (1.0 - 1e-12)) {
+      best_lines = cost;
       best = ch;
     }
   }
@@ -511,7 +531,7 @@ int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
 // MM(9,1) (25000-row slab: 10 chunks 46.8 ms, 8 chunks 38.7, 7 chunks 34.8, 6 chunks
 // 35.7; profiles/r02ac_*).  Largest chunk: the int32 LDS accumulator plus the kernel's
 // tables (launch_gram_mismatch1_slots) in 160 KB, and uint16 entries (<= 65536 columns).
-int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
+int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
   const int nsub = k + 3 * k * (k - 1) / 2;
   int64_t max_chunk = (160 * 1024 / 4 - (int64_t)pmax * k - nsub - ldp) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536);
@@ -530,8 +550,9 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap) {
       if (x > 0) pr *= mean / x;
       cdf += pr;
     }
-    const double cost = (double)nch * (1.0 + 6.0 * std::max(0.0, 1.0 - cdf));
-    if (cost < best_cost - 1e-9) {
+    const double per = (double)nsub * (1.0 + 6.0 * std::max(0.0, 1.0 - cdf));
+    const double cost = tri_cost(n, pmax, per, nch, tri_esz);
+    if (cost < best_cost * (1.0 - 1e-12)) {
       best_cost = cost;
       best = ch;
     }
@@ -800,6 +821,20 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const SmPath path = sm_path(c->tune, p, g.pmax);
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS, use_pl = path == SM_PL;
       const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl;
+      // a full square K (one range over [0, n), every column written) of a mismatch
+      // posting-list formulation: built by its upper block triangle, then mirrored
+      // (OutSpec::tri; set below once the chunking is known)
+      const bool square = ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
+                          ranges[0].col_lo == 0 && !after && !narrow && n > 0;
+      const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_pl))
+                              ? (int)dtype_size(dt) : 0;
+      auto mirror = [&]() -> int {
+        if (!o.tri) return KMG_OK;
+        StageTimer t(c, ST_MIRROR);
+        KMG_HIP(launch_mirror_chunks(ranges[0].out, ranges[0].ld > 0 ? ranges[0].ld : ld, n,
+                                     g.chunk, (int)dtype_size(dt), c->stream));
+        return KMG_OK;
+      };
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       const int mm_eff = mm ? std::min(p->m, k) : 0;
@@ -858,6 +893,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
         choose_chunks(g, pair_chunk(n, g.pmax, k, c->tune.mm_chunk));
+        o.tri = tri_esz > 0 && g.nchunks > 1;
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         PairGeom pg{};
         pg.k = k;
@@ -896,12 +932,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             o.dsq = c->dsq.as<double>();
           }
         }
-        return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_pairs(pg, g, pkd, c->pr_summary.as<uint32_t>(),
                                              c->pr_lines.as<uint4>(), nlines,
                                              c->off.as<uint32_t>(), c->ent.as<uint16_t>(), r0,
                                              r1, (int)w[0], (int)w[1], (int)w[2], oq, c->stream);
-        }, true);
+        }, true));
+        return mirror();
       }
       if (use_pl) {
         // exact k-mer index over the mismatch window (kernels.py:171), then the pair-lines
@@ -909,7 +946,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // correction pairs G(r) = {r-1, r} (r >= 1) and {0, k-1} (outer letter k-1)
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk));
+        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz));
+        o.tri = tri_esz > 0 && g.nchunks > 1;
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         PairGeom pg{};
         pg.k = k;
@@ -953,12 +991,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             o.dsq = c->dsq.as<double>();
           }
         }
-        return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_pl(pg, g, pkd, c->pr_summary.as<uint32_t>(),
                                           c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
                                           c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, c->tune.pl_depth, c->tune.pl_dbg);
-        }, true);
+                                          (int)w[2], oq, c->stream, 4, c->tune.pl_dbg);
+        }, true));
+        return mirror();
       }
       if (exact) {
         g.copies = 1;
@@ -968,7 +1007,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = k;
         g.rot = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, slot_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk));
+        choose_chunks(g, slot_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz));
+        o.tri = use_slots && tri_esz > 0 && g.nchunks > 1;
       }
       KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
       if (use_slots) {
@@ -986,7 +1026,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           o.dsq = c->dsq.as<double>();
         }
       }
-      return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+      KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         return exact ? launch_gram_spectrum(g, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                             r0, r1, oq, c->stream, c->tune.sp_store,
                                             c->tune.sp_order)
@@ -994,7 +1034,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                                    c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                                    r0, r1, (int)w[0], (int)w[1], (int)w[2], oq,
                                                    c->stream);
-      }, true);
+      }, true));
+      return mirror();
     }
     case KMG_WD:
     case KMG_WDS: {

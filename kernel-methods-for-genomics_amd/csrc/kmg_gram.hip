@@ -262,8 +262,9 @@ __global__ __launch_bounds__(1024) void gram_mm1_kernel(IndexGeom g, Packed pk,
   constexpr int G = 2, CH = 4;
   constexpr int NSUB = K + 3 * K * (K - 1) / 2;
   extern __shared__ __align__(16) uint32_t smem[];  // acc first: LDS offset 0 (col_addr_sdwa)
-  const int c = (int)(blockIdx.x / rows);
-  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  int c;
+  int64_t il;
+  rowacc_block(g, o, row0, rows, c, il);
   const int64_t i = row0 + il;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
@@ -467,8 +468,9 @@ __global__ __launch_bounds__(1024) void gram_mm2_kernel(PairGeom pg, IndexGeom g
   // one dynamic LDS block, accumulator first: col_addr_sdwa needs acc at LDS offset 0, so
   // this kernel declares no static __shared__ variable
   extern __shared__ __align__(16) uint32_t smem[];
-  const int c = (int)(blockIdx.x / rows);
-  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  int c;
+  int64_t il;
+  rowacc_block(g, o, row0, rows, c, il);
   const int64_t i = row0 + il;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
@@ -1105,16 +1107,82 @@ hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, in
   return hipGetLastError();
 }
 
+// In-place mirror of a full square K built with OutSpec::tri: K[i][j] = K[j][i] for every
+// j < (i / chunk) * chunk, the blocks left of row i's own column chunk that the mismatch
+// kernels skipped (rowacc_block).  Row j < (i / chunk) * chunk did compute column i (its
+// own chunk is left of i's), so every source entry exists.  64 x 64 tiles through LDS: the
+// source K[j0.., i0..] is read along its rows and the target K[i0.., j0..] written along
+// its rows, 16 bytes per lane each way.
+template <typename T>
+__global__ __launch_bounds__(256) void mirror_chunks_kernel(T *__restrict__ K, int64_t ld,
+                                                            int64_t n, int chunk) {
+  constexpr int V = 16 / (int)sizeof(T), CPR = 64 / V;
+  __shared__ T tile[64][64 + 1];  // [j - j0][i - i0]
+  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
+  const int64_t imax = min(n - 1, i0 + 63);
+  if (j0 >= (imax / chunk) * chunk) return;  // no target entry in this tile
+  for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
+    const int r = c / CPR, q = (c - r * CPR) * V;
+    const int64_t j = j0 + r, i = i0 + q;
+    if (j >= n) continue;
+    const T *src = K + j * ld + i;
+    if (i + V <= n && (((uintptr_t)src) & 15) == 0) {
+      const uint4 x = *(const uint4 *)src;
+      const T *v = (const T *)&x;
+#pragma unroll
+      for (int h = 0; h < V; ++h) tile[r][q + h] = v[h];
+    } else {
+      for (int h = 0; h < V && i + h < n; ++h) tile[r][q + h] = src[h];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
+    const int r = c / CPR, q = (c - r * CPR) * V;
+    const int64_t i = i0 + r, j = j0 + q;
+    if (i >= n) continue;
+    const int64_t cs = (i / chunk) * chunk;
+    if (j >= cs) continue;
+    T o[V];
+#pragma unroll
+    for (int h = 0; h < V; ++h) o[h] = tile[q + h][r];
+    T *dst = K + i * ld + j;
+    if (j + V <= cs && (((uintptr_t)dst) & 15) == 0) {
+      *(uint4 *)dst = *(const uint4 *)o;
+    } else {
+      for (int h = 0; h < V && j + h < cs; ++h) dst[h] = o[h];
+    }
+  }
+}
+
+hipError_t launch_mirror_chunks(void *K, int64_t ld, int64_t n, int chunk, int esz,
+                                hipStream_t s) {
+  if (n <= chunk) return hipSuccess;
+  const int64_t t = (n + 63) / 64;
+  if (t > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)t, (unsigned)t);
+  if (esz == 8)
+    hipLaunchKernelGGL(mirror_chunks_kernel<uint64_t>, grid, dim3(256), 0, s, (uint64_t *)K, ld, n,
+                       chunk);
+  else if (esz == 4)
+    hipLaunchKernelGGL(mirror_chunks_kernel<uint32_t>, grid, dim3(256), 0, s, (uint32_t *)K, ld, n,
+                       chunk);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store, int order) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
-  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (o.tri) return hipErrorInvalidValue;  // (the spectrum grid has its own row orders)
+  const int64_t nblk = rowacc_blocks(g, o, row0, rows);
+  if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   const bool pack = g.pmax <= 255;
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   const size_t lds = (size_t)words * 4;
-  const dim3 grid((unsigned)(rows * g.nchunks));
+  const dim3 grid((unsigned)nblk);
   // store policy: 0 auto (plain for a single-chunk int32 K, else non-temporal), 1 NT, 2 plain
   const bool nt = store == 1 || (store == 0 && !(o.dtype == KMG_I32 && g.nchunks == 1));
   const int64_t cmr = (order == 1 && g.nchunks > 1) ? rows : 0;
@@ -1148,11 +1216,12 @@ hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, con
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (g.k < 8 || g.k > 12 || !g.rot) return hipErrorNotSupported;
   if (w0 > 255 || w1 > 255 || w2 > 255) return hipErrorNotSupported;
-  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  const int64_t nblk = rowacc_blocks(g, o, row0, rows);
+  if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   const int nsub = g.k + 3 * g.k * (g.k - 1) / 2;
   const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + g.pmax * g.k + nsub + pk.ldp) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(rows * g.nchunks));
+  const dim3 grid((unsigned)nblk);
   switch (g.k) {
 #define KMG_MM(KK)                                                                               \
   case KK:                                                                                       \
@@ -1173,11 +1242,12 @@ hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, c
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
-  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  const int64_t nblk = rowacc_blocks(g, o, row0, rows);
+  if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   if (nlines * 128 >= 0xFFFFFFF0LL) return hipErrorInvalidValue;  // 32-bit buffer offsets
   const size_t lds = (size_t)((((g.chunk + 3) >> 2) << 2) + 64 + g.pmax + pk.ldp + KMG_PAIRS_MAX) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(rows * g.nchunks));
+  const dim3 grid((unsigned)nblk);
   const uint32_t lb = (uint32_t)(nlines * 128);
   switch (pg.k) {
 #define KMG_MM2(KK)                                                                               \

@@ -379,6 +379,7 @@ hipError_t launch_slot_pack(const IndexGeom &g, const uint32_t *off, const uint1
   const int64_t ngroups = g.nbins() >> 2;
   if (ngroups == 0) return hipSuccess;
   const int64_t threads = ngroups * 8;
+  if (threads >= (1LL << 32)) return hipErrorInvalidValue;  // grid x block < 2^32 work-items
   const uint32_t sent_base = (uint32_t)(((g.chunk + 3) >> 2) << 2);
   if (sent_base + 1024u > 0xFFFFu) return hipErrorInvalidValue;
   hipLaunchKernelGGL(slot_pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
@@ -505,6 +506,7 @@ hipError_t launch_pair_count(const PairGeom &pg, const uint32_t *xoff, uint32_t 
                              uint32_t *rtot, hipStream_t s) {
   const int64_t threads = pg.nrec() * 4;
   if (threads == 0) return hipSuccess;
+  if (threads >= (1LL << 32)) return hipErrorInvalidValue;  // grid x block < 2^32 work-items
   hipLaunchKernelGGL(pair_count_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                      pg, xoff, summary, rtot);
   return hipGetLastError();
@@ -515,6 +517,7 @@ hipError_t launch_pair_pack(const PairGeom &pg, const uint32_t *xoff, const uint
                             hipStream_t s) {
   const int64_t blocks = (pg.ngroups() + PAIR_PACK_GROUPS - 1) / PAIR_PACK_GROUPS;
   if (blocks == 0) return hipSuccess;
+  if (blocks * 256 >= (1LL << 32)) return hipErrorInvalidValue;  // < 2^32 work-items
   if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
   hipLaunchKernelGGL(pair_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent,
                      rbase, summary, lines);

@@ -192,6 +192,9 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
   int64_t col_lo = 0;   // columns < col_lo are not written (upper-triangle multi-GPU
                         // builds; kernels that honour it: spectrum, mismatch slots / pairs)
+  int tri = 0;          // full square K (rows [0, n)): the mismatch posting-list kernels
+                        // compute only the column chunks that reach column i of row i
+                        // (rowacc_block); the caller mirrors the rest (launch_mirror_chunks)
   uint32_t *ovf = nullptr;  // dtype KMG_U16 / KMG_U8: set to 1 when a count exceeds 65535
                             // / an off-diagonal count exceeds 255 (the stored value is then
                             // clipped and the caller redoes the build with wider slabs)
@@ -227,6 +230,8 @@ hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, in
 // the same from a uint16 slab of raw counts into K of dtype dt (int32 / float32 / float64),
 // normalize_K applied on the way when `normalize` and diagv[0] != 1 (the fused epilogue's
 // formula, bit for bit)
+hipError_t launch_mirror_chunks(void *K, int64_t ld, int64_t n, int chunk, int esz,
+                                hipStream_t s);
 hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
                                void *K, int64_t ld, int dt, int normalize, const double *diagv,
                                const double *dsq, hipStream_t s);

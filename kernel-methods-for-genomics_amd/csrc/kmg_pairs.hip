@@ -282,6 +282,7 @@ hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *s
                            uint32_t *rtot, hipStream_t s) {
   const int64_t threads = pg.nrec() * 32;
   if (threads == 0) return hipSuccess;
+  if (threads >= (1LL << 32)) return hipErrorInvalidValue;  // grid x block < 2^32 work-items
   hipLaunchKernelGGL(pl_count_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, pg,
                      xoff, summary, rtot);
   return hipGetLastError();
@@ -291,6 +292,9 @@ hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16
                           const uint32_t *rbase, uint32_t *summary, uint4 *lines, hipStream_t s) {
   const int64_t blocks = (pg.ngroups() + PL_PACK_GROUPS - 1) / PL_PACK_GROUPS;
   if (blocks == 0) return hipSuccess;
+  // grid x block < 2^32 work-items (k = 11 at 63 chunks of 8 columns is 14.5 G: the
+  // launch wrapped and packed a fraction of the table)
+  if (blocks * 256 >= (1LL << 32)) return hipErrorInvalidValue;
   if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
   hipLaunchKernelGGL(pl_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent, rbase,
                      summary, lines);
@@ -361,8 +365,9 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
   constexpr uint32_t NK2 = 1u << (2 * (K - 2));
   // one dynamic LDS block, accumulator first (col_addr_sdwa: acc at LDS offset 0)
   extern __shared__ __align__(16) uint32_t smem[];
-  const int c = (int)(blockIdx.x / rows);
-  const int64_t il = (int64_t)blockIdx.x - (int64_t)c * rows;
+  int c;
+  int64_t il;
+  rowacc_block(g, o, row0, rows, c, il);
   const int64_t i = row0 + il;
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
@@ -512,19 +517,24 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
     const bool wide = nl == PL_WIDE;
     const uint32_t cu = (valid && !corr && !wide && nl <= (uint32_t)PL_QU) ? nl : 0u;
     const uint32_t cn = pc_on ? pc_nl : 0u;
-    const uint32_t cnt = cu + cn;
+    // uniform lines first, then the correction lines, each run padded to whole steps of 8:
+    // a step then holds one kind only, and the uniform steps (3 of 4) never take the
+    // per-halfword weight path.  One scan: uniform counts in the low, correction counts in
+    // the high 16 bits.
+    const uint32_t cnt = cu | (cn << 16);
     uint32_t incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t v = (uint32_t)__shfl_up((int)incl, d, 64);
       if (lane >= d) incl += v;
     }
-    const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
-    const uint32_t Tp = (T + 7u) & ~7u;
-    uint32_t pos = tail + incl - cnt;
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+    const uint32_t TU = tot & 0xFFFFu, TC = tot >> 16;
+    const uint32_t TUp = (TU + 7u) & ~7u, TCp = (TC + 7u) & ~7u;
+    const uint32_t pos = tail + (incl & 0xFFFFu) - cu;
     for (uint32_t e = 0; e < cu; ++e) ring[(pos + e) & (PL_RING - 1)] = make_uint2(base + e, 0u);
-    pos += cu;
     if (pc_on) {
+      const uint32_t cpos = tail + TUp + (incl >> 16) - cn;
       const int uo = (int)((pc_meta >> 2) & 3u), ui = (int)((pc_meta >> 4) & 3u);
       const int rs = (int)hdr_start(pc_h, 4 * uo), re = (int)hdr_byte(pc_h, 4 * uo + 3);
       const int es = (int)hdr_start(pc_h, 4 * uo + ui), ee = (int)hdr_byte(pc_h, 4 * uo + ui);
@@ -534,11 +544,13 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
         const int sh = 8 - 64 * (int)s;
         const uint32_t y = clamp64(rs + sh) | (clamp64(re + sh) << 8) | (clamp64(es + sh) << 16) |
                            (clamp64(ee + sh) << 24);
-        ring[(pos + s) & (PL_RING - 1)] = make_uint2((pc_base + s) | fl | (s == 0 ? RE_HDR : 0u), y);
+        ring[(cpos + s) & (PL_RING - 1)] = make_uint2((pc_base + s) | fl | (s == 0 ? RE_HDR : 0u), y);
       }
     }
-    if ((uint32_t)lane < Tp - T) ring[(tail + T + lane) & (PL_RING - 1)] = make_uint2(RE_EMPTY, 0u);
-    tail += Tp;
+    if ((uint32_t)lane < TUp - TU) ring[(tail + TU + lane) & (PL_RING - 1)] = make_uint2(RE_EMPTY, 0u);
+    if ((uint32_t)lane < TCp - TC)
+      ring[(tail + TUp + TC + lane) & (PL_RING - 1)] = make_uint2(RE_EMPTY, 0u);
+    tail += TUp + TCp;
     // this batch's correction lists: headers now, lines at the next call
     pc_on = valid && corr && !wide && nl > 0 && nl <= (uint32_t)PL_QC;
     if (pc_on) {
@@ -648,25 +660,22 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
-  if (rows * g.nchunks > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  // ring depth 4 only: one batch enters at most 64 (PL_QU + PL_QC) + 14 = 462 ring entries
+  // on top of < 8 (depth + 1) unread ones, and the ring holds 512
+  (void)depth;
+  const int64_t nblk = rowacc_blocks(g, o, row0, rows);
+  if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   if (nlines * 128 >= 0xFFFFFFF0LL || nlines >= (1LL << 28)) return hipErrorInvalidValue;
   const size_t lds = (size_t)(((((((g.chunk + 3) >> 2) << 2) + 64 + g.pmax + pk.ldp + KMG_PAIRS_MAX + 1) & ~1) +
                                16 * KMG_PL_WAVE_WORDS)) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(rows * g.nchunks));
+  const dim3 grid((unsigned)nblk);
   const uint32_t lb = (uint32_t)(nlines * 128);
   switch (pg.k) {
 #define KMG_PL(KK)                                                                                 \
   case KK:                                                                                         \
-    if (depth >= 8)                                                                                \
-      hipLaunchKernelGGL((gram_pl_kernel<KK, 8>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
-    else if (depth >= 6)                                                                           \
-      hipLaunchKernelGGL((gram_pl_kernel<KK, 6>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
-    else                                                                                           \
-      hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(1024), lds, s, pg, g, pk, summary,    \
-                         lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                        \
+    hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(1024), lds, s, pg, g, pk, summary, lines, \
+                       lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                               \
     break;
     KMG_PL(3) KMG_PL(4) KMG_PL(5) KMG_PL(6) KMG_PL(7) KMG_PL(8) KMG_PL(9) KMG_PL(10) KMG_PL(11)
     KMG_PL(12)

@@ -6,6 +6,39 @@
 
 namespace kmg {
 
+// Workgroup -> (column chunk c, local row il) of the row-accumulator grids, chunk-major.
+// With o.tri (a full square K) chunk c keeps only the rows i < col0(c) + cw(c), the blocks
+// that reach the diagonal or lie right of it: K is symmetric, and the blocks left of row
+// i's own chunk are mirrored afterwards (launch_mirror_chunks), so a row reads the posting
+// lines of (nch + 1) / 2 chunks on average instead of nch.  rowacc_blocks() is the grid size.
+__host__ __device__ __forceinline__ int64_t tri_rows(int64_t n, int chunk, int c, int64_t row0,
+                                                    int64_t rows) {
+  const int64_t end = min(n, (int64_t)(c + 1) * chunk) - row0;
+  return end < 0 ? 0 : (end < rows ? end : rows);
+}
+__host__ __device__ __forceinline__ int64_t rowacc_blocks(const IndexGeom &g, const OutSpec &o,
+                                                         int64_t row0, int64_t rows) {
+  if (!o.tri) return rows * g.nchunks;
+  int64_t t = 0;
+  for (int c = 0; c < g.nchunks; ++c) t += tri_rows(g.n, g.chunk, c, row0, rows);
+  return t;
+}
+__device__ __forceinline__ void rowacc_block(const IndexGeom &g, const OutSpec &o, int64_t row0,
+                                             int64_t rows, int &c, int64_t &il) {
+  int64_t b = (int64_t)blockIdx.x;
+  if (!o.tri) {
+    c = (int)(b / rows);
+    il = b - (int64_t)c * rows;
+    return;
+  }
+  for (c = 0; c < g.nchunks - 1; ++c) {
+    const int64_t rc = tri_rows(g.n, g.chunk, c, row0, rows);
+    if (b < rc) break;
+    b -= rc;
+  }
+  il = b;
+}
+
 // copy the packed record of sequence i into LDS (every thread of the block takes part)
 __device__ __forceinline__ void stage_record(const Packed &pk, int64_t i, uint32_t *srec) {
   const uint32_t *rec = pk.w + i * pk.ldp;

@@ -99,6 +99,54 @@ def assemble_upper_triangle(slabs, n, world, block, dtype):
     return K
 
 
+XGMI_LINK_GBPS = 76.5  # one xGMI link, one direction (MI355X: 7 links per GPU, point to point)
+
+
+def scaling_projection(n, t1_ms, t_index_ms, t_gram_ms, fill_gbps, out_bytes, wire_bytes,
+                       chunk=None, worlds=(2, 4, 8), link_gbps=XGMI_LINK_GBPS, link_eff=1.0):
+    """Predicted G-GPU times of one full-K build from one-GPU measurements.
+
+    Two builds are modelled:
+    * ``every_gpu`` (K complete on every GPU; kmg_gram_blocks gather = 2):
+      compute = index + the rank's share of the upper-triangle Gram work (whole column
+      chunks at or right of each round's first row, ``chunk`` columns per chunk);
+      receive = the round slabs' (G-1)/G share over the G-1 point-to-point links into
+      each GPU (fully connected xGMI: S / (G * link)); unpack = every GPU writes the
+      whole K (n^2 * out_bytes) and reads the slabs at the measured fill rate.  The three
+      run on separate streams, so t = max(stages) + one round of the largest stage
+      (pipeline fill).
+    * ``collective_free``: every GPU builds the index and its own rows only (the sharded
+      reference loop, kernels.py:41-45 / 211-215, without the assembly): index + gram / G.
+
+    Returns {G: {...}} with times in ms and speedups against t1_ms (the measured one-GPU
+    build).  Assumptions are in the arguments: link_gbps per link and direction, link_eff
+    the fraction of it an all-gather reaches (1.0: upper bound, not measured)."""
+    chunk = chunk or n
+    out = {}
+    nn = float(n) * n
+    for g in worlds:
+        block = default_block(n, g, n * out_bytes)
+        rounds = triangle_rounds(n, g, block)
+        r = g * block
+        work = slab = 0.0
+        for c0, w in rounds:
+            rows = min(r, n - c0)
+            work += rows * (n - (c0 // chunk) * chunk)
+            slab += r * w
+        compute = t_index_ms + t_gram_ms * (work / nn) / g
+        recv = slab * wire_bytes / (g * link_gbps * link_eff * 1e9) * 1e3
+        unpack = (nn * out_bytes + slab * wire_bytes) / (fill_gbps * 1e9) * 1e3
+        stages = {"compute_ms": compute, "receive_ms": recv, "unpack_ms": unpack}
+        t_every = max(stages.values()) + max(stages.values()) / max(1, len(rounds))
+        t_cf = t_index_ms + t_gram_ms / g
+        out[g] = {"block_rows": block, "rounds": len(rounds), **stages,
+                  "bytes_received_per_gpu": slab * wire_bytes * (g - 1) / g,
+                  "bound": max(stages, key=stages.get).replace("_ms", ""),
+                  "every_gpu_ms": t_every, "every_gpu_speedup": t1_ms / t_every,
+                  "collective_free_ms": t_cf, "collective_free_speedup": t1_ms / t_cf}
+    return out
+
+
 def u8_slab_escapes(counts, row0, col0):
     """Restatement of the uint8 round-slab form the Gram kernels write (kmg_rowacc.h
     emit_row, KMG_U8, with an escape list): `counts` holds rows row0.. at columns col0..;

@@ -1,0 +1,39 @@
+"""kmgram.shard.scaling_projection: the G-GPU model bench.py emits at N=1."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "kernel-methods-for-genomics_amd"))
+
+from kmgram.shard import default_block, scaling_projection, triangle_rounds  # noqa: E402
+
+
+def test_projection_bytes_and_bounds():
+    n = 100000
+    p = scaling_projection(n, 6.5, 0.15, 6.35, 6100.0, 4, 1, chunk=20000)
+    for g, v in p.items():
+        b = default_block(n, g, n * 4)
+        assert v["block_rows"] == b
+        slab = sum(g * b * w for _, w in triangle_rounds(n, g, b))
+        assert abs(v["bytes_received_per_gpu"] - slab * (g - 1) / g) < 1
+        # the slabs cover the upper triangle at least once
+        assert slab >= n * (n + 1) / 2
+        # receive: the (G-1)/G share over G-1 links of 76.5 GB/s
+        assert abs(v["receive_ms"] - slab / (g * 76.5e9) * 1e3) < 1e-9
+        # every GPU writes the whole int32 K: never below n^2 * 4 / fill
+        assert v["unpack_ms"] >= n * n * 4 / 6100e9 * 1e3
+        assert v["every_gpu_ms"] >= max(v["compute_ms"], v["receive_ms"], v["unpack_ms"])
+        assert v["collective_free_ms"] == 0.15 + 6.35 / g
+    # config 4 with K on every GPU cannot beat the single-GPU build
+    assert all(v["every_gpu_speedup"] < 1.0 for v in p.values())
+    assert p[8]["collective_free_speedup"] > p[4]["collective_free_speedup"] > p[2]["collective_free_speedup"]
+
+
+def test_projection_chunk_granularity():
+    """Whole column chunks left of a round's first row are skipped, so the Gram share lies
+    between the exact upper triangle and the full rows."""
+    n = 200000
+    fine = scaling_projection(n, 277.7, 2.8, 274.9, 6100.0, 4, 1, chunk=1, worlds=(8,))[8]
+    coarse = scaling_projection(n, 277.7, 2.8, 274.9, 6100.0, 4, 1, chunk=n, worlds=(8,))[8]
+    mid = scaling_projection(n, 277.7, 2.8, 274.9, 6100.0, 4, 1, chunk=28572, worlds=(8,))[8]
+    assert fine["compute_ms"] < mid["compute_ms"] < coarse["compute_ms"]
+    assert abs(coarse["compute_ms"] - (2.8 + 274.9 / 8)) < 1e-6
