@@ -732,17 +732,20 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 // Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
 // kmg_gram_blocks' choice of the round-slab format).
 enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL };
-SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax) {
+SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
   const bool exact = !mm || p->m == 0;  // spectrum-shaped: only ham 0 counts
-  // mismatch m = 1: drop-two pair table (auto for k = 10, 11: fewest posting lines per
-  // row) or the drop-one slot table (auto for k = 8, 9 and 12).  At k = 9 the pair kernel
-  // fetches 24% fewer bytes but issues 2x the VALU/SALU work and loses (6.3 vs 4.45 ms,
-  // profiles/r02_mm_pmc.txt); at k = 12 the 66 x 4^10 pair groups cost more to build.
+  // mismatch m = 1, auto (N=20000 normalised float64 builds, profiles/r03g_mm_forms.jsonl):
+  //   k = 9 up to one pair-lines chunk (n <= 24000): the pair-lines table (3.93 ms against
+  //     the slot table's 4.17: 0.64x the lines, uniform groups); larger n (config 5,
+  //     7 chunks): the slot table (one-GPU raw K 184.6 vs 210.9 ms, both upper-triangle);
+  //   k = 10, 11: the drop-two pair table (k = 10: 4.74 vs 5.98 ms slots);
+  //   k = 8 and 12: the drop-one slot table (k = 8: 6.70 vs 7.78 pair lines, 15.8 pairs).
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
-  const bool use_pl = s1 && form == 3 && k >= 3 && k <= 12;
+  const bool use_pl =
+      s1 && k >= 3 && k <= 12 && (form == 3 || (form == 0 && k == 9 && n <= 24000));
   const bool use_pairs =
       s1 && !use_pl && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
   const bool use_slots = s1 && !use_pairs && !use_pl && k >= 8 && k <= 12 && form != 2;
@@ -818,7 +821,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
-      const SmPath path = sm_path(c->tune, p, g.pmax);
+      const SmPath path = sm_path(c->tune, p, g.pmax, n);
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS, use_pl = path == SM_PL;
       const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl;
       // a full square K (one range over [0, n), every column written) of a mismatch
@@ -1088,7 +1091,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     case KMG_SUBSTRING: {
       if (p->k < 0) return fail(KMG_EINVAL, "k < 0");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "SS produces float64 values");
-      if (p->k > 16) return fail(KMG_EUNSUPPORTED, "SS k > 16");
+      // k <= 33 at sequence lengths <= 127 (grouped sweep), k <= 16 at any length (strips)
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
       // one range covering the whole matrix: upper triangle + mirror (kernels.py:378-381)
       const int mirror = (ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n) ? 1 : 0;
@@ -1101,7 +1104,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         }
         return e;
       });
-      if (unsupported) return fail(KMG_EUNSUPPORTED, "SS parameters");
+      if (unsupported)
+        return fail(KMG_EUNSUPPORTED, "SS: k = %d with sequences of length %d (k <= 33 up to "
+                    "length 127, k <= 16 beyond)", p->k, maxlen);
       return r;
     }
     case KMG_LOCALALIGN: {
@@ -1110,7 +1115,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // the recurrence the reference means (kernels.py:226-270 with its aliasing, loop
         // bounds and gap signs fixed; gram_la_kernel): parity unpinned
         if (!(p->la_beta > 0.0)) return fail(KMG_EINVAL, "LA: beta must be > 0");
-        if (maxlen > 1024) return fail(KMG_EUNSUPPORTED, "LA: sequences longer than 1024");
+        // (no length check here: the launch picks the grouped sweep up to length 127, the
+        // strip kernel with 4..1 pairs a block up to ~5100, and reports longer as unsupported)
         {  // the substitution matrix S covers A, C, G, T only (kernels.py:223)
           uint32_t mc = 0, ml = 0;
           KMG_TRY(row_stats(c, d_codes, d_lens, n, ldc, mc, ml));
@@ -1134,7 +1140,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           }
           return hipSuccess;
         });
-        if (unsupported) return fail(KMG_EUNSUPPORTED, "LA parameters");
+        if (unsupported)
+          return fail(KMG_EUNSUPPORTED, "LA: sequences of length %d (the boundary rows of a "
+                      "64-row strip must fit the 160 KB LDS: length <= ~5100)", maxlen);
         return r;
       }
       if (p->la_mode != KMG_LA_REFERENCE) return fail(KMG_EINVAL, "LA: unknown la_mode");
@@ -1463,7 +1471,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     const bool mm = p->kind == KMG_MISMATCH;
     const int L = mm ? (p->window > 0 ? p->window : 101) : (int)ldc;  // gram_device's maxlen
     const int pmax = std::max(1, L - p->k + 1);
-    const SmPath path = sm_path(c->tune, p, pmax);
+    const SmPath path = sm_path(c->tune, p, pmax, n);
     // 8-bit slabs for every posting-list path: an off-diagonal count >= 255 (a pair sharing
     // a long k-mer; ~1e-4 of random 101-mer pairs for MM(9,1)) travels in an escape list
     // that is all-gathered after the slabs and patched into K; a full list redoes the

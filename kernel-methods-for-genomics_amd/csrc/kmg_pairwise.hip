@@ -10,6 +10,7 @@
 // plus the dense host-matrix helpers normalize_K (kernels.py:398-415) and
 // center_K (kernels.py:387-395).
 #include "kmg_internal.h"
+#include <type_traits>
 
 #include <cmath>
 
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, i
   extern __shared__ __align__(16) double ssm[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t i = row0 + blockIdx.y;
-  const int64_t j = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (j >= q.n || i >= row1) return;
   if (mirror && j < i) return;
   const int ML = q.maxlen;
@@ -580,6 +581,142 @@ __global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, i
   }
 }
 
+// ------------------------------------------------------------------ SS, grouped sweep
+// The same recurrences, 64 / LPP pairs a wave: lane s of a pair's LPP-lane group owns the
+// DP rows r = s R .. s R + R - 1 (r = 0..n_x, row 0 the zero boundary) and at step st
+// computes column c = st - s of each of its rows in row order.  Row r - 1 at column c is
+// the row above in the same lane, or for the lane's first row lane s - 1's last row,
+// published at step st - 1 and moved by DPP wave_shr:1 (across a group boundary it lands
+// on a lane whose first row is row 0, which never reads it); the diagonal is the row
+// above's previous value.  The strip kernel above ran one pair a wave in 64-row strips:
+// at L = 101 two strips of ny + 64 steps each with 38 of 64 lanes live in the second, and
+// KMAX - 1 >= kk - 1 levels; here ML + LPP steps of R rows and exactly NL levels per
+// lane, so every lane stays busy.  Per cell the operation order is the strip kernel's
+// (bit-identical), S_{r+1} accumulates in column order, K sums S_i in row order.
+template <int LPP, int R, int NL>
+__global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, int64_t row1,
+                                                       int kk, double lam, double lam2,
+                                                       int mirror, OutSpec o) {
+  constexpr int G = 64 / LPP;
+  extern __shared__ __align__(16) double gsm[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane / LPP, s = lane % LPP;
+  const int64_t i = row0 + blockIdx.y;
+  const int64_t jb = (mirror ? i : 0) + ((int64_t)blockIdx.x * 4 + wave) * G;
+  if (i >= row1 || jb >= q.n) return;  // wave-uniform
+  const int ML = q.maxlen;
+  const int SW = ML + 2;  // S slots per group
+  double *Ssh = gsm + (size_t)(wave * G + g) * SW;
+  uint8_t *ysh = (uint8_t *)(gsm + (size_t)4 * G * SW) + (size_t)(wave * G + g) * (ML + 1);
+  const int64_t j = jb + g;
+  const bool pv = j < q.n;
+  const int64_t ia = pv ? min(i, j) : i, ib = pv ? max(i, j) : i;
+  const uint8_t *xs = q.codes + ia * q.ldc;
+  const uint8_t *ys = q.codes + ib * q.ldc;
+  const int nx = pv ? q.lens[ia] : -1, ny = pv ? q.lens[ib] : -1;
+  // a pair takes part in the sweep unless its value is a constant (kernels.py:354-358)
+  const bool dp = pv && kk >= 1 && nx >= kk && ny >= kk;
+  for (int c = s; c < ny; c += LPP) ysh[c] = ys[c];
+  // x_{r-1} and x_r of the lane's rows, packed 4 a word (0x1FF-like sentinel 0xFF:
+  // never equal to a code of y, which the match tests compare as bytes)
+  uint32_t xw[(R + 4) / 4];
+#pragma unroll
+  for (int w = 0; w < (R + 4) / 4; ++w) xw[w] = 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k <= R; ++k) {  // xw byte k = x_{r0 + k - 1}
+    const int rr = s * R + k - 1;
+    const uint32_t v = (dp && rr >= 0 && rr < nx) ? (uint32_t)xs[rr] : 0xFFu;
+    xw[k >> 2] = (xw[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | (v << (8 * (k & 3)));
+  }
+  __builtin_amdgcn_wave_barrier();
+  double last[R][NL], sacc[R], pub[NL], pup[NL];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    sacc[k] = 0.0;
+#pragma unroll
+    for (int t = 0; t < NL; ++t) last[k][t] = 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < NL; ++t) {
+    pub[t] = 0.0;
+    pup[t] = 0.0;
+  }
+  const int r0 = s * R;
+  const int steps = ML + LPP;
+  for (int st = 0; st < steps; ++st) {
+    const int c = st - s;
+    double up[NL];
+#pragma unroll
+    for (int t = 0; t < NL; ++t) up[t] = wave_shr1(pub[t]);
+    if (dp && c >= 0 && c <= ny) {
+      const uint32_t yprev = c >= 1 ? (uint32_t)ysh[c - 1] : 0x1FFu;
+      const uint32_t ycur = c < ny ? (uint32_t)ysh[c] : 0x1FFu;
+      double above[NL], adiag[NL];
+#pragma unroll
+      for (int t = 0; t < NL; ++t) {
+        above[t] = up[t];
+        adiag[t] = pup[t];
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int r = r0 + k;
+        // rows past n_x compute don't-care values: they feed only rows below them (also
+        // past n_x) and the next lane's rows (past n_x as well), never S or K; every level
+        // is evaluated and selected, no per-lane branches
+        {
+          const uint32_t xprev = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          const uint32_t xcur = (xw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+          const bool match = r >= 1 && c >= 1 && xprev == yprev;
+          const int rc = min(r, c);  // level lvl is live where lvl <= min(r, c)
+          double cur[NL];
+#pragma unroll
+          for (int t = 0; t < NL; ++t) {
+            const int lvl = t + 1;
+            double v = __dadd_rn(__dmul_rn(lam, above[t]), __dmul_rn(lam, last[k][t]));
+            v = __dsub_rn(v, __dmul_rn(lam2, adiag[t]));
+            const double prevlvl = (t == 0) ? 1.0 : adiag[t - 1];
+            const double vm = __dadd_rn(v, __dmul_rn(lam2, prevlvl));
+            v = match ? vm : v;
+            cur[t] = (lvl < kk && lvl <= rc) ? v : 0.0;
+          }
+          if (c < ny && r < nx && ycur == xcur) {
+            double bkm1 = 1.0;  // B_0 == 1
+#pragma unroll
+            for (int t = 0; t < NL; ++t)
+              if (t == kk - 2) bkm1 = cur[t];
+            sacc[k] = __dadd_rn(sacc[k], bkm1);
+          }
+#pragma unroll
+          for (int t = 0; t < NL; ++t) {
+            adiag[t] = last[k][t];
+            above[t] = cur[t];
+            last[k][t] = cur[t];
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NL; ++t) {
+        pup[t] = up[t];
+        pub[t] = last[R - 1][t];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    if (dp && r0 + k < nx) Ssh[r0 + k + 1] = sacc[k];
+  __builtin_amdgcn_wave_barrier();
+  if (s == 0 && pv) {
+    double K = 0.0;
+    if (kk == 0) {
+      K = 1.0;  // K_k(.., 0, ..) returns 1 (kernels.py:354-355)
+    } else if (dp) {
+      for (int ii = kk; ii <= nx; ++ii) K = __dadd_rn(K, __dmul_rn(lam2, Ssh[ii]));
+    }
+    store_f(o, i - row0, j, K);
+    if (mirror && j != i && j >= row0 && j < row1) store_f(o, j - row0, i, K);
+  }
+}
+
 // ------------------------------------------------------------------ LA (intended)
 // Local-alignment kernel with the reference's three defects removed (KMG_LA_INTENDED;
 // oracle cpu_ref.la_intended_pair documents the semantics; parity unpinned): five DP
@@ -604,7 +741,7 @@ __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, i
   extern __shared__ __align__(16) double lsm[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t i = row0 + blockIdx.y;
-  const int64_t j = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (j >= q.n || i >= row1) return;
   if (mirror && j < i) return;
   const int ML = q.maxlen;
@@ -681,13 +818,133 @@ __global__ __launch_bounds__(256) void gram_la_kernel(SeqSpec q, int64_t row0, i
   }
 }
 
+// LA, grouped sweep (the SS layout above): 64 / LPP pairs a wave, lane s of a group owns
+// the DP rows s R .. s R + R - 1; up (M, X, Y, X2 of row r - 1 at column c) comes from the
+// row above in the lane or, for its first row, from lane s - 1's last row of the previous
+// step (DPP wave_shr:1); the diagonal is the previous up.  Per cell the strip kernel's
+// operation order (bit-identical).
+template <int LPP, int R, bool SMITH>
+__global__ __launch_bounds__(256) void gram_lag_kernel(SeqSpec q, int64_t row0, int64_t row1,
+                                                       LaCoef cf, int mirror, OutSpec o) {
+  constexpr int G = 64 / LPP;
+  extern __shared__ __align__(16) double gsm[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane / LPP, s = lane % LPP;
+  const int64_t i = row0 + blockIdx.y;
+  const int64_t jb = (mirror ? i : 0) + ((int64_t)blockIdx.x * 4 + wave) * G;
+  const bool wlive = i < row1 && jb < q.n;  // wave-uniform (the block syncs once below)
+  const int ML = q.maxlen;
+  double *res = gsm + (wave * G + g);
+  uint8_t *ysh = (uint8_t *)(gsm + 4 * G) + (size_t)(wave * G + g) * (ML + 1);
+  const int64_t j = jb + g;
+  const bool pv = wlive && j < q.n;
+  const int64_t ia = pv ? min(i, j) : 0, ib = pv ? max(i, j) : 0;
+  const uint8_t *xs = q.codes + ia * q.ldc;
+  const uint8_t *ys = q.codes + ib * q.ldc;
+  const int nx = pv ? q.lens[ia] : -1, ny = pv ? q.lens[ib] : -1;
+  for (int c = s; c < ny; c += LPP) ysh[c] = ys[c];
+  if (s == 0) *res = 1.0;  // n_x or n_y == 0: cell [n_x, n_y] is the zero boundary
+  // the substitution factors in LDS (a dynamically indexed kernel-argument array would be
+  // materialised in VGPRs with a select chain per read)
+  double *es = gsm + 4 * G + (4 * G * (ML + 1) + 7) / 8;
+  if (threadIdx.x < 16) es[threadIdx.x] = cf.es[threadIdx.x];
+  __syncthreads();
+  uint32_t xw[(R + 3) / 4];  // byte k: x_{r0 + k - 1} & 3 (ACGT, host-checked)
+#pragma unroll
+  for (int w = 0; w < (R + 3) / 4; ++w) xw[w] = 0u;
+  const int r0 = s * R;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int rr = r0 + k - 1;
+    const uint32_t v = (pv && rr >= 0 && rr < nx) ? (uint32_t)xs[rr] & 3u : 0u;
+    xw[k >> 2] |= v << (8 * (k & 3));
+  }
+  if (!wlive) return;
+  __builtin_amdgcn_wave_barrier();
+  const double eo = cf.eo, ee = cf.ee;
+  double lM[R], lX[R], lY[R], lX2[R], lY2[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) lM[k] = lX[k] = lY[k] = lX2[k] = lY2[k] = 0.0;
+  double pM = 0.0, pX = 0.0, pY = 0.0, pX2 = 0.0;  // published: last row at this column
+  double qM = 0.0, qX = 0.0, qY = 0.0;             // previous up (first row's diagonal)
+  const int steps = ML + LPP;
+  for (int st = 0; st < steps; ++st) {
+    const int c = st - s;
+    const double uM0 = wave_shr1(pM), uX0 = wave_shr1(pX), uY0 = wave_shr1(pY),
+                 uX20 = wave_shr1(pX2);
+    if (pv && c >= 0 && c <= ny) {
+      const uint32_t yc = c >= 1 ? (uint32_t)ysh[c - 1] & 3u : 0u;
+      double uM = uM0, uX = uX0, uY = uY0, uX2 = uX20;  // row above at column c
+      double dM = qM, dX = qX, dY = qY;                  // row above at column c - 1
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int r = r0 + k;
+        {  // rows past n_x: don't-care values (only rows below them read them), no branch
+          double M, X, Y, X2, Y2;
+          {
+            const uint32_t xr = (xw[k >> 2] >> (8 * (k & 3))) & 3u;
+            const double sub = es[xr * 4 + yc];
+            if (SMITH) {
+              M = __dmul_rn(sub, fmax(fmax(fmax(1.0, dX), dY), dM));
+              X = fmax(__dmul_rn(eo, uM), __dmul_rn(ee, uX));
+              Y = fmax(fmax(__dmul_rn(eo, lM[k]), __dmul_rn(eo, lX[k])), __dmul_rn(ee, lY[k]));
+              X2 = fmax(uM, uX2);
+              Y2 = fmax(fmax(lM[k], lX2[k]), lY2[k]);
+            } else {
+              M = __dmul_rn(sub, __dadd_rn(__dadd_rn(__dadd_rn(1.0, dX), dY), dM));
+              X = __dadd_rn(__dmul_rn(eo, uM), __dmul_rn(ee, uX));
+              Y = __dadd_rn(__dmul_rn(eo, __dadd_rn(lM[k], lX[k])), __dmul_rn(ee, lY[k]));
+              X2 = __dadd_rn(uM, uX2);
+              Y2 = __dadd_rn(__dadd_rn(lM[k], lX2[k]), lY2[k]);
+            }
+            const bool in = r >= 1 && c >= 1;  // row 0 / column 0: the zero boundary
+            M = in ? M : 0.0;
+            X = in ? X : 0.0;
+            Y = in ? Y : 0.0;
+            X2 = in ? X2 : 0.0;
+            Y2 = in ? Y2 : 0.0;
+          }
+          if (r == nx && c == ny && r >= 1 && c >= 1)
+            *res = SMITH ? fmax(fmax(fmax(1.0, X2), Y2), M)
+                         : __dadd_rn(__dadd_rn(__dadd_rn(1.0, X2), Y2), M);
+          // this row at c - 1 is the next row's diagonal, this row at c its up
+          dM = lM[k];
+          dX = lX[k];
+          dY = lY[k];
+          uM = M;
+          uX = X;
+          uY = Y;
+          uX2 = X2;
+          lM[k] = M;
+          lX[k] = X;
+          lY[k] = Y;
+          lX2[k] = X2;
+          lY2[k] = Y2;
+        }
+      }
+      qM = uM0;
+      qX = uX0;
+      qY = uY0;
+      pM = lM[R - 1];
+      pX = lX[R - 1];
+      pY = lY[R - 1];
+      pX2 = lX2[R - 1];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (s == 0 && pv) {
+    const double result = __dmul_rn(cf.inv_beta, log(*res));
+    store_f(o, i - row0, j, result);
+    if (mirror && j != i && j >= row0 && j < row1) store_f(o, j - row0, i, result);
+  }
+}
+
 hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
                           double beta, int smith, int mirror, const OutSpec &o, hipStream_t s) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   const int ML = q.maxlen;
-  const size_t lds = (size_t)4 * (4 * (ML + 1) + 1 + (ML + 8) / 8) * sizeof(double);
-  if (lds > 160 * 1024 || rows > 65535) return hipErrorNotSupported;
+  if (rows > 65535) return hipErrorNotSupported;
   static const int S[4][4] = {{4, 0, 0, 0}, {0, 9, -3, -1}, {0, -3, 6, 2}, {0, -1, -2, 5}};
   LaCoef cf;
   for (int a = 0; a < 4; ++a)
@@ -695,11 +952,36 @@ hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e
   cf.eo = std::exp(-beta * e);
   cf.ee = std::exp(-beta * d);
   cf.inv_beta = 1.0 / beta;
-  const dim3 grid((unsigned)((q.n + 3) / 4), (unsigned)rows);
+  // grouped sweep while a group's rows cover the sequences (LPP x R >= ML + 1)
+  auto grouped = [&](auto lpp_c, auto r_c) -> hipError_t {
+    constexpr int LPP = decltype(lpp_c)::value, R = decltype(r_c)::value, G = 64 / LPP;
+    const size_t lds = (size_t)4 * G * sizeof(double) + ((4 * G * (ML + 1) + 7) / 8) * 8 + 16 * 8;
+    const int64_t cols = mirror ? q.n - row0 : q.n;  // mirror: columns from row i on
+    const dim3 grid((unsigned)((cols + 4 * G - 1) / (4 * G)), (unsigned)rows);
+    if (smith)
+      hipLaunchKernelGGL((gram_lag_kernel<LPP, R, true>), grid, dim3(256), (lds + 15) & ~(size_t)15,
+                         s, q, row0, row1, cf, mirror, o);
+    else
+      hipLaunchKernelGGL((gram_lag_kernel<LPP, R, false>), grid, dim3(256), (lds + 15) & ~(size_t)15,
+                         s, q, row0, row1, cf, mirror, o);
+    return hipGetLastError();
+  };
+  if (ML + 1 <= 8 * 13)
+    return grouped(std::integral_constant<int, 8>{}, std::integral_constant<int, 13>{});
+  if (ML + 1 <= 16 * 8)
+    return grouped(std::integral_constant<int, 16>{}, std::integral_constant<int, 8>{});
+  // longer sequences: the 64-row strip kernel, as many waves a block as the boundary rows'
+  // LDS allows (4 up to length ~1250, 1 up to ~5100)
+  const size_t per_wave = (size_t)(4 * (ML + 1) + 1 + (ML + 8) / 8) * sizeof(double);
+  const int W = (int)std::min<size_t>(4, (160 * 1024) / per_wave);
+  if (W < 1) return hipErrorNotSupported;
+  const dim3 grid((unsigned)((q.n + W - 1) / W), (unsigned)rows);
   if (smith)
-    hipLaunchKernelGGL((gram_la_kernel<true>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
+    hipLaunchKernelGGL((gram_la_kernel<true>), grid, dim3(64 * W), per_wave * W, s, q, row0, row1, cf,
+                       mirror, o);
   else
-    hipLaunchKernelGGL((gram_la_kernel<false>), grid, dim3(256), lds, s, q, row0, row1, cf, mirror, o);
+    hipLaunchKernelGGL((gram_la_kernel<false>), grid, dim3(64 * W), per_wave * W, s, q, row0, row1, cf,
+                       mirror, o);
   return hipGetLastError();
 }
 
@@ -914,13 +1196,52 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   const int ML = q.maxlen;
-  const dim3 grid((unsigned)((q.n + 3) / 4), (unsigned)rows);
-  auto lds_for = [&](int KM) {
-    const int per = (KM - 1) * (ML + 1) + (ML + 2) + (ML + 4 + 7) / 8;
-    return (size_t)per * 8 * 4;
+  if (rows > 65535) return hipErrorInvalidValue;
+  // grouped sweep whenever the rows fit one group (LPP x R >= ML + 1) and kk - 1 <= 32
+  // levels: NL levels exactly for kk <= 9, rounded up to 12 / 16 / 24 / 32 above
+  const int nl = kk >= 2 ? kk - 1 : 1;
+  auto grouped = [&](auto lpp_c, auto r_c, auto nl_c) -> hipError_t {
+    constexpr int LPP = decltype(lpp_c)::value, R = decltype(r_c)::value, NL = decltype(nl_c)::value;
+    constexpr int G = 64 / LPP;
+    const size_t lds = (size_t)4 * G * ((ML + 2) * sizeof(double) + (ML + 1));
+    const int64_t cols = mirror ? q.n - row0 : q.n;  // mirror: columns from row i on
+    const dim3 grid((unsigned)((cols + 4 * G - 1) / (4 * G)), (unsigned)rows);
+    hipLaunchKernelGGL((gram_ssg_kernel<LPP, R, NL>), grid, dim3(256), (lds + 15) & ~(size_t)15, s,
+                       q, row0, row1, kk, lam, lam2, mirror, o);
+    return hipGetLastError();
   };
+#define KMG_SSG(LPP_, R_, NL_) \
+  grouped(std::integral_constant<int, LPP_>{}, std::integral_constant<int, R_>{}, \
+          std::integral_constant<int, NL_>{})
+  if (nl <= 4 && ML + 1 <= 8 * 13) {
+    switch (nl) {
+      case 1: return KMG_SSG(8, 13, 1);
+      case 2: return KMG_SSG(8, 13, 2);
+      case 3: return KMG_SSG(8, 13, 3);
+      default: return KMG_SSG(8, 13, 4);
+    }
+  }
+  if (nl <= 8 && ML + 1 <= 16 * 7) {
+    switch (nl) {
+      case 5: return KMG_SSG(16, 7, 5);
+      case 6: return KMG_SSG(16, 7, 6);
+      case 7: return KMG_SSG(16, 7, 7);
+      default: return KMG_SSG(16, 7, 8);
+    }
+  }
+  if (nl <= 16 && ML + 1 <= 32 * 4) return nl <= 12 ? KMG_SSG(32, 4, 12) : KMG_SSG(32, 4, 16);
+  if (nl <= 32 && ML + 1 <= 64 * 2) return nl <= 24 ? KMG_SSG(64, 2, 24) : KMG_SSG(64, 2, 32);
+#undef KMG_SSG
+  // longer sequences: the strip kernel (64-row strips, the boundary row in LDS), as many
+  // waves (pairs) a block as their LDS allows (4 up to length ~300 at k = 16, 1 to ~1200)
+  const int kmx = kk <= 2 ? 2 : kk <= 4 ? 4 : kk <= 8 ? 8 : 16;
+  const size_t per_wave = (size_t)((kmx - 1) * (ML + 1) + (ML + 2) + (ML + 4 + 7) / 8) * 8;
+  const int W = (int)std::min<size_t>(4, (160 * 1024) / per_wave);
+  if (W < 1) return hipErrorNotSupported;
+  const dim3 grid((unsigned)((q.n + W - 1) / W), (unsigned)rows);
+  auto lds_for = [&](int) { return per_wave * W; };
 #define KMG_SS(KM_)                                                                          \
-  hipLaunchKernelGGL((gram_ss_kernel<KM_>), grid, dim3(256), lds_for(KM_), s, q, row0, row1, kk, \
+  hipLaunchKernelGGL((gram_ss_kernel<KM_>), grid, dim3(64 * W), lds_for(KM_), s, q, row0, row1, kk, \
                      lam, lam2, mirror, o)
   if (kk <= 2) KMG_SS(2);
   else if (kk <= 4) KMG_SS(4);

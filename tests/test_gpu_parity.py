@@ -327,20 +327,42 @@ def test_wds_xtr0(ctx, d, S):
     assert np.array_equal(K, cref.wds(codes, lens, d, S))
 
 
-@pytest.mark.parametrize("lb,k", [(0.5, 3), (1.0, 3), (0.7, 5), (0.3, 2), (0.5, 1), (0.9, 8), (0.6, 11)])
+@pytest.mark.parametrize("lb,k", [(0.5, 3), (1.0, 3), (0.7, 5), (0.3, 2), (0.5, 1), (0.9, 8), (0.6, 11),
+                                  (0.8, 4), (0.7, 6), (0.8, 7), (0.9, 9), (0.9, 16), (0.95, 17),
+                                  (0.97, 24), (0.99, 33)])
 def test_ss_xtr0(ctx, lb, k):
+    """Every level count of the grouped sweep (k - 1 = 1..8 exactly, 12 / 16 / 24 / 32
+    rounded up) bit-exact against the golden-pinned oracle at L = 101 (k > 16: past the
+    round-2 limit)."""
     codes, lens = load_xtr0()
     codes, lens = codes[:48], lens[:48]
     K = ctx.gram(P.make(L.KMG_SUBSTRING, k=k, lbda=lb), codes, lens, L.KMG_F64)
     assert np.array_equal(K, cref.ss(codes, lens, lb, k))
 
 
-def test_ss_ragged(ctx):
-    rng = np.random.default_rng(4)
-    seqs = ["".join(rng.choice(list("ACGT"), size=rng.integers(0, 150))) for _ in range(40)]
+@pytest.mark.parametrize("k,maxlen", [(3, 150), (12, 150), (3, 100), (6, 100), (20, 110)])
+def test_ss_ragged(ctx, k, maxlen):
+    """Ragged rows (lengths 0..maxlen): past length 127 the 64-row strip kernel, below it
+    the grouped sweep with idle rows / groups of short pairs."""
+    rng = np.random.default_rng(4 + k)
+    seqs = ["".join(rng.choice(list("ACGT"), size=rng.integers(0, maxlen))) for _ in range(40)]
     codes, lens = E.encode(seqs)
-    K = ctx.gram(P.make(L.KMG_SUBSTRING, k=3, lbda=0.5), codes, lens, L.KMG_F64)
-    assert np.array_equal(K, cref.ss(codes, lens, 0.5, 3))
+    K = ctx.gram(P.make(L.KMG_SUBSTRING, k=k, lbda=0.8), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.ss(codes, lens, 0.8, k))
+    if maxlen <= 110:  # rows of another call: the lower triangle without the mirror
+        Kr = ctx.gram(P.make(L.KMG_SUBSTRING, k=k, lbda=0.8), codes[5:], lens[5:], L.KMG_F64)
+        assert np.array_equal(Kr, K[5:, 5:])
+
+
+def test_ss_limits(ctx):
+    """k = 34 at L = 101 (more than 32 DP levels in registers) and k = 17 past length 127
+    are the SS kernels' remaining limits: KMG_EUNSUPPORTED, never a wrong value."""
+    codes, lens = load_xtr0()
+    with pytest.raises(L.KmgUnsupported):
+        ctx.gram(P.make(L.KMG_SUBSTRING, k=34, lbda=0.9), codes[:4], lens[:4], L.KMG_F64)
+    c2, l2 = E.encode(["ACGT" * 40, "ACGA" * 40])
+    with pytest.raises(L.KmgUnsupported):
+        ctx.gram(P.make(L.KMG_SUBSTRING, k=17, lbda=0.9), c2, l2, L.KMG_F64)
 
 
 def test_gappy_k1g0(ctx):

@@ -143,3 +143,33 @@ def test_gpu_la_intended_rejects_non_acgt(ctx):
     finally:
         for x in (d_codes, d_lens, d_out):
             ctx.dfree(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("smith", [0, 1])
+@pytest.mark.parametrize("lmin,lmax", [(60, 103), (104, 127), (128, 250)])
+def test_gpu_la_intended_lengths(engine, smith, lmin, lmax):
+    """Every launch shape against the oracle: the grouped sweep with 8-lane groups (rows up
+    to 103), 16-lane groups (up to 127), and the 64-row strip kernel beyond."""
+    rng = np.random.default_rng(40 + lmax + smith)
+    seqs = ["".join(rng.choice(list("ACGT"), size=int(rng.integers(lmin, lmax + 1))))
+            for _ in range(9)]
+    codes, lens = E.encode(seqs)
+    got = engine.local_alignment(seqs, 11, 1, 0.2, smith, eig=1, intended=True)
+    ref = cpu_ref.la_intended(codes, lens, 11, 1, 0.2, smith)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, ref, rtol=4e-16, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_la_intended_past_1024(engine):
+    """Lengths past round 2's 1024 limit: the strip kernel with fewer pairs a block (the
+    boundary rows of 1300 columns take 42 KB of LDS per pair).  Max form, small beta so the
+    values stay finite."""
+    rng = np.random.default_rng(77)
+    seqs = ["".join(rng.choice(list("ACGT"), size=n)) for n in (1100, 1300)]
+    codes, lens = E.encode(seqs)
+    got = engine.local_alignment(seqs, 11, 1, 0.05, 1, eig=1, intended=True)
+    ref = cpu_ref.la_intended(codes, lens, 11, 1, 0.05, 1)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, ref, rtol=4e-16, atol=0)
