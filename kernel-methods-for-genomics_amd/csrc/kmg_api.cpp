@@ -108,6 +108,8 @@ struct Tuning {
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
   int pl_dbg = 0;           // KMG_PL_DBG: diagnostics only (wrong results): 1 no correction
                             // weights, 2 no bank rotation
+  int ss_lpp = 0;           // KMG_SS_LPP: SS grouped sweep, lanes a pair (0 auto, 16, 32)
+  int la_lpp = 0;           // KMG_LA_LPP: intended-LA grouped sweep, lanes a pair (0 auto, 16, 32)
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
   int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
@@ -151,6 +153,8 @@ void read_tuning(Tuning &t) {
   t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
   t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
+  t.ss_lpp = env_or("KMG_SS_LPP", d.ss_lpp);
+  t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
@@ -171,6 +175,7 @@ struct kmg_ctx {
   DevBuf dense_tiles;             // dense Gram tile order (dense_tile_order)
   int64_t dense_key[4] = {-1, -1, -1, -1};
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
+  DevBuf gcoef;                   // generic WD/WDS kernel: beta_k, delta_s (device copies)
   DevBuf packed;                  // 2-bit packed sequence records (Packed, kmg_internal.h)
   DevBuf tri_stage, tri_scratch;  // upper-triangle multi-GPU build: round slabs, full rows
   DevBuf ovf;                     // 16-bit round slabs: count-overflow flag
@@ -249,7 +254,8 @@ void mismatch_weights(int k, int m, int64_t *w) {
     return v;
   };
   for (int d = 0; d <= 32; ++d) w[d] = 0;
-  for (int d = 0; d <= k; ++d) {
+  // two k-mers further apart than 2m share no beta within m of both: w[d > 2m] = 0
+  for (int d = 0; d <= std::min(k, std::min(2 * m, 32)); ++d) {
     int64_t tot = 0;
     for (int i = 0; i <= k - d; ++i) {
       int64_t p3 = 1;
@@ -800,7 +806,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     case KMG_MISMATCH: {
       const bool mm = p->kind == KMG_MISMATCH;
       const int k = p->k;
-      if (k < 1 || k > 16) return fail(KMG_EUNSUPPORTED, "k=%d outside [1,16]", k);
+      if (k < 1) return fail(KMG_EINVAL, "k=%d < 1", k);
       if (mm && p->m < 0) return fail(KMG_EINVAL, "m < 0");
       IndexGeom g{};
       g.k = k;
@@ -811,6 +817,56 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (mm && n > 0 && ldc < g.window)
         return fail(KMG_EINVAL, "mismatch: code rows (%lld) shorter than the window %d",
                     (long long)ldc, g.window);
+      if (k > 16) {
+        // k-mers past 32 bits: the generic per-pair kernels (kmg_generic.hip)
+        if (narrow) return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
+        if (dt == KMG_I32 && mm && p->normalize)
+          return fail(KMG_EINVAL, "normalised output needs a floating dtype");
+        const SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
+        const int sq = (ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
+                        ranges[0].col_lo == 0) ? 1 : 0;
+        bool unsupported = false;
+        auto run = [&](hipError_t e) {
+          if (e == hipErrorNotSupported) {
+            unsupported = true;
+            return hipSuccess;
+          }
+          return e;
+        };
+        int rc;
+        if (!mm) {
+          rc = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+            return run(launch_gram_sp_generic(q, r0, r1, k, sq, oq, c->stream));
+          });
+        } else {
+          int64_t w[33];
+          mismatch_weights(k, p->m, w);
+          const int maxd = std::min(k, std::min(2 * p->m, 32));
+          const int P = std::max(0, g.window - k + 1);
+          double wmax = 0.0;
+          for (int d = 0; d <= maxd; ++d) wmax = std::max(wmax, (double)w[d]);
+          if (p->m > 16 || wmax * P * P >= 4.0e18)
+            return fail(KMG_EUNSUPPORTED, "mismatch (%d, %d): counts past 64 bits", k, p->m);
+          KMG_TRY(upload_wtab(c, w));
+          if (p->normalize) {
+            KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)std::max<int64_t>(1, n)));
+            KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)std::max<int64_t>(1, n)));
+            StageTimer t(c, ST_DIAG);
+            KMG_HIP(launch_mm_generic_diag(q, g.window, k, c->wtab.as<int64_t>(), maxd,
+                                           c->diagv.as<double>(), c->dsq.as<double>(), c->stream));
+            o.normalize = 1;
+            o.diagv = c->diagv.as<double>();
+            o.dsq = c->dsq.as<double>();
+          }
+          rc = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+            return run(launch_gram_mm_generic(q, r0, r1, g.window, k, c->wtab.as<int64_t>(), maxd,
+                                              sq, oq, c->stream));
+          });
+        }
+        if (unsupported)
+          return fail(KMG_EUNSUPPORTED, "k = %d: rows longer than 4096 symbols", k);
+        return rc;
+      }
       const int L = mm ? g.window : maxlen;
       g.pmax = L - k + 1 > 0 ? L - k + 1 : 1;
       if (g.pmax > 4095) return fail(KMG_EUNSUPPORTED, "more than 4095 k-mers per sequence");
@@ -1043,8 +1099,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     case KMG_WD:
     case KMG_WDS: {
       if (p->d < 0 || p->d > KMG_MAX_COEF) return fail(KMG_EUNSUPPORTED, "d outside [0,64]");
-      if (p->kind == KMG_WDS && (p->S < 0 || p->S > 15))
-        return fail(KMG_EUNSUPPORTED, "S outside [0,15]");
+      if (p->kind == KMG_WDS && p->S < 0) return fail(KMG_EINVAL, "S < 0");
+      if (p->kind == KMG_WDS && p->S >= KMG_MAX_COEF)
+        return fail(KMG_EUNSUPPORTED, "S outside [0,%d]", KMG_MAX_COEF - 1);
       if (dt == KMG_I32) return fail(KMG_EINVAL, "WD/WDS produce float64 values");
       if (p->span < 0) return fail(KMG_EINVAL, "span < 0");
       if (p->span > 0) {
@@ -1069,6 +1126,32 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, 0, c->packed.as<uint32_t>(), c->stream));
       }
       bool unsupported = false;
+      // past the specialised kernels' shift / length limits (WDS S > 15, or S > 7 above 128
+      // symbols; WD / WDS above 256): the generic per-pair kernel (kmg_generic.hip), the
+      // coefficients in a device buffer
+      const bool sq = ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
+                      ranges[0].col_lo == 0;
+      auto generic = [&](int64_t r0, int64_t r1, const OutSpec &oq) -> hipError_t {
+        if (p->kind == KMG_WD && p->span > 0) return hipErrorNotSupported;
+        if (!c->gcoef.p) {
+          if (c->gcoef.ensure(2 * KMG_MAX_COEF * sizeof(double)) != KMG_OK) return hipErrorOutOfMemory;
+        }
+        double h[2 * KMG_MAX_COEF];
+        memcpy(h, p->coef_a, sizeof(double) * KMG_MAX_COEF);
+        if (p->kind == KMG_WD) {
+          for (int t = 0; t < KMG_MAX_COEF; ++t) h[KMG_MAX_COEF + t] = 0.0;
+          h[KMG_MAX_COEF] = 0.5;  // delta_0: a WD match adds 0.5 * 2 = 1.0 exactly
+        } else {
+          memcpy(h + KMG_MAX_COEF, p->coef_b, sizeof(double) * KMG_MAX_COEF);
+        }
+        hipError_t e = hipMemcpyAsync(c->gcoef.p, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // pageable source
+        if (e != hipSuccess) return e;
+        const double *ca = c->gcoef.as<double>();
+        return launch_gram_wds_generic(q, r0, r1, p->d, p->kind == KMG_WD ? 0 : p->S, p->span, ca,
+                                       ca + KMG_MAX_COEF, p->kind == KMG_WD ? 1 : 0,
+                                       sq && r0 == 0 && r1 == n ? 1 : 0, oq, c->stream);
+      };
       const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         hipError_t e = p->kind == KMG_WD
                            ? (packed_wd ? launch_gram_wd_packed(q, pkd, r0, r1, p->d, p->span,
@@ -1077,6 +1160,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                                          c->stream))
                            : launch_gram_wds(q, r0, r1, p->d, p->S, p->span, p->coef_a,
                                              p->coef_b, oq, c->stream);
+        if (e == hipErrorNotSupported) e = generic(r0, r1, oq);
         if (e == hipErrorNotSupported) {
           unsupported = true;
           return hipSuccess;
@@ -1097,7 +1181,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const int mirror = (ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n) ? 1 : 0;
       bool unsupported = false;
       const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-        hipError_t e = launch_gram_ss(q, r0, r1, p->k, p->lambda, p->lambda2, mirror, oq, c->stream);
+        hipError_t e = launch_gram_ss(q, r0, r1, p->k, p->lambda, p->lambda2, mirror, oq, c->stream,
+                                      c->tune.ss_lpp);
         if (e == hipErrorNotSupported) {
           unsupported = true;
           return hipSuccess;
@@ -1131,7 +1216,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             os.out = (char *)oq.out + (size_t)(a - r0) * oq.ld * dtype_size(dt);
             const int64_t b = std::min(r1, a + 65535);
             hipError_t e = launch_gram_la(q, a, b, p->la_e, p->la_d, p->la_beta, p->smith,
-                                          full && b - a == n ? 1 : 0, os, c->stream);
+                                          full && b - a == n ? 1 : 0, os, c->stream,
+                                          c->tune.la_lpp);
             if (e == hipErrorNotSupported) {
               unsupported = true;
               return hipSuccess;
@@ -1238,7 +1324,8 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
-                    &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs};
+                    &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
+                    &c->gcoef};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);

@@ -277,6 +277,20 @@ struct SeqSpec {
   int64_t n, ldc;
   int maxlen;
 };
+
+// kmg_generic.hip: per-pair fallbacks (spectrum / mismatch k > 16, WD / WDS past the
+// specialised kernels' shift and length limits)
+hipError_t launch_gram_sp_generic(const SeqSpec &q, int64_t row0, int64_t row1, int k, int mirror,
+                                  const OutSpec &o, hipStream_t s);
+hipError_t launch_mm_generic_diag(const SeqSpec &q, int W, int k, const int64_t *w, int maxd,
+                                  double *diagv, double *dsq, hipStream_t s);
+hipError_t launch_gram_mm_generic(const SeqSpec &q, int64_t row0, int64_t row1, int W, int k,
+                                  const int64_t *w, int maxd, int mirror, const OutSpec &o,
+                                  hipStream_t s);
+hipError_t launch_gram_wds_generic(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S,
+                                   int span, const double *coef_a, const double *coef_b,
+                                   int wd_diag, int mirror, const OutSpec &o, hipStream_t s);
+
 hipError_t launch_gram_wd(const SeqSpec &q, int64_t row0, int64_t row1, int d, int span,
                           const double *beta, const OutSpec &o, hipStream_t s);
 hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row0, int64_t row1,
@@ -285,11 +299,13 @@ hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row
 hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S, int span,
                            const double *beta, const double *delta, const OutSpec &o,
                            hipStream_t s);
+// lpp: lanes a pair of the grouped sweep (0 auto; 16 / 32 force the wider groups)
 hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
-                          double lam2, int mirror, const OutSpec &o, hipStream_t s);
+                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp = 0);
 // LA kernel, intended semantics (KMG_LA_INTENDED): five-array affine-gap DP per pair
 hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
-                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s);
+                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s,
+                          int lpp = 0);
 // stats[0] = max code over every row's first len symbols, stats[1] = min len (preset to 0 /
 // UINT_MAX by the caller)
 hipError_t launch_row_stats(const SeqSpec &q, uint32_t *stats, hipStream_t s);

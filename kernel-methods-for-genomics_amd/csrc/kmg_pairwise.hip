@@ -660,24 +660,24 @@ __global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, 
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int r = r0 + k;
-        // rows past n_x compute don't-care values: they feed only rows below them (also
-        // past n_x) and the next lane's rows (past n_x as well), never S or K; every level
-        // is evaluated and selected, no per-lane branches
-        {
+        if (r <= nx) {
           const uint32_t xprev = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
           const uint32_t xcur = (xw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
           const bool match = r >= 1 && c >= 1 && xprev == yprev;
-          const int rc = min(r, c);  // level lvl is live where lvl <= min(r, c)
           double cur[NL];
 #pragma unroll
           for (int t = 0; t < NL; ++t) {
             const int lvl = t + 1;
-            double v = __dadd_rn(__dmul_rn(lam, above[t]), __dmul_rn(lam, last[k][t]));
-            v = __dsub_rn(v, __dmul_rn(lam2, adiag[t]));
-            const double prevlvl = (t == 0) ? 1.0 : adiag[t - 1];
-            const double vm = __dadd_rn(v, __dmul_rn(lam2, prevlvl));
-            v = match ? vm : v;
-            cur[t] = (lvl < kk && lvl <= rc) ? v : 0.0;
+            double v = 0.0;
+            if (lvl < kk && r >= lvl && c >= lvl) {
+              v = __dadd_rn(__dmul_rn(lam, above[t]), __dmul_rn(lam, last[k][t]));
+              v = __dsub_rn(v, __dmul_rn(lam2, adiag[t]));
+              if (match) {
+                const double prevlvl = (t == 0) ? 1.0 : adiag[t - 1];
+                v = __dadd_rn(v, __dmul_rn(lam2, prevlvl));
+              }
+            }
+            cur[t] = v;
           }
           if (c < ny && r < nx && ycur == xcur) {
             double bkm1 = 1.0;  // B_0 == 1
@@ -940,7 +940,8 @@ __global__ __launch_bounds__(256) void gram_lag_kernel(SeqSpec q, int64_t row0, 
 }
 
 hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
-                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s) {
+                          double beta, int smith, int mirror, const OutSpec &o, hipStream_t s,
+                          int lpp) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   const int ML = q.maxlen;
@@ -966,8 +967,14 @@ hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e
                          s, q, row0, row1, cf, mirror, o);
     return hipGetLastError();
   };
-  if (ML + 1 <= 8 * 13)
+  // 16 lanes x 8 rows a pair by default (N = 1000, L = 101: 7.2 ms sum form against 11.9 at
+  // 8 x 13 and 7.6 at 32 x 4; profiles/r03j_ss_la_lpp_ab.jsonl); KMG_LA_LPP for the A/B
+  if (lpp == 8 && ML + 1 <= 8 * 13)
     return grouped(std::integral_constant<int, 8>{}, std::integral_constant<int, 13>{});
+  if (lpp == 32 && ML + 1 <= 32 * 4)
+    return grouped(std::integral_constant<int, 32>{}, std::integral_constant<int, 4>{});
+  if (lpp == 64 && ML + 1 <= 64 * 2)
+    return grouped(std::integral_constant<int, 64>{}, std::integral_constant<int, 2>{});
   if (ML + 1 <= 16 * 8)
     return grouped(std::integral_constant<int, 16>{}, std::integral_constant<int, 8>{});
   // longer sequences: the 64-row strip kernel, as many waves a block as the boundary rows'
@@ -1192,7 +1199,7 @@ hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, 
 }
 
 hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
-                          double lam2, int mirror, const OutSpec &o, hipStream_t s) {
+                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   const int ML = q.maxlen;
@@ -1213,24 +1220,33 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
 #define KMG_SSG(LPP_, R_, NL_) \
   grouped(std::integral_constant<int, LPP_>{}, std::integral_constant<int, R_>{}, \
           std::integral_constant<int, NL_>{})
-  if (nl <= 4 && ML + 1 <= 8 * 13) {
+  // defaults from interleaved A/B at N = 1000, L = 101 (profiles/r03j_ss_la_lpp_ab.jsonl):
+  // fewer rows a lane keep the cell registers small (k = 5: 8 lanes x 13 rows 23.4 ms,
+  // 16 x 7 10.6 ms); KMG_SS_LPP forces another group width for the A/B
+  if (lpp == 8 && nl <= 4 && ML + 1 <= 8 * 13) return KMG_SSG(8, 13, 4);
+  if (lpp == 16 && nl <= 8 && ML + 1 <= 16 * 7) return KMG_SSG(16, 7, 8);
+  if (lpp == 32 && nl <= 4 && ML + 1 <= 32 * 4) return KMG_SSG(32, 4, 4);
+  if (lpp == 64 && nl <= 8 && ML + 1 <= 64 * 2) return KMG_SSG(64, 2, 8);
+  if (lpp == 32 && nl > 8 && nl <= 16 && ML + 1 <= 32 * 4) return KMG_SSG(32, 4, 16);
+  if (nl <= 4 && ML + 1 <= 16 * 7) {
     switch (nl) {
-      case 1: return KMG_SSG(8, 13, 1);
-      case 2: return KMG_SSG(8, 13, 2);
-      case 3: return KMG_SSG(8, 13, 3);
-      default: return KMG_SSG(8, 13, 4);
+      case 1: return KMG_SSG(16, 7, 1);
+      case 2: return KMG_SSG(16, 7, 2);
+      case 3: return KMG_SSG(16, 7, 3);
+      default: return KMG_SSG(16, 7, 4);
     }
   }
-  if (nl <= 8 && ML + 1 <= 16 * 7) {
+  if (nl <= 8 && ML + 1 <= 32 * 4) {
     switch (nl) {
-      case 5: return KMG_SSG(16, 7, 5);
-      case 6: return KMG_SSG(16, 7, 6);
-      case 7: return KMG_SSG(16, 7, 7);
-      default: return KMG_SSG(16, 7, 8);
+      case 5: return KMG_SSG(32, 4, 5);
+      case 6: return KMG_SSG(32, 4, 6);
+      case 7: return KMG_SSG(32, 4, 7);
+      default: return KMG_SSG(32, 4, 8);
     }
   }
-  if (nl <= 16 && ML + 1 <= 32 * 4) return nl <= 12 ? KMG_SSG(32, 4, 12) : KMG_SSG(32, 4, 16);
-  if (nl <= 32 && ML + 1 <= 64 * 2) return nl <= 24 ? KMG_SSG(64, 2, 24) : KMG_SSG(64, 2, 32);
+  if (nl <= 32 && ML + 1 <= 64 * 2)
+    return nl <= 12 ? KMG_SSG(64, 2, 12) : nl <= 16 ? KMG_SSG(64, 2, 16)
+                    : nl <= 24 ? KMG_SSG(64, 2, 24) : KMG_SSG(64, 2, 32);
 #undef KMG_SSG
   // longer sequences: the strip kernel (64-row strips, the boundary row in LDS), as many
   // waves (pairs) a block as their LDS allows (4 up to length ~300 at k = 16, 1 to ~1200)

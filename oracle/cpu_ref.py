@@ -55,6 +55,31 @@ def spectrum(codes, lens, k):
     return (Phi @ Phi.T).toarray().astype(np.int64)
 
 
+def spectrum_windows(codes, lens, k):
+    """get_spectrum_K for any k (kernels.py:28-47) by counting windows: K[i, j] =
+    sum_w c_i(w) c_j(w) over the all-ACGT windows w of length k (a window holding another
+    character equals none of the 4^k ACGT betas, kernels.py:23-24).  The same count as
+    spectrum() without the 4^k-column Phi, so it also covers k past 31; checked against
+    spectrum() for small k in tests/test_oracle_generic.py."""
+    from collections import Counter
+    seqs = _codes_list(codes, lens)
+    cnt = []
+    for s in seqs:
+        c = Counter()
+        for a in range(len(s) - k + 1):
+            win = s[a:a + k]
+            if np.all(win < 4):
+                c[win.tobytes()] += 1
+        cnt.append(c)
+    n = len(seqs)
+    K = np.zeros((n, n), dtype=np.int64)
+    for i in range(n):
+        for j in range(i, n):
+            a, b = (cnt[i], cnt[j]) if len(cnt[i]) <= len(cnt[j]) else (cnt[j], cnt[i])
+            K[i, j] = K[j, i] = sum(v * b.get(w, 0) for w, v in a.items())
+    return K
+
+
 # --------------------------------------------------------------------- mismatch
 def mismatch_weights(k, m):
     """Closed form of <Phi_x, Phi_y> per k-mer pair at Hamming distance h (see
