@@ -51,7 +51,7 @@ INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROAR
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
           "(k=9,m=1), 1/2/4/8 GPUs")
 STAGES = ("count", "scan", "place", "fine", "pack", "slots", "extract", "features", "diag",
-          "gram", "gather")
+          "gram", "mirror", "gather")
 
 
 class Dist:
@@ -614,6 +614,34 @@ def gather_roofline(res, world, esz):
             "frac": recv / t / XGMI_IN_PEAK}
 
 
+def mm_gather_roofline(n, rows, gram_ms, k=9, P=93):
+    """Random-line gather model of the MM(9,1) Gram launch (see the secondary line)."""
+    import math
+    if n <= 24000:
+        mean = 16.0 * n * P / 4.0 ** k
+        eu = ec = 0.0
+        pr = math.exp(-mean)
+        for x in range(0, 4000):
+            if x > 0:
+                pr *= mean / x
+                eu += pr * math.ceil(x / 64.0)
+                ec += pr * math.ceil((8.0 + x) / 64.0)
+        per_window = 27 * eu + 9 * ec
+        form = "pair lines (27 uniform + 9 correction groups a window, one chunk)"
+    else:
+        nch = -(-n // 28572)
+        per_window = 117.0 * nch
+        form = "slot table (117 one-line lists a window and chunk, %d chunks)" % nch
+    lines = rows * P * per_window
+    rate = lines / (gram_ms / 1e3)
+    return {"bound": "infinity-cache random 128-B line gathers", "table": form,
+            "lines_per_window": per_window, "lines_per_launch": lines,
+            "achieved_Glines_per_s": rate / 1e9, "ceiling_Glines_per_s": GATHER_CEILING / 1e9,
+            "frac": rate / GATHER_CEILING,
+            "source": "profiles/r02_mall_gather.jsonl (78.6 MB table, 128-B lines); "
+                      "PMC of the same launch profiles/r03l_mm_n20000_pmc.txt"}
+
+
 def _chunked(n, max_chunk):
     """Column chunk width of a posting-list build: n split evenly into ceil(n / max_chunk)."""
     nch = -(-n // max_chunk)
@@ -641,10 +669,16 @@ def projection(sp, n, extra):
         t5_index = sum(v for k, v in s5.items() if k in ("count", "scan", "place", "fine", "pack",
                                                          "slots"))
         n5 = c5["N"]
+        # the one-GPU build computes the upper block triangle (7 chunks: (7 + 1) / 14 of the
+        # full rows) and mirrors the rest: the model wants the full-row Gram time
+        nch = -(-n5 // _chunked(n5, 28572))
+        g_rows = s5["gram"] * (2.0 * nch) / (nch + 1) if s5.get("mirror") else s5["gram"]
         out["config5_mismatch_k9_n200000_raw_int32"] = {
-            str(g): v for g, v in scaling_projection(
-                n5, c5["ms_per_step"], t5_index, s5["gram"], fill, 4, 1,
-                chunk=_chunked(n5, 28572)).items()}
+            "one_gpu": {"gram_ms": s5["gram"], "mirror_ms": s5.get("mirror"),
+                        "full_rows_gram_ms_model": g_rows},
+            **{str(g): v for g, v in scaling_projection(
+                n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1,
+                chunk=_chunked(n5, 28572)).items()}}
     return out
 
 
@@ -751,16 +785,13 @@ def main():
             "N": args.mm_n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
             "hbm_frac_of_gram_kernel": mm_bytes / (mm["stages_ms"]["gram"] / 1e3) / HBM_PEAK,
-            # the kernel's real bound: one random 128-B slot line per posting list, 117 lists
-            # per window (k + 3k(k-1)/2 at k = 9), 93 windows per row, against the measured
-            # random-line gather ceiling of a 79 MB table (tools/mall_gather.hip)
-            "gather_roofline": {
-                "bound": "infinity-cache random 128-B line gathers",
-                "lines_per_launch": mm_rows_launch * 93 * 117,
-                "achieved_Glines_per_s": mm_rows_launch * 93 * 117 / (mm["stages_ms"]["gram"] / 1e3) / 1e9,
-                "ceiling_Glines_per_s": GATHER_CEILING / 1e9,
-                "frac": mm_rows_launch * 93 * 117 / (mm["stages_ms"]["gram"] / 1e3) / GATHER_CEILING,
-                "source": "profiles/r02_mall_gather.jsonl (78.6 MB table, 128-B lines)"},
+            # the kernel's other bound: random 128-B posting lines from the Infinity Cache.
+            # N <= 24000 runs the pair-lines table (one chunk): per row window 27 uniform
+            # groups of E[ceil(X / 64)] lines and 9 correction groups of E[ceil((8 + X) / 64)],
+            # X ~ Poisson(16 * N * 93 / 4^9) (kmg_pairs.hip); the slot table above that
+            # (117 one-line lists per window and chunk)
+            "gather_roofline": mm_gather_roofline(args.mm_n, mm_rows_launch,
+                                                  mm["stages_ms"]["gram"]),
             "spot_check": mm["spot_check"],
         }
         if "collective_free" in mm:
