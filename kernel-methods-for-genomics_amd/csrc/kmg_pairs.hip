@@ -568,29 +568,40 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
   const int slot = g8 & 3;  // lane group inside its half-wave (bank-sorted lines)
   const bool rs1 = (slot & 1) != 0, rs2 = (slot & 2) != 0;
   uint32_t sink = 0;
-  auto consume = [&](const uint4 &xr, const uint2 &e) {
-    const uint4 x = (dbg & 2) ? xr : rot4(xr, rs1, rs2);
+  // the header piece of a correction group's first line (lane j8 = 0): its 8 halfwords
+  // become the dummy columns dcol .. dcol + 7, so every add of a step takes the same path
+  const uint4 dpiece = make_uint4(dcol | ((dcol + 1u) << 16), (dcol + 2u) | ((dcol + 3u) << 16),
+                                  (dcol + 4u) | ((dcol + 5u) << 16), (dcol + 6u) | ((dcol + 7u) << 16));
+  auto consume = [&](const uint4 &xl, const uint2 &e) {
     if (dbg & 4) {  // diagnostics: no LDS adds
-      sink += x.x ^ x.y ^ x.z ^ x.w;
+      sink += xl.x ^ xl.y ^ xl.z ^ xl.w;
       return;
     }
     if ((dbg & 1) || !__any((e.x & RE_CORR) != 0)) {
-      add_piece(x, w2);
+      add_piece((dbg & 2) ? xl : rot4(xl, rs1, rs2), w2);
       return;
     }
+    const uint4 x = rot4(((e.x & RE_HDR) && j8 == 0) ? dpiece : xl, rs1, rs2);
+    // the lane adds halfwords hb .. hb + 7 of its line, instruction v halfword hb + ((v + 2
+    // slot) & 7): the halfword ranges of the row z_outer = u_outer and of the exact bin
+    // become 8-bit masks over the lane's halfwords, rotated into instruction order once;
+    // each add's weight is w2 + cc [in the row] + (wx - cc) [in the exact bin]
     const uint32_t rlo = e.y & 0xFFu, rhi = (e.y >> 8) & 0xFFu;
     const uint32_t elo = (e.y >> 16) & 0xFFu, ehi = e.y >> 24;
-    const uint32_t vlo = (e.x & RE_HDR) ? 8u : 0u;
-    const int wx = (e.x & RE_DESIG) ? h0 : 0;
+    const int dwx = ((e.x & RE_DESIG) ? h0 : 0) - cc;
+    const uint32_t hb = 8u * (uint32_t)j8, sh = 2u * (uint32_t)slot;
+    auto lane_mask = [&](uint32_t lo, uint32_t hi) -> uint32_t {
+      const uint32_t a = min(max(lo, hb), hb + 8u) - hb, b = min(max(hi, hb), hb + 8u) - hb;
+      const uint32_t m = ((1u << b) - 1u) & ~((1u << a) - 1u);
+      return ((m >> sh) | (m << (8u - sh))) & 0xFFu;
+    };
+    const uint32_t mr = (e.x & RE_CORR) ? lane_mask(rlo, rhi) : 0u;
+    const uint32_t me = (e.x & RE_CORR) ? lane_mask(elo, ehi) : 0u;
     const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      // halfword of the line this instruction adds (rotated dwords)
-      const uint32_t h = 8u * (uint32_t)j8 + 2u * (((uint32_t)(v >> 1) + (uint32_t)slot) & 3u) +
-                         (uint32_t)(v & 1);
-      const int w = (h - rlo < rhi - rlo) ? ((h - elo < ehi - elo) ? w2 + wx : w2 + cc) : w2;
-      const uint32_t ad = (v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]);
-      lds_add(h < vlo ? 4u * (dcol + h) : ad, w);
+      const int w = w2 + cc * (int)((mr >> v) & 1u) + dwx * (int)((me >> v) & 1u);
+      lds_add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w);
     }
   };
   // next ring entry of this lane's 8-lane group (the dummy line 0 when the ring is empty)
