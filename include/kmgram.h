@@ -212,7 +212,10 @@ int kmg_svm_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
  * all-gathered in place (half the xGMI bytes of gather = 1) and every rank copies it into
  * K and mirrors it into the lower triangle locally (K[x][t*R + y] = K[t*R + y][x]).
  * gather = 3: the gather = 2 layout with every rank's blocks computed on this GPU (a
- * one-GPU rehearsal of the multi-rank assembly; no RCCL).  gather = 1 or 2 with nranks > 1
+ * one-GPU rehearsal of the multi-rank assembly; no RCCL).  gather = 4: like 0 (no data-path
+ * collective) with this rank's blocks packed: row t*block + y of d_out holds row
+ * t*R + rank*block + y of K (d_out needs ceil(n / R) * block rows: a rank's share of a K
+ * that no single GPU could hold).  gather = 1 or 2 with nranks > 1
  * needs kmg_comm_init with the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
  * get_mismatch_K (kernels.py:41-45, 211-215) split over GPUs.
  */

@@ -1531,7 +1531,9 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      int32_t gather, int narrow_bits) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
   if (block < 1) return fail(KMG_EINVAL, "block < 1");
-  if (gather < 0 || gather > 3) return fail(KMG_EINVAL, "gather must be 0..3");
+  if (gather < 0 || gather > 4) return fail(KMG_EINVAL, "gather must be 0..4");
+  const bool packed = gather == 4;  // this rank's blocks, packed (no collective)
+  if (packed) gather = 0;
   if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
   const bool tri = gather >= 2;               // upper-triangle round slabs + local mirror
   // RCCL path: more than one rank, or a communicator of exactly this one rank (a 1-rank
@@ -1606,7 +1608,8 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     for (int64_t t = 0; t < nround; ++t) {
       const int64_t r0 = std::min(n, t * round + (int64_t)rank * block);
       const int64_t r1 = std::min(n, r0 + block);
-      ranges.push_back(RowRange{r0, r1, (char *)d_out + (size_t)r0 * ld_out * esz});
+      const int64_t orow = packed ? t * block : r0;  // output row of K's row r0
+      ranges.push_back(RowRange{r0, r1, (char *)d_out + (size_t)orow * ld_out * esz});
     }
     if (rccl) {
       after = [&](size_t t) -> int {

@@ -205,7 +205,8 @@ class Context:
         """Block-cyclic rows of this rank.  gather: False / 0 this rank's blocks only; True / 1
         full rows all-gathered in place over RCCL per round; 2 upper-triangle round slabs
         all-gathered + local mirror; 3 the upper-triangle layout with every rank's blocks
-        computed locally (one-GPU rehearsal, no RCCL)."""
+        computed locally (one-GPU rehearsal, no RCCL); 4 this rank's blocks packed (row
+        t * block + y of d_out = K row t * nranks * block + rank * block + y)."""
         g = int(gather) if not isinstance(gather, bool) else (1 if gather else 0)
         check(self.lib.kmg_gram_blocks(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        out_dtype, d_out, ld, int(nranks), int(rank), int(block),

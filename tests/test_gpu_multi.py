@@ -64,6 +64,30 @@ def test_blocks_union_equals_full(ctx, data, case, world, block):
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("world,rank,block", [(1, 0, 1500), (3, 1, 100), (8, 7, 64), (2, 0, 256)])
+def test_blocks_packed_rank_share(ctx, data, case, world, rank, block):
+    """gather = 4 (the multi-GPU bench's collective-free build): this rank's blocks packed
+    in its own buffer, row t*block + y = K row t*world*block + rank*block + y."""
+    params, dt = CASES[case]
+    codes, lens, d_codes, d_lens = data
+    n, ldc = codes.shape
+    full = ctx.gram(params, codes, lens, dt)
+    rounds = block_cyclic_ranges(n, world, rank, block)
+    esz = np.dtype(L.DTYPES[dt]).itemsize
+    d_out = ctx.dmalloc(len(rounds) * block * n * esz)
+    try:
+        ctx.memset(d_out, 0xA5, len(rounds) * block * n * esz)
+        ctx.gram_blocks(params, d_codes, d_lens, n, ldc, dt, d_out, n, world, rank, block, 4)
+        ctx.synchronize()
+        got = np.empty((len(rounds) * block, n), dtype=L.DTYPES[dt])
+        ctx.d2h(got, d_out)
+    finally:
+        ctx.dfree(d_out)
+    for t, (a, b) in enumerate(rounds):
+        assert np.array_equal(got[t * block:t * block + (b - a)], full[a:b]), (t, a, b)
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
 @pytest.mark.parametrize("world,block", [(1, 1500), (1, 336), (2, 256), (3, 100), (8, 64),
                                          (4, 50)])
 def test_upper_triangle_assembly_equals_full(ctx, data, case, world, block):
