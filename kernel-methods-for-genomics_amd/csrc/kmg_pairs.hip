@@ -150,7 +150,8 @@ __device__ __forceinline__ uint32_t pl_dummy(uint32_t dcol, uint32_t bank, uint3
 // in bank order.
 constexpr int PL_PACK_GROUPS = 16;
 constexpr int PL_IMG_WORDS = KMG_PL_MAXNL * 32;
-constexpr int PL_PACK_U = 8;  // entry loads in flight per lane
+constexpr int PL_PACK_U = 8;   // entry loads in flight per lane (runs past PL_PACK_R)
+constexpr int PL_PACK_R = 12;  // entries of a run kept in registers across both passes
 __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
                                                       const uint16_t *__restrict__ xent,
                                                       const uint32_t *__restrict__ rbase,
@@ -190,6 +191,11 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   const uint32_t n = __shfl(end, 15, 16);
   const uint32_t nl = live ? pl_lines(n, corr) : 0u;
   const bool pack = live && nl != PL_WIDE && n > 0;
+  // the run's first PL_PACK_R entries, issued before the LDS set-up and the summary loads
+  uint32_t colr[PL_PACK_R];
+#pragma unroll
+  for (int u = 0; u < PL_PACK_R; ++u)
+    colr[u] = (pack && (uint32_t)u < cnt) ? (uint32_t)xent[s0 + u] : 0xFFFFFFFFu;
   hist[lg][b] = 0;
   hist[lg][b + 16] = 0;
   rank[lg][b] = 0;
@@ -222,9 +228,14 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   uint16_t *im16 = (uint16_t *)img[lg];
   const uint32_t cap = 2u * nl;  // slots per bank and group
   auto slot = [&](uint32_t bk, uint32_t rk) { return 64u * (rk >> 1) + 2u * pl_dword(bk) + (rk & 1u); };
-  // this lane's run: entries [s0, s0 + cnt) of the exact index, group positions end - cnt + e
+  // this lane's run: entries [s0, s0 + cnt) of the exact index, group positions end - cnt + e.
+  // The first PL_PACK_R are loaded once, all in flight, and kept in registers for both
+  // passes (a sub-bin holds ~7 entries at N=20000); longer runs reload the rest per pass.
   auto for_run = [&](auto &&f) {
-    for (uint32_t e0 = 0; e0 < cnt; e0 += PL_PACK_U) {
+#pragma unroll
+    for (int u = 0; u < PL_PACK_R; ++u)
+      if (colr[u] != 0xFFFFFFFFu) f(end - cnt + (uint32_t)u, colr[u]);
+    for (uint32_t e0 = PL_PACK_R; e0 < cnt; e0 += PL_PACK_U) {
       uint32_t col[PL_PACK_U];
 #pragma unroll
       for (int u = 0; u < PL_PACK_U; ++u)

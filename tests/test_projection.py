@@ -37,3 +37,19 @@ def test_projection_chunk_granularity():
     mid = scaling_projection(n, 277.7, 2.8, 274.9, 6100.0, 4, 1, chunk=28572, worlds=(8,))[8]
     assert fine["compute_ms"] < mid["compute_ms"] < coarse["compute_ms"]
     assert abs(coarse["compute_ms"] - (2.8 + 274.9 / 8)) < 1e-6
+
+
+def test_bench_gather_model_matches_pmc():
+    """bench.mm_gather_roofline's pair-lines line count at N=20000 (76.5 lines a window,
+    142.3 M a launch) against the PMC of the same launch: TCC requests / 2 (64-B halves)
+    = 142.6 M (profiles/r03l_mm_n20000_pmc.txt)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    g = bench.mm_gather_roofline(20000, 20000, 3.9)
+    assert 76.0 < g["lines_per_window"] < 77.0
+    assert abs(g["lines_per_launch"] - (107359627.0 + 177767490.7) / 2) / g["lines_per_launch"] < 0.01
+    # the weak-scaled headline N keeps every GPU at ~n1^2 pairs
+    from kmgram.shard import weak_scaled_n
+    for w in (2, 4, 8):
+        n = weak_scaled_n(100000, w)
+        assert abs(n * n / w - 1e10) / 1e10 < 1e-3

@@ -7,6 +7,7 @@
 #                           log gpurun_out/<tag>/pytest.txt
 #   smoke                   __graft_entry__.smoke()
 #   bench[:ARGS]            python bench.py ARGS (colon-separated, e.g. bench:--steps:10)
+#   benchprof[:ARGS]        the same under rocprofv3 --kernel-trace --stats
 #   prof:WL[,WL...]         rocprofv3 kernel trace + PMC passes (profiles/run_profiles_r02.sh)
 #   ab:<cfg json>@@<sets json>   interleaved A/B of KMG_* settings (tools/ab_env.py)
 #   time:<cases json>       device-resident build timing (tools/time_mm.py)
@@ -40,6 +41,17 @@ for STEP in "$@"; do
       timeout -k 10 600 python3 -u bench.py ${ARGS//:/ } > "$OUT/bench$n.json" 2> "$OUT/bench$n.err" \
         || { echo "bench failed"; tail -30 "$OUT/bench$n.err"; exit 1; }
       cut -c1-400 "$OUT/bench$n.json"
+      ;;
+    benchprof*)
+      # bench.py itself under rocprofv3 --kernel-trace --stats (the roofline's kernel average
+      # must agree with the rocprof average of the same command)
+      ARGS=${STEP#benchprof}
+      ARGS=${ARGS#:}
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_trace" -o run \
+        -- python3 -u bench.py ${ARGS//:/ } > "$OUT/benchprof$n.json" 2> "$OUT/benchprof$n.err" \
+        || { echo "benchprof failed"; tail -30 "$OUT/benchprof$n.err"; exit 1; }
+      cut -c1-400 "$OUT/benchprof$n.json"
+      grep -m1 gram_sp_kernel "$OUT/bench_trace/run_kernel_stats.csv" | cut -d, -f1-4 | cut -c1-160
       ;;
     prof:*)
       WL=${STEP#prof:}
