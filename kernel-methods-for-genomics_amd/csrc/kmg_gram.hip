@@ -789,17 +789,29 @@ __global__ __launch_bounds__(256) void diag_ham_small_kernel(IndexGeom g, Packed
   __syncthreads();
   if (!valid) return;
   const uint32_t mask55 = (g.k >= 16) ? 0x55555555u : (0x55555555u & ((1u << (2 * g.k)) - 1u));
+  // K_ii = sum_{a,b} w[ham(x_a, x_b)] is symmetric in (a, b): count b > a twice and a = b
+  // once.  Lane l takes the windows a = l and a = P - 1 - l (and so on in strides of 128),
+  // whose b > a tails add up to ~P iterations for every lane (half the work of the full
+  // a x b square, no lane idling through a second, shorter stride)
   int cnt[M2 + 1];
 #pragma unroll
   for (int d = 0; d <= M2; ++d) cnt[d] = 0;
-  for (int a = lane; a < P; a += 64) {
+  auto tail = [&](int a) {
     const uint32_t xa = xk[a];
-    if (xa == KMG_INVALID) continue;
-    for (int b = 0; b < P; ++b) {
-      const uint32_t yb = xk[b];  // same address in every lane: LDS broadcast
+    if (xa == KMG_INVALID) return;
+    cnt[0] += 1;  // b = a
+    for (int b = a + 1; b < P; ++b) {
+      const uint32_t yb = xk[b];
       const int h = (yb == KMG_INVALID) ? 64 : ham2bit(xa, yb, mask55);
 #pragma unroll
-      for (int d = 0; d <= M2; ++d) cnt[d] += (h == d) ? 1 : 0;
+      for (int d = 0; d <= M2; ++d) cnt[d] += (h == d) ? 2 : 0;
+    }
+  };
+  for (int a0 = 0; a0 < (P + 1) / 2; a0 += 64) {
+    const int a = a0 + lane, a2 = P - 1 - a;
+    if (a < (P + 1) / 2) {
+      tail(a);
+      if (a2 != a) tail(a2);
     }
   }
   int64_t s = 0;
