@@ -24,6 +24,9 @@
 
 #include "kmg_internal.h"
 
+struct kmg_ctx;
+static int blas_handle(kmg_ctx *c);  // rocBLAS / rocSOLVER handle on the context stream
+
 using namespace kmg;
 
 namespace {
@@ -111,7 +114,8 @@ struct Tuning {
   int ss_lpp = 0;           // KMG_SS_LPP: SS grouped sweep, lanes a pair (0 auto, 16, 32)
   int la_lpp = 0;           // KMG_LA_LPP: intended-LA grouped sweep, lanes a pair (0 auto, 16, 32)
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
-  int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming
+  int algo = 0;             // KMG_ALGO: 0 auto, 1 dense MFMA, 2 index / Hamming, 3 dense
+                            // count vectors as an fp32 rocBLAS GEMM (configs[3]'s wording)
   int dense_kmax_sp = 5;    // KMG_DENSE_KMAX_SP: dense formulation for spectrum k <= this
   int dense_kmax_mm = 7;    // KMG_DENSE_KMAX_MM: ... and mismatch k <= this
   int idx_seqs = 0;         // KMG_IDX_SEQS: sequences per partition block (0: auto, build_index)
@@ -172,6 +176,7 @@ struct kmg_ctx {
   DevBuf kmers, partials, tmp, off, ent, diagv, dsq, wtab;
   DevBuf hcnt, hstart;            // index build v2: per-(bucket, block) counts / local starts
   DevBuf feat, masks;             // dense formulation: int8 F, neighbour xor masks
+  DevBuf feat32, k32;             // KMG_ALGO=3: fp32 F and the fp32 GEMM's K
   DevBuf dense_tiles;             // dense Gram tile order (dense_tile_order)
   int64_t dense_key[4] = {-1, -1, -1, -1};
   DevBuf slots;                   // mismatch slot layout (one 128-byte line per list)
@@ -678,6 +683,33 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
     o.diagv = c->diagv.as<double>();
     o.dsq = c->dsq.as<double>();
   }
+  if (c->tune.algo == 3) {
+    // BASELINE configs[3]'s literal "count-vector fp32 GEMM": F widened to fp32 and
+    // K = F F^T by rocblas_sgemm (dense fp32 MFMA; 2 N^2 4^k flops), then written out
+    KMG_TRY(c->feat32.ensure(sizeof(float) * (size_t)n * dp));
+    KMG_TRY(c->k32.ensure(sizeof(float) * (size_t)n * n));
+    {
+      StageTimer t(c, ST_FEATURES);
+      KMG_HIP(launch_i8_to_f32(c->feat.as<int8_t>(), n * (int64_t)dp, c->feat32.as<float>(), c->stream));
+    }
+    KMG_TRY(blas_handle(c));
+    {
+      StageTimer t(c, ST_GRAM);
+      const float one = 1.0f, zero = 0.0f;
+      // column-major view: G = F^T is dp x n (lda dp); K = G^T G (n x n, symmetric)
+      const rocblas_status st = rocblas_sgemm(c->blas, rocblas_operation_transpose,
+                                              rocblas_operation_none, (rocblas_int)n, (rocblas_int)n,
+                                              (rocblas_int)dp, &one, c->feat32.as<float>(), dp,
+                                              c->feat32.as<float>(), dp, &zero, c->k32.as<float>(),
+                                              (rocblas_int)n);
+      if (st != rocblas_status_success)
+        return fail(KMG_EHIP, "rocblas_sgemm: %s", rocblas_status_to_string(st));
+    }
+    return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+      StageTimer t(c, ST_EXTRACT);
+      return launch_f32_gram_out(c->k32.as<float>(), n, r0, r1, oq, c->stream);
+    });
+  }
   return each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
     const uint32_t *order = nullptr;
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
@@ -761,7 +793,7 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
   const int mm_eff = mm ? std::min(p->m, k) : 0;
   const bool dense_ok = k <= 8 && pmax <= 127 && dense_mask_count(k, mm_eff) <= 4096;
-  if (t.algo == 1 || (t.algo == 0 && dense_ok &&
+  if (t.algo == 1 || t.algo == 3 || (t.algo == 0 && dense_ok &&
                       (mm ? (k <= t.dense_kmax_mm) : (k <= t.dense_kmax_sp))))
     return SM_DENSE;  // (algo 1 without dense_ok: gram_device reports it)
   if (!use_index) return SM_HAMMING;
@@ -1325,7 +1357,7 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
-                    &c->gcoef};
+                    &c->gcoef, &c->feat32, &c->k32};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);

@@ -363,6 +363,56 @@ hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int6
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ fp32 GEMM form
+// BASELINE configs[3]'s literal formulation ("count-vector fp32 GEMM"): the int8 count
+// rows widened to fp32 for rocblas_sgemm (KMG_ALGO=3), and the fp32 K written out in the
+// call's dtype with the fused normalize_K formula.  Every count product and partial sum
+// is an integer below 2^24 (spectrum k=8 at L=101: K <= 94^2), so the fp32 K is exact.
+__global__ __launch_bounds__(256) void i8_to_f32_kernel(const int8_t *__restrict__ F, int64_t n,
+                                                        float *__restrict__ G) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t * 4 >= n) return;
+  const uint32_t v = ((const uint32_t *)F)[t];
+  ((float4 *)G)[t] = make_float4((float)(int8_t)(v & 0xFF), (float)(int8_t)((v >> 8) & 0xFF),
+                                 (float)(int8_t)((v >> 16) & 0xFF), (float)(int8_t)(v >> 24));
+}
+
+__global__ __launch_bounds__(256) void f32_gram_out_kernel(const float *__restrict__ K32,
+                                                           int64_t n, int64_t row0, OutSpec o) {
+  const int64_t il = blockIdx.y;
+  const int64_t i = row0 + il;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double raw = (double)K32[i * n + j];
+  double v = raw;
+  if (o.normalize && o.diagv[0] != 1.0) v = (i == j) ? 1.0 : raw / (o.dsq[i] * o.dsq[j]);
+  if (o.dtype == KMG_F64)
+    ((double *)o.out)[il * o.ld + j] = v;
+  else if (o.dtype == KMG_F32)
+    ((float *)o.out)[il * o.ld + j] = (float)v;
+  else
+    ((int32_t *)o.out)[il * o.ld + j] = (int32_t)raw;
+}
+
+hipError_t launch_i8_to_f32(const int8_t *F, int64_t elems, float *G, hipStream_t s) {
+  if (elems <= 0) return hipSuccess;
+  if (elems & 3) return hipErrorInvalidValue;
+  const int64_t t = elems / 4;
+  hipLaunchKernelGGL(i8_to_f32_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, s, F, elems,
+                     G);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_gram_out(const float *K32, int64_t n, int64_t row0, int64_t row1,
+                               const OutSpec &o, hipStream_t s) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || n == 0) return hipSuccess;
+  if (rows > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(f32_gram_out_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)rows), dim3(256),
+                     0, s, K32, n, row0, o);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ gappy features
 // Gappy (k, g) with the semantics get_gappy_K intends (kernels.py:420-455, report §3.7;
 // the reference itself raises for every (k, g) but (1, 0)): F[i][b] = 1 if the (k-g)-mer b

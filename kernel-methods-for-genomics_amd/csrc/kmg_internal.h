@@ -318,6 +318,10 @@ hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, i
                                  int window, int dp, const uint32_t *combos, int ncomb, int8_t *F,
                                  double *diagv, double *dsq, hipStream_t s);
 // dense count-vector formulation (kmg_dense.hip): int8 F [rows >= n + 128][dp], K = F F^T
+// KMG_ALGO=3: int8 count rows widened to fp32 for rocblas_sgemm; the fp32 K to the output
+hipError_t launch_i8_to_f32(const int8_t *F, int64_t elems, float *G, hipStream_t s);
+hipError_t launch_f32_gram_out(const float *K32, int64_t n, int64_t row0, int64_t row1,
+                               const OutSpec &o, hipStream_t s);
 hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t n,
                                  int k, int window, int dp, const uint32_t *masks, int nmask,
                                  int8_t *F, double *diagv, double *dsq, hipStream_t s);

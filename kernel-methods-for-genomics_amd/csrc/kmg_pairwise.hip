@@ -874,7 +874,7 @@ __global__ __launch_bounds__(256) void gram_lag_kernel(SeqSpec q, int64_t row0, 
                  uX20 = wave_shr1(pX2);
     if (pv && c >= 0 && c <= ny) {
       const uint32_t yc = c >= 1 ? (uint32_t)ysh[c - 1] & 3u : 0u;
-      double uM = uM0, uX = uX0, uY = uY0, uX2 = uX20;  // row above at column c
+      double uM = uM0, uX = uX0, uX2 = uX20;  // row above at column c (Y: left only)
       double dM = qM, dX = qX, dY = qY;                  // row above at column c - 1
 #pragma unroll
       for (int k = 0; k < R; ++k) {
@@ -913,7 +913,6 @@ __global__ __launch_bounds__(256) void gram_lag_kernel(SeqSpec q, int64_t row0, 
           dY = lY[k];
           uM = M;
           uX = X;
-          uY = Y;
           uX2 = X2;
           lM[k] = M;
           lX[k] = X;

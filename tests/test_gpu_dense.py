@@ -155,3 +155,23 @@ def test_auto_picks_dense_for_run_py_kernels(ctx, tune):
             assert np.array_equal(K, K.T)
     finally:
         ctx.set_timing(False)
+
+
+@pytest.mark.parametrize("k", [4, 6, 8])
+def test_fp32_gemm_spectrum(ctx, tune, k):
+    """KMG_ALGO=3: BASELINE configs[3]'s literal "count-vector fp32 GEMM" (rocblas_sgemm on
+    the widened count rows) gives the exact integer K (every partial sum < 2^24)."""
+    tune(KMG_ALGO=3)
+    codes, lens = E.synthetic(300, 101, seed=500 + k)
+    codes[7] = codes[3]  # a duplicate row: the largest off-diagonal counts
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=k), codes, lens, L.KMG_I32)
+    assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, k))
+    Kd = ctx.gram(P.make(L.KMG_SPECTRUM, k=k), codes, lens, L.KMG_F64)
+    assert np.array_equal(Kd, K.astype(np.float64))
+
+
+def test_fp32_gemm_mismatch_normalised(ctx, tune):
+    tune(KMG_ALGO=3)
+    codes, lens = E.synthetic(200, 101, seed=505)
+    Kn = ctx.gram(P.make(L.KMG_MISMATCH, k=5, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, 5, 1))
