@@ -405,11 +405,14 @@ hipError_t launch_i8_to_f32(const int8_t *F, int64_t elems, float *G, hipStream_
 
 hipError_t launch_f32_gram_out(const float *K32, int64_t n, int64_t row0, int64_t row1,
                                const OutSpec &o, hipStream_t s) {
-  const int64_t rows = row1 - row0;
-  if (rows <= 0 || n == 0) return hipSuccess;
-  if (rows > 65535) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(f32_gram_out_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)rows), dim3(256),
-                     0, s, K32, n, row0, o);
+  for (int64_t r = row0; r < row1; r += 65535) {  // grid.y <= 65535 rows a launch
+    const int64_t rows = std::min<int64_t>(65535, row1 - r);
+    if (n == 0) break;
+    OutSpec os = o;
+    os.out = (char *)o.out + (size_t)(r - row0) * o.ld * (o.dtype == KMG_F64 ? 8 : 4);
+    hipLaunchKernelGGL(f32_gram_out_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)rows),
+                       dim3(256), 0, s, K32, n, r, os);
+  }
   return hipGetLastError();
 }
 
