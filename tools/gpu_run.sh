@@ -35,13 +35,6 @@ for STEP in "$@"; do
         > "$OUT/smoke.txt" 2>&1 || { echo "smoke failed"; tail -20 "$OUT/smoke.txt"; exit 1; }
       tail -n 1 "$OUT/smoke.txt"
       ;;
-    bench*)
-      ARGS=${STEP#bench}
-      ARGS=${ARGS#:}
-      timeout -k 10 600 python3 -u bench.py ${ARGS//:/ } > "$OUT/bench$n.json" 2> "$OUT/bench$n.err" \
-        || { echo "bench failed"; tail -30 "$OUT/bench$n.err"; exit 1; }
-      cut -c1-400 "$OUT/bench$n.json"
-      ;;
     benchprof*)
       # bench.py itself under rocprofv3 --kernel-trace --stats (the roofline's kernel average
       # must agree with the rocprof average of the same command)
@@ -52,6 +45,13 @@ for STEP in "$@"; do
         || { echo "benchprof failed"; tail -30 "$OUT/benchprof$n.err"; exit 1; }
       cut -c1-400 "$OUT/benchprof$n.json"
       grep -m1 gram_sp_kernel "$OUT/bench_trace/run_kernel_stats.csv" | cut -d, -f1-4 | cut -c1-160
+      ;;
+    bench*)
+      ARGS=${STEP#bench}
+      ARGS=${ARGS#:}
+      timeout -k 10 600 python3 -u bench.py ${ARGS//:/ } > "$OUT/bench$n.json" 2> "$OUT/bench$n.err" \
+        || { echo "bench failed"; tail -30 "$OUT/bench$n.err"; exit 1; }
+      cut -c1-400 "$OUT/bench$n.json"
       ;;
     prof:*)
       WL=${STEP#prof:}
