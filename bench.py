@@ -168,7 +168,7 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
 
         t, stages = timed(gather, steps)
         res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages,
-                    "wire_bytes": ctx.blocks_wire()})
+                    "wire_bytes": ctx.blocks_wire(), "plan": ctx.last_plan()})
         if gather:
             tcf, scf = timed(0, steps)
             res["collective_free"] = {"ms_per_step": tcf * 1e3, "pairs_per_s": n * n / tcf,
@@ -627,11 +627,15 @@ def gather_roofline(res, world, esz):
             "frac": recv / t / XGMI_IN_PEAK}
 
 
-def mm_gather_roofline(n, rows, gram_ms, k=9, P=93):
-    """Random-line gather model of the MM(9,1) Gram launch (see the secondary line)."""
+def mm_gather_roofline(n, rows, gram_ms, plan, k=9, P=93):
+    """Random-line gather model of the MM(9,1) Gram launch (see the secondary line), for the
+    chunking the library reports (kmg_last_plan): a row reads every column chunk, or (a
+    square K built by its upper block triangle) (nch + 1) / 2 of them on average."""
     import math
-    if n <= 24000:
-        mean = 16.0 * n * P / 4.0 ** k
+    nch, ch = max(1, plan["nchunks"]), max(8, plan["chunk"])
+    reads = (nch + 1) / 2.0 if plan["triangle"] else float(nch)
+    if plan["formulation"] == "pair_lines":
+        mean = 16.0 * ch * P / 4.0 ** k
         eu = ec = 0.0
         pr = math.exp(-mean)
         for x in range(0, 4000):
@@ -639,12 +643,15 @@ def mm_gather_roofline(n, rows, gram_ms, k=9, P=93):
                 pr *= mean / x
                 eu += pr * math.ceil(x / 64.0)
                 ec += pr * math.ceil((8.0 + x) / 64.0)
-        per_window = 27 * eu + 9 * ec
-        form = "pair lines (27 uniform + 9 correction groups a window, one chunk)"
+        per_chunk = 27 * eu + 9 * ec
+        form = ("pair lines (27 uniform + 9 correction groups a window and chunk; %d chunk(s) "
+                "of %d columns%s; %d-thread workgroups)"
+                % (nch, ch, ", upper block triangle" if plan["triangle"] else "", plan["threads"]))
     else:
-        nch = -(-n // 28572)
-        per_window = 117.0 * nch
-        form = "slot table (117 one-line lists a window and chunk, %d chunks)" % nch
+        per_chunk = 117.0
+        form = ("slot table (117 one-line lists a window and chunk, %d chunks%s)"
+                % (nch, ", upper block triangle" if plan["triangle"] else ""))
+    per_window = per_chunk * reads
     lines = rows * P * per_window
     rate = lines / (gram_ms / 1e3)
     return {"bound": "infinity-cache random 128-B line gathers", "table": form,
@@ -827,18 +834,20 @@ def main():
     if mm:
         mm_rows_launch = mm["rows_this_rank"] / max(1, mm["rounds"])
         mm_bytes = 8.0 * mm_rows_launch * args.mm_n + 52.0 * args.mm_n
+        # Gram launch + (a square K built by its upper block triangle) the mirror of the rest
+        mm_k_ms = mm["stages_ms"]["gram"] + mm["stages_ms"].get("mirror", 0.0)
         line["secondary"] = {
             "workload": "mismatch (k=9,m=1) full-K build, float64 normalised (BASELINE configs[2])",
             "N": args.mm_n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
-            "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"],
-            "hbm_frac_of_gram_kernel": mm_bytes / (mm["stages_ms"]["gram"] / 1e3) / HBM_PEAK,
+            "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"], "plan": mm["plan"],
+            "hbm_frac_of_gram_and_mirror": mm_bytes / (mm_k_ms / 1e3) / HBM_PEAK,
             # the kernel's other bound: random 128-B posting lines from the Infinity Cache.
-            # N <= 24000 runs the pair-lines table (one chunk): per row window 27 uniform
+            # N <= 24000 runs the pair-lines table: per row window and chunk 27 uniform
             # groups of E[ceil(X / 64)] lines and 9 correction groups of E[ceil((8 + X) / 64)],
-            # X ~ Poisson(16 * N * 93 / 4^9) (kmg_pairs.hip); the slot table above that
+            # X ~ Poisson(16 * chunk * 93 / 4^9) (kmg_pairs.hip); the slot table above that
             # (117 one-line lists per window and chunk)
             "gather_roofline": mm_gather_roofline(args.mm_n, mm_rows_launch,
-                                                  mm["stages_ms"]["gram"]),
+                                                  mm["stages_ms"]["gram"], mm["plan"]),
             "spot_check": mm["spot_check"],
         }
         if "collective_free" in mm:

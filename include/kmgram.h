@@ -255,6 +255,14 @@ int kmg_timing_reset(kmg_ctx *ctx);
 int kmg_stage_ms(kmg_ctx *ctx, const char *stage, double *ms);
 int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *count);
 
+/* How the last spectrum / mismatch Gram call on ctx was built (for roofline accounting):
+ * plan[0] formulation (0 dense count-vector GEMM, 1 all-pairs Hamming, 2 posting lists,
+ * 3 mismatch drop-one slot table, 4 drop-two pair table, 5 pair lines; -1 none yet),
+ * plan[1] columns per chunk, plan[2] column chunks, plan[3] 1 when a full square K was built
+ * by its upper block triangle and mirrored, plan[4] Gram workgroup threads (0 where the
+ * formulation has no column chunks).  No reference counterpart (diagnostics). */
+int kmg_last_plan(kmg_ctx *ctx, int32_t plan[5]);
+
 /* RCCL (one rank per process / GPU).  id is an opaque 128-byte ncclUniqueId. */
 int kmg_comm_unique_id(uint8_t id[128]);
 int kmg_comm_init(kmg_ctx *ctx, const uint8_t id[128], int32_t nranks, int32_t rank);

@@ -111,6 +111,8 @@ struct Tuning {
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
   int pl_dbg = 0;           // KMG_PL_DBG: diagnostics only (wrong results): 1 no correction
                             // weights, 2 no bank rotation
+  int pl_threads = 0;       // KMG_PL_THREADS: pair-lines Gram workgroup, 1024 (one a CU), 512
+                            // (two a CU, chunks <= ~11800 columns) or 0 auto (pl_threads())
   int ss_lpp = 0;           // KMG_SS_LPP: SS grouped sweep, lanes a pair (0 auto, 16, 32)
   int la_lpp = 0;           // KMG_LA_LPP: intended-LA grouped sweep, lanes a pair (0 auto, 16, 32)
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
@@ -158,6 +160,8 @@ void read_tuning(Tuning &t) {
   t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.ss_lpp = env_or("KMG_SS_LPP", d.ss_lpp);
+  t.pl_threads = env_or("KMG_PL_THREADS", d.pl_threads);
+  if (t.pl_threads != 512 && t.pl_threads != 1024) t.pl_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
@@ -187,6 +191,7 @@ struct kmg_ctx {
   DevBuf esc, esc_all, esc_cnt;   // uint8 round slabs: escape list, all-gathered lists, counts
   uint32_t esc_cap = 0;           // entries of `esc` in use by the current build (0: none)
   int64_t cur_n = 0;              // columns of the current Gram call
+  int32_t plan[5] = {-1, 0, 0, 0, 0};  // last spectrum / mismatch call (kmg_last_plan)
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
@@ -493,11 +498,28 @@ double tri_cost(int64_t n, int pmax, double lines_per_window_chunk, int64_t nch,
   return lines / 54e9 + mirror / 5.5e12;
 }
 
-int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
+// Workgroup size of the pair-lines Gram kernel.  512 threads (two workgroups a CU: one row's
+// float64 epilogue and LDS adds overlap the other row's line gathers) need chunks of <= ~11800
+// columns: they win where the K is built by its upper block triangle anyway or fits one such
+// chunk; a row range over more columns keeps 1024 (one chunk of up to ~24000 columns).
+// N=20000 normalised square K: Gram 3.97 -> 3.19 ms (2 chunks, triangle), build 4.40 -> 4.09;
+// the same 2 chunks without the triangle 4.21 (profiles/r03t_pl_threads_ab.jsonl).
+int64_t pl_max_chunk(int pmax, int ldp, int threads) {
+  const int64_t lds_words = (threads == 512 ? 80 : 160) * 1024 / 4;  // 512: two workgroups a CU
+  const int64_t m =
+      (lds_words - 66 - pmax - ldp - KMG_PAIRS_MAX - (threads / 64) * KMG_PL_WAVE_WORDS) & ~7LL;
+  return std::min<int64_t>(m, 65536 - 64);
+}
+
+int pl_threads(const Tuning &t, int64_t n, int tri_esz, int pmax, int ldp) {
+  if (t.pl_threads) return t.pl_threads;
+  return (tri_esz > 0 || n <= pl_max_chunk(pmax, ldp, 512)) ? 512 : 1024;
+}
+
+int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads) {
   const double keys = (double)pow4(k - 2);
   const int np = k * (k - 1) / 2;
-  int64_t max_chunk = (160 * 1024 / 4 - 66 - pmax - ldp - KMG_PAIRS_MAX - 16 * KMG_PL_WAVE_WORDS) & ~7LL;
-  max_chunk = std::min<int64_t>(max_chunk, 65536 - 64);
+  int64_t max_chunk = pl_max_chunk(pmax, ldp, threads);
   if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
   if (max_chunk < 8) return 8;
   const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
@@ -926,6 +948,15 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                      g.chunk, (int)dtype_size(dt), c->stream));
         return KMG_OK;
       };
+      // kmg_last_plan: formulation, then chunking / triangle / workgroup once chosen
+      c->plan[0] = (int32_t)path;
+      c->plan[1] = c->plan[2] = c->plan[3] = c->plan[4] = 0;
+      auto note_plan = [&](int threads) {
+        c->plan[1] = g.chunk;
+        c->plan[2] = g.nchunks;
+        c->plan[3] = o.tri;
+        c->plan[4] = threads;
+      };
       if (dt == KMG_I32 && p->normalize)
         return fail(KMG_EINVAL, "normalised output needs a floating dtype");
       const int mm_eff = mm ? std::min(p->m, k) : 0;
@@ -985,6 +1016,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.nkeys = (uint32_t)pow4(k);
         choose_chunks(g, pair_chunk(n, g.pmax, k, c->tune.mm_chunk));
         o.tri = tri_esz > 0 && g.nchunks > 1;
+        note_plan(1024);
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         PairGeom pg{};
         pg.k = k;
@@ -1037,8 +1069,10 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // correction pairs G(r) = {r-1, r} (r >= 1) and {0, k-1} (outer letter k-1)
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz));
+        const int plt = pl_threads(c->tune, n, tri_esz, g.pmax, (int)pkd.ldp);
+        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, plt));
         o.tri = tri_esz > 0 && g.nchunks > 1;
+        note_plan(plt);
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         PairGeom pg{};
         pg.k = k;
@@ -1086,7 +1120,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           return launch_gram_mismatch1_pl(pg, g, pkd, c->pr_summary.as<uint32_t>(),
                                           c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
                                           c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, 4, c->tune.pl_dbg);
+                                          (int)w[2], oq, c->stream, 4, c->tune.pl_dbg, plt);
         }, true));
         return mirror();
       }
@@ -1101,6 +1135,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         choose_chunks(g, slot_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz));
         o.tri = use_slots && tri_esz > 0 && g.nchunks > 1;
       }
+      note_plan(1024);
       KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
       if (use_slots) {
         KMG_TRY(c->slots.ensure((size_t)(g.nbins() >> 2) * KMG_SLOT_BYTES));
@@ -1893,6 +1928,13 @@ int kmg_stage_ms(kmg_ctx *c, const char *stage, double *ms) {
   int32_t n;
   KMG_TRY(stage_sum(c, idx, (size_t)c->last_call_first, &t, &n));
   *ms = n ? t : -1.0;
+  return KMG_OK;
+}
+
+int kmg_last_plan(kmg_ctx *c, int32_t plan[5]) {
+  if (!c || !plan) return fail(KMG_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (int q = 0; q < 5; ++q) plan[q] = c->plan[q];
   return KMG_OK;
 }
 

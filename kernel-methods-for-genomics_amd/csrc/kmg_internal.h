@@ -263,7 +263,8 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
                                     const uint32_t *summary, const uint4 *lines, int64_t nlines,
                                     const uint32_t *xoff, const uint16_t *xent, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int depth = 4, int dbg = 0);
+                                    hipStream_t s, int depth = 4, int dbg = 0,
+                                    int threads = 1024);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -678,7 +678,7 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
                                     const uint32_t *summary, const uint4 *lines, int64_t nlines,
                                     const uint32_t *xoff, const uint16_t *xent, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int depth, int dbg) {
+                                    hipStream_t s, int depth, int dbg, int threads) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
@@ -688,16 +688,21 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
   const int64_t nblk = rowacc_blocks(g, o, row0, rows);
   if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   if (nlines * 128 >= 0xFFFFFFF0LL || nlines >= (1LL << 28)) return hipErrorInvalidValue;
+  // 1024 threads: one workgroup a CU (the int32 accumulator of up to ~24000 columns);
+  // 512: two a CU (chunks up to ~11800 columns), so one row's float64 epilogue and LDS adds
+  // overlap the other row's line gathers (the kernel's 1024-thread bound keeps it at <= 128
+  // VGPRs, which two 8-wave workgroups a CU need)
+  if (threads != 512 && threads != 1024) return hipErrorInvalidValue;
   const size_t lds = (size_t)(((((((g.chunk + 3) >> 2) << 2) + 64 + g.pmax + pk.ldp + KMG_PAIRS_MAX + 1) & ~1) +
-                               16 * KMG_PL_WAVE_WORDS)) * 4;
+                               (threads / 64) * KMG_PL_WAVE_WORDS)) * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk);
   const uint32_t lb = (uint32_t)(nlines * 128);
   switch (pg.k) {
 #define KMG_PL(KK)                                                                                 \
   case KK:                                                                                         \
-    hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(1024), lds, s, pg, g, pk, summary, lines, \
-                       lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                               \
+    hipLaunchKernelGGL((gram_pl_kernel<KK, 4>), grid, dim3(threads), lds, s, pg, g, pk, summary,   \
+                       lines, lb, xoff, xent, row0, rows, w0, w1, w2, o, dbg);                       \
     break;
     KMG_PL(3) KMG_PL(4) KMG_PL(5) KMG_PL(6) KMG_PL(7) KMG_PL(8) KMG_PL(9) KMG_PL(10) KMG_PL(11)
     KMG_PL(12)

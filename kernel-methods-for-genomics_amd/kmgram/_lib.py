@@ -34,7 +34,7 @@ EXPORTS = (
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
-    "kmg_gram_to_host", "kmg_gram_blocks_wire",
+    "kmg_gram_to_host", "kmg_gram_blocks_wire", "kmg_last_plan",
 )
 
 
@@ -101,6 +101,7 @@ def load():
             "kmg_set_timing": ([P, I32], ctypes.c_int),
             "kmg_timing_reset": ([P], ctypes.c_int),
             "kmg_stage_ms": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+            "kmg_last_plan": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
             "kmg_stage_stats": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(I32)], ctypes.c_int),
             "kmg_comm_unique_id": ([P], ctypes.c_int),
@@ -365,6 +366,14 @@ class Context:
         s = ctypes.c_void_p()
         check(self.lib.kmg_stream(self._h, ctypes.byref(s)))
         return s.value
+
+    def last_plan(self):
+        """How the last spectrum / mismatch call was built (include/kmgram.h kmg_last_plan)."""
+        v = (ctypes.c_int32 * 5)()
+        check(self.lib.kmg_last_plan(self._h, v))
+        names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines")
+        return {"formulation": names[v[0]] if 0 <= v[0] < len(names) else None,
+                "chunk": v[1], "nchunks": v[2], "triangle": bool(v[3]), "threads": v[4]}
 
     def stage_ms(self, stage):
         v = ctypes.c_double(0.0)

@@ -149,11 +149,18 @@ def test_spectrum_long_sequences_unpacked(ctx):
     assert np.array_equal(K.astype(np.int64), cref.spectrum(codes, lens, 5))
 
 
-@pytest.mark.parametrize("form", ["0", "3"])
+def _form(tune, form):
+    """"F" -> KMG_MM_FORM=F; "F:T" also KMG_PL_THREADS=T (pair lines, 512: two workgroups a CU,
+    1024: one; unset: by size)"""
+    f, _, t = form.partition(":")
+    tune(KMG_MM_FORM=f, KMG_PL_THREADS=t or None)
+
+
+@pytest.mark.parametrize("form", ["0", "3:1024", "3:512"])
 def test_mismatch_k9_n20000(ctx, tune, form):
     """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows
-    (default formulation and the pair-lines table)."""
-    tune(KMG_MM_FORM=form)
+    (default formulation and the pair-lines table at both workgroup sizes)."""
+    _form(tune, form)
     codes, lens = E.synthetic(20000, 101, seed=3)
     K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
                  L.KMG_F64)
@@ -195,7 +202,7 @@ def test_mismatch_slots_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["2", "3"])
+@pytest.mark.parametrize("form", ["2", "3", "3:1024"])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_mismatch_pairs_k_range(ctx, tune, k, form):
     """Drop-two tables (2: pair table with per-group headers, 3: pair lines) at every
@@ -203,7 +210,7 @@ def test_mismatch_pairs_k_range(ctx, tune, k, form):
     group table)."""
     codes, lens = E.synthetic(500, 101, seed=80 + k)
     ref = cref.mismatch_raw(codes, lens, k, 1)
-    tune(KMG_MM_FORM=form)
+    _form(tune, form)
     for chunk in (("40", "168", "20480") if k <= 9 else ("168", "20480") if k == 10 else ("20480",)):
         tune(KMG_MM_CHUNK=chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
@@ -214,13 +221,14 @@ def test_mismatch_pairs_k_range(ctx, tune, k, form):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
     >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
     entries (wide marker, read from the exact index).  720 poly-A rows put 720 * 93 = 66960
     occurrences in the AAAAAAAAA groups of every copy / pair."""
-    tune(KMG_MM_CHUNK=20480, KMG_MM_FORM=form)
+    tune(KMG_MM_CHUNK=20480)
+    _form(tune, form)
     codes, lens = E.synthetic(760, 101, seed=61)
     codes[:720] = 0
     codes[700] = np.tile([0, 1], 51)[:101]
@@ -233,9 +241,9 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     assert np.array_equal(raw, raw.T)
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024"])
 def test_mismatch_stress_repeats(ctx, tune, form):
-    tune(KMG_MM_FORM=form)
+    _form(tune, form)
     codes, lens = E.synthetic(40, 101, seed=12)
     codes[3] = 0
     codes[4] = np.tile([0, 1], 51)[:101]

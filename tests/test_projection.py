@@ -45,7 +45,9 @@ def test_bench_gather_model_matches_pmc():
     = 142.6 M (profiles/r03l_mm_n20000_pmc.txt)."""
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
     import bench
-    g = bench.mm_gather_roofline(20000, 20000, 3.9)
+    one = {"formulation": "pair_lines", "chunk": 20000, "nchunks": 1, "triangle": False,
+           "threads": 1024}
+    g = bench.mm_gather_roofline(20000, 20000, 3.9, one)
     assert 76.0 < g["lines_per_window"] < 77.0
     assert abs(g["lines_per_launch"] - (107359627.0 + 177767490.7) / 2) / g["lines_per_launch"] < 0.01
     # the weak-scaled headline N keeps every GPU at ~n1^2 pairs

@@ -55,9 +55,11 @@ def main():
             ctx.synchronize()
             wall = (time.perf_counter() - t) / steps * 1e3
             tot, cnt = ctx.stage_stats("gram")
+            mtot, mcnt = ctx.stage_stats("mirror")
             ctx.set_timing(0)
             print(json.dumps({"cfg": cfg, "env": env, "rep": rep, "ms": wall,
-                              "gram_ms": tot / max(1, cnt)}), flush=True)
+                              "gram_ms": tot / max(1, cnt),
+                              "mirror_ms": mtot / mcnt if mcnt else 0.0}), flush=True)
 
 
 if __name__ == "__main__":
