@@ -46,12 +46,15 @@ __host__ __device__ __forceinline__ uint32_t pl_lines(uint32_t n, bool corr) {
   return l > (uint32_t)KMG_PL_MAXNL ? PL_WIDE : l;
 }
 
+// (groups < 2^32: launch_pl_count / launch_pl_pack; nkeys2 = 4^(k-2), so the key is the low
+// 2(k-2) bits and no 64-bit division is needed)
 __device__ __forceinline__ void pl_decode_group(const PairGeom &pg, int64_t g, int &pi, int &p,
                                                 int &q, int &c, uint32_t &key) {
-  key = (uint32_t)(g % pg.nkeys2);
-  const int64_t pc = g / pg.nkeys2;  // pair * nchunks + chunk
-  c = (int)(pc % pg.nchunks);
-  pi = (int)(pc / pg.nchunks);
+  const uint32_t g32 = (uint32_t)g;
+  key = g32 & (pg.nkeys2 - 1u);
+  const uint32_t pc = g32 >> (2 * (pg.k - 2));  // pair * nchunks + chunk
+  c = (int)(pc % (uint32_t)pg.nchunks);
+  pi = (int)(pc / (uint32_t)pg.nchunks);
   p = pg.pq[pi] & 0xF;
   q = (pg.pq[pi] >> 8) & 0xF;
 }
@@ -148,16 +151,21 @@ __device__ __forceinline__ uint32_t pl_dummy(uint32_t dcol, uint32_t bank, uint3
 // bank; the free slots per bank (two per line) are prefix-summed; pass 2 puts a column of
 // rank < 2 nl into its bank's slot and the Poisson tail into the free slots of other banks,
 // in bank order.
+// Two launches: IMGL = PL_SMALL packs the groups of <= PL_SMALL lines (a 4-line image per
+// group: 14 KB of LDS a block, twice the resident blocks of the 14-line image), IMGL =
+// KMG_PL_MAXNL the rest (blocks without such a group leave after one summary load).
 constexpr int PL_PACK_GROUPS = 16;
-constexpr int PL_IMG_WORDS = KMG_PL_MAXNL * 32;
+constexpr int PL_SMALL = 4;
 constexpr int PL_PACK_U = 8;   // entry loads in flight per lane (runs past PL_PACK_R)
 constexpr int PL_PACK_R = 12;  // entries of a run kept in registers across both passes
+template <int IMGL>
 __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
                                                       const uint16_t *__restrict__ xent,
                                                       const uint32_t *__restrict__ rbase,
                                                       uint32_t *__restrict__ summary,
                                                       uint4 *__restrict__ lines) {
-  __shared__ __align__(16) uint32_t img[PL_PACK_GROUPS][PL_IMG_WORDS];
+  constexpr bool BIG = IMGL > PL_SMALL;
+  __shared__ __align__(16) uint32_t img[PL_PACK_GROUPS][IMGL * 32];
   __shared__ uint32_t hist[PL_PACK_GROUPS][32];   // columns per bank (pass 1)
   __shared__ uint32_t rank[PL_PACK_GROUPS][32];   // running rank per bank (pass 2)
   __shared__ uint32_t freeb[PL_PACK_GROUPS][33];  // exclusive prefix of the free slots per bank
@@ -165,8 +173,18 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   const int lg = threadIdx.x >> 4, b = threadIdx.x & 15;
   const int64_t g = (int64_t)blockIdx.x * PL_PACK_GROUPS + lg;
   const bool live = g < pg.ngroups();
-  // line 0 is the dummy line (read for empty ring entries): group bases start at 1
-  if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5] + 1u;
+  if constexpr (BIG) {  // this block's groups of more than PL_SMALL lines (summary nibbles)
+    bool big = false;
+    if (live) {
+      const uint32_t r = (uint32_t)(g & 31);
+      const uint32_t wd = summary[(g >> 5) * 8 + 1 + (r >> 3)];
+      big = ((wd >> (4 * (r & 7))) & 15u) > (uint32_t)PL_SMALL;
+    }
+    if (!__syncthreads_or(big)) return;
+  } else {
+    // line 0 is the dummy line (read for empty ring entries): group bases start at 1
+    if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5] + 1u;
+  }
   const uint32_t dcol = (uint32_t)(((pg.chunk + 3) >> 2) << 2);
   uint32_t s0 = 0, cnt = 0;
   bool corr = false;
@@ -190,7 +208,7 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   }
   const uint32_t n = __shfl(end, 15, 16);
   const uint32_t nl = live ? pl_lines(n, corr) : 0u;
-  const bool pack = live && nl != PL_WIDE && n > 0;
+  const bool pack = live && nl != PL_WIDE && n > 0 && (BIG ? nl > (uint32_t)PL_SMALL : nl <= (uint32_t)PL_SMALL);
   // the run's first PL_PACK_R entries, issued before the LDS set-up and the summary loads
   uint32_t colr[PL_PACK_R];
 #pragma unroll
@@ -216,7 +234,7 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
     for (int q = 0; q < 4; ++q)
       base += nib_sum(wd[q] & (q < wsel ? 0xFFFFFFFFu : (q == wsel ? ((1u << sh) - 1u) : 0u)));
   }
-  if (blockIdx.x == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
+  if (!BIG && blockIdx.x == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
     uint32_t w[4];
     for (int q = 0; q < 4; ++q) {
       const uint32_t bk = pl_bank(4u * threadIdx.x + q);
@@ -307,8 +325,10 @@ hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16
   // launch wrapped and packed a fraction of the table)
   if (blocks * 256 >= (1LL << 32)) return hipErrorInvalidValue;
   if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
-  hipLaunchKernelGGL(pl_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent, rbase,
-                     summary, lines);
+  hipLaunchKernelGGL(pl_pack_kernel<PL_SMALL>, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff,
+                     xent, rbase, summary, lines);
+  hipLaunchKernelGGL(pl_pack_kernel<KMG_PL_MAXNL>, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff,
+                     xent, rbase, summary, lines);
   return hipGetLastError();
 }
 
