@@ -612,26 +612,24 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
       add_piece((dbg & 2) ? xl : rot4(xl, rs1, rs2), w2);
       return;
     }
-    const uint4 x = rot4(((e.x & RE_HDR) && j8 == 0) ? dpiece : xl, rs1, rs2);
-    // the lane adds halfwords hb .. hb + 7 of its line, instruction v halfword hb + ((v + 2
-    // slot) & 7): the halfword ranges of the row z_outer = u_outer and of the exact bin
-    // become 8-bit masks over the lane's halfwords, rotated into instruction order once;
-    // each add's weight is w2 + cc [in the row] + (wx - cc) [in the exact bin]
-    const uint32_t rlo = e.y & 0xFFu, rhi = (e.y >> 8) & 0xFFu;
-    const uint32_t elo = (e.y >> 16) & 0xFFu, ehi = e.y >> 24;
-    const int dwx = ((e.x & RE_DESIG) ? h0 : 0) - cc;
-    const uint32_t hb = 8u * (uint32_t)j8, sh = 2u * (uint32_t)slot;
+    // correction lines are not bank-sorted: no rotation.  The lane adds halfwords hb ..
+    // hb + 7 of its line in order; the halfword ranges of the row z_outer = u_outer and of
+    // the exact bin become 8-bit masks over them; each add's weight is w2, w2 + cc [in the
+    // row] or w2 (+ h0 in G(1)) [in the exact bin, inside the row: cc is not applied there]
+    const uint4 x = ((e.x & RE_HDR) && j8 == 0) ? dpiece : xl;
+    const uint32_t hb = 8u * (uint32_t)j8;
     auto lane_mask = [&](uint32_t lo, uint32_t hi) -> uint32_t {
       const uint32_t a = min(max(lo, hb), hb + 8u) - hb, b = min(max(hi, hb), hb + 8u) - hb;
-      const uint32_t m = ((1u << b) - 1u) & ~((1u << a) - 1u);
-      return ((m >> sh) | (m << (8u - sh))) & 0xFFu;
+      return ((1u << b) - 1u) & ~((1u << a) - 1u);
     };
-    const uint32_t mr = (e.x & RE_CORR) ? lane_mask(rlo, rhi) : 0u;
-    const uint32_t me = (e.x & RE_CORR) ? lane_mask(elo, ehi) : 0u;
+    const bool ce = (e.x & RE_CORR) != 0;
+    const uint32_t mr = ce ? lane_mask(e.y & 0xFFu, (e.y >> 8) & 0xFFu) : 0u;
+    const uint32_t me = ce ? lane_mask((e.y >> 16) & 0xFFu, e.y >> 24) : 0u;
+    const int wr = w2 + cc, we = w2 + ((e.x & RE_DESIG) ? h0 : 0);
     const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      const int w = w2 + cc * (int)((mr >> v) & 1u) + dwx * (int)((me >> v) & 1u);
+      const int w = ((me >> v) & 1u) ? we : (((mr >> v) & 1u) ? wr : w2);
       lds_add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w);
     }
   };
