@@ -1127,10 +1127,10 @@ hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, in
 // its rows, 16 bytes per lane each way.
 template <typename T>
 __global__ __launch_bounds__(256) void mirror_chunks_kernel(T *__restrict__ K, int64_t ld,
-                                                            int64_t n, int chunk) {
+                                                            int64_t n, int chunk, int64_t ti0) {
   constexpr int V = 16 / (int)sizeof(T), CPR = 64 / V;
   __shared__ T tile[64][64 + 1];  // [j - j0][i - i0]
-  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
+  const int64_t i0 = (ti0 + (int64_t)blockIdx.y) * 64, j0 = (int64_t)blockIdx.x * 64;
   const int64_t imax = min(n - 1, i0 + 63);
   if (j0 >= (imax / chunk) * chunk) return;  // no target entry in this tile
   for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
@@ -1169,17 +1169,20 @@ __global__ __launch_bounds__(256) void mirror_chunks_kernel(T *__restrict__ K, i
 hipError_t launch_mirror_chunks(void *K, int64_t ld, int64_t n, int chunk, int esz,
                                 hipStream_t s) {
   if (n <= chunk) return hipSuccess;
-  const int64_t t = (n + 63) / 64;
-  if (t > 65535) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)t, (unsigned)t);
-  if (esz == 8)
-    hipLaunchKernelGGL(mirror_chunks_kernel<uint64_t>, grid, dim3(256), 0, s, (uint64_t *)K, ld, n,
-                       chunk);
-  else if (esz == 4)
-    hipLaunchKernelGGL(mirror_chunks_kernel<uint32_t>, grid, dim3(256), 0, s, (uint32_t *)K, ld, n,
-                       chunk);
-  else
-    return hipErrorInvalidValue;
+  if (esz != 8 && esz != 4) return hipErrorInvalidValue;
+  if ((n + 63) / 64 > 65535) return hipErrorInvalidValue;
+  // one launch per row chunk c >= 1: its 64-row tiles x the column tiles left of c * chunk
+  // (a square grid over all tile pairs would start ~57 % of its blocks only to leave)
+  for (int64_t c0 = chunk; c0 < n; c0 += chunk) {
+    const int64_t ti0 = c0 / 64, ti1 = (std::min(n, c0 + chunk) + 63) / 64;
+    const dim3 grid((unsigned)((c0 + 63) / 64), (unsigned)(ti1 - ti0));
+    if (esz == 8)
+      hipLaunchKernelGGL(mirror_chunks_kernel<uint64_t>, grid, dim3(256), 0, s, (uint64_t *)K, ld,
+                         n, chunk, ti0);
+    else
+      hipLaunchKernelGGL(mirror_chunks_kernel<uint32_t>, grid, dim3(256), 0, s, (uint32_t *)K, ld,
+                         n, chunk, ti0);
+  }
   return hipGetLastError();
 }
 

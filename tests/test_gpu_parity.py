@@ -164,7 +164,13 @@ def test_mismatch_k9_n20000(ctx, tune, form):
     codes, lens = E.synthetic(20000, 101, seed=3)
     K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
                  L.KMG_F64)
-    rows = [0, 1, 7777, 19999]
+    plan = ctx.last_plan()
+    assert plan["formulation"] == "pair_lines"
+    if form in ("0", "3:512"):  # 512 threads: 2 chunks of 10000, upper block triangle + mirror
+        assert (plan["threads"], plan["nchunks"], plan["chunk"], plan["triangle"]) == (512, 2, 10000, True)
+    else:                       # 1024 threads: one chunk, no mirror
+        assert (plan["threads"], plan["nchunks"], plan["triangle"]) == (1024, 1, False)
+    rows = [0, 1, 7777, 10000, 19999]
     for r in rows:
         ref = cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0]
         assert np.array_equal(K[r], ref), r
