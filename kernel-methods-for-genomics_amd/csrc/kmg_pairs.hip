@@ -429,6 +429,11 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
   const uint32_t pair_stride = (uint32_t)g.nchunks * NK2;
   const int cc = w1 - (K - 1) * w2;  // Hamming 1, on top of the w2 of its K-1 groups
   const int h0 = w0 - NP * w2;       // Hamming 0, on top of the w2 of all NP groups
+  // correction weights as bytes (launch_gram_mismatch1_pl checks they fit int8): class 0
+  // (outside the row) w2, 1 (row) w2 + cc, 2 / 3 (exact bin) w2 (+ h0 in G(1))
+  auto b8 = [](int v) { return (uint32_t)v & 0xFFu; };
+  const uint32_t lut_n = b8(w2) | (b8(w2 + cc) << 8) | (b8(w2) << 16) | (b8(w2) << 24);
+  const uint32_t lut_d = b8(w2) | (b8(w2 + cc) << 8) | (b8(w2 + h0) << 16) | (b8(w2 + h0) << 24);
   const int g8 = lane >> 3, j8 = lane & 7;
   const uint32_t dcol = (uint32_t)accw;  // first dummy column
 
@@ -600,9 +605,13 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
   const bool rs1 = (slot & 1) != 0, rs2 = (slot & 2) != 0;
   uint32_t sink = 0;
   // the header piece of a correction group's first line (lane j8 = 0): its 8 halfwords
-  // become the dummy columns dcol .. dcol + 7, so every add of a step takes the same path
-  const uint4 dpiece = make_uint4(dcol | ((dcol + 1u) << 16), (dcol + 2u) | ((dcol + 3u) << 16),
-                                  (dcol + 4u) | ((dcol + 5u) << 16), (dcol + 6u) | ((dcol + 7u) << 16));
+  // become dummy columns, so every add of a step takes the same path.  Halfword v of lane
+  // group g8 goes to dummy column dcol + 8 v + g8: the up to 8 header lanes of one add
+  // instruction hit 8 different words in 8 banks (one shared set dcol .. dcol + 7 made them
+  // same-address atomics, serialised)
+  const uint32_t dg = dcol + (uint32_t)g8;
+  const uint4 dpiece = make_uint4(dg | ((dg + 8u) << 16), (dg + 16u) | ((dg + 24u) << 16),
+                                  (dg + 32u) | ((dg + 40u) << 16), (dg + 48u) | ((dg + 56u) << 16));
   auto consume = [&](const uint4 &xl, const uint2 &e) {
     if (dbg & 4) {  // diagnostics: no LDS adds
       sink += xl.x ^ xl.y ^ xl.z ^ xl.w;
@@ -622,14 +631,21 @@ __global__ __launch_bounds__(1024) void gram_pl_kernel(PairGeom pg, IndexGeom g,
       const uint32_t a = min(max(lo, hb), hb + 8u) - hb, b = min(max(hi, hb), hb + 8u) - hb;
       return ((1u << b) - 1u) & ~((1u << a) - 1u);
     };
-    const bool ce = (e.x & RE_CORR) != 0;
-    const uint32_t mr = ce ? lane_mask(e.y & 0xFFu, (e.y >> 8) & 0xFFu) : 0u;
-    const uint32_t me = ce ? lane_mask((e.y >> 16) & 0xFFu, e.y >> 24) : 0u;
-    const int wr = w2 + cc, we = w2 + ((e.x & RE_DESIG) ? h0 : 0);
+    // (masks computed for every lane and cleared off correction entries: no exec branches.
+    // Weights through a byte table: halfword v's class r_v + 2 e_v (the exact bin lies
+    // inside the row) selects byte w2 / w2 + cc / w2 [+ h0] of `lut`, four at a time with
+    // one v_perm_b32, each then sign-extended: 2.5 VALU a weight instead of 5)
+    const uint32_t cm = (e.x & RE_CORR) ? 0xFFu : 0u;
+    const uint32_t mr = lane_mask(e.y & 0xFFu, (e.y >> 8) & 0xFFu) & cm;
+    const uint32_t me = lane_mask((e.y >> 16) & 0xFFu, e.y >> 24) & cm;
+    const uint32_t lut = (e.x & RE_DESIG) ? lut_d : lut_n;
+    auto spread = [](uint32_t m4) { return (m4 * 0x00204081u) & 0x01010101u; };  // bit i -> byte i
+    const uint32_t wlo = __builtin_amdgcn_perm(lut, lut, spread(mr & 15u) + 2u * spread(me & 15u));
+    const uint32_t whi = __builtin_amdgcn_perm(lut, lut, spread(mr >> 4) + 2u * spread(me >> 4));
     const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
-      const int w = ((me >> v) & 1u) ? we : (((mr >> v) & 1u) ? wr : w2);
+      const int w = __builtin_amdgcn_sbfe((int)(v < 4 ? wlo : whi), 8 * (v & 3), 8);
       lds_add((v & 1) ? col_addr_sdwa<1>(wd[v >> 1]) : col_addr_sdwa<0>(wd[v >> 1]), w);
     }
   };
@@ -700,6 +716,11 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (pg.k < 3 || pg.k > 12 || pg.k != g.k) return hipErrorNotSupported;
+  {  // the correction weights travel as int8 (gram_pl_kernel's byte table)
+    const int np = pg.k * (pg.k - 1) / 2, cc = w1 - (pg.k - 1) * w2, h0 = w0 - np * w2;
+    for (int v : {w2, w2 + cc, w2 + h0})
+      if (v < -128 || v > 127) return hipErrorNotSupported;
+  }
   // ring depth 4 only: one batch enters at most 64 (PL_QU + PL_QC) + 14 = 462 ring entries
   // on top of < 8 (depth + 1) unread ones, and the ring holds 512
   (void)depth;
