@@ -193,6 +193,7 @@ struct kmg_ctx {
   int64_t cur_n = 0;              // columns of the current Gram call
   int32_t plan[5] = {-1, 0, 0, 0, 0};  // last spectrum / mismatch call (kmg_last_plan)
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
+  DevBuf pr_big;                  // pair lines: blocks with groups past the small image
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -1096,6 +1097,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
         KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nrec)));
         KMG_TRY(c->pr_lines.ensure((size_t)nlines * 128));
+        KMG_TRY(c->pr_big.ensure(sizeof(uint32_t) * (size_t)(pl_pack_blocks(pg) + 1)));
         {
           StageTimer t(c, ST_SLOTS);
           KMG_HIP(launch_pl_count(pg, c->off.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
@@ -1105,7 +1107,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                               c->stream));
           KMG_HIP(launch_pl_pack(pg, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                  c->pr_rbase.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
-                                 c->pr_lines.as<uint4>(), c->stream));
+                                 c->pr_lines.as<uint4>(), c->pr_big.as<uint32_t>(), c->stream));
         }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));
@@ -1388,7 +1390,7 @@ int kmg_destroy(kmg_ctx *c) {
   DevBuf *bufs[] = {&c->kmers, &c->partials, &c->tmp, &c->esc, &c->esc_all, &c->esc_cnt,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
-                    &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
+                    &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines, &c->pr_big,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,

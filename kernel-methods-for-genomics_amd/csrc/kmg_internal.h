@@ -174,7 +174,10 @@ inline int64_t pair_lines_bound(const PairGeom &pg, int64_t occurrences) {
 hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
                            uint32_t *rtot, hipStream_t s);
 hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
-                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, hipStream_t s);
+                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, uint32_t *big,
+                          hipStream_t s);
+// pl_pack's list of blocks holding groups of more than 4 lines: 1 + this many words
+inline int64_t pl_pack_blocks(const PairGeom &pg) { return (pg.ngroups() + 15) / 16; }
 // upper bound of the line count of the pair-lines table
 inline int64_t pl_lines_bound(const PairGeom &pg, int64_t occurrences) {
   const int64_t entries = (int64_t)pg.npairs * occurrences;

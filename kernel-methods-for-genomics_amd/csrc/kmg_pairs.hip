@@ -152,18 +152,21 @@ __device__ __forceinline__ uint32_t pl_dummy(uint32_t dcol, uint32_t bank, uint3
 // rank < 2 nl into its bank's slot and the Poisson tail into the free slots of other banks,
 // in bank order.
 // Two launches: IMGL = PL_SMALL packs the groups of <= PL_SMALL lines (a 4-line image per
-// group: 14 KB of LDS a block, twice the resident blocks of the 14-line image), IMGL =
-// KMG_PL_MAXNL the rest (blocks without such a group leave after one summary load).
+// group: 14 KB of LDS a block, twice the resident blocks of the 14-line image) and lists
+// the blocks holding a larger group in `big` (count, block indices); IMGL = KMG_PL_MAXNL
+// packs those from that list with a small grid (a full grid of blocks that each only
+// found nothing to do cost 52 us at N=20000).
 constexpr int PL_PACK_GROUPS = 16;
 constexpr int PL_SMALL = 4;
 constexpr int PL_PACK_U = 8;   // entry loads in flight per lane (runs past PL_PACK_R)
 constexpr int PL_PACK_R = 12;  // entries of a run kept in registers across both passes
 template <int IMGL>
-__global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
-                                                      const uint16_t *__restrict__ xent,
-                                                      const uint32_t *__restrict__ rbase,
-                                                      uint32_t *__restrict__ summary,
-                                                      uint4 *__restrict__ lines) {
+__device__ __forceinline__ void pl_pack_body(int64_t vb, const PairGeom &pg,
+                                             const uint32_t *__restrict__ xoff,
+                                             const uint16_t *__restrict__ xent,
+                                             const uint32_t *__restrict__ rbase,
+                                             uint32_t *__restrict__ summary,
+                                             uint4 *__restrict__ lines, uint32_t *__restrict__ big) {
   constexpr bool BIG = IMGL > PL_SMALL;
   __shared__ __align__(16) uint32_t img[PL_PACK_GROUPS][IMGL * 32];
   __shared__ uint32_t hist[PL_PACK_GROUPS][32];   // columns per bank (pass 1)
@@ -171,17 +174,9 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   __shared__ uint32_t freeb[PL_PACK_GROUPS][33];  // exclusive prefix of the free slots per bank
   __shared__ uint32_t novf[PL_PACK_GROUPS];       // columns placed into other banks' slots
   const int lg = threadIdx.x >> 4, b = threadIdx.x & 15;
-  const int64_t g = (int64_t)blockIdx.x * PL_PACK_GROUPS + lg;
+  const int64_t g = vb * PL_PACK_GROUPS + lg;
   const bool live = g < pg.ngroups();
-  if constexpr (BIG) {  // this block's groups of more than PL_SMALL lines (summary nibbles)
-    bool big = false;
-    if (live) {
-      const uint32_t r = (uint32_t)(g & 31);
-      const uint32_t wd = summary[(g >> 5) * 8 + 1 + (r >> 3)];
-      big = ((wd >> (4 * (r & 7))) & 15u) > (uint32_t)PL_SMALL;
-    }
-    if (!__syncthreads_or(big)) return;
-  } else {
+  if constexpr (!BIG) {
     // line 0 is the dummy line (read for empty ring entries): group bases start at 1
     if (live && (g & 31) == 0 && b == 0) summary[(g >> 5) * 8] = rbase[g >> 5] + 1u;
   }
@@ -208,7 +203,11 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
   }
   const uint32_t n = __shfl(end, 15, 16);
   const uint32_t nl = live ? pl_lines(n, corr) : 0u;
-  const bool pack = live && nl != PL_WIDE && n > 0 && (BIG ? nl > (uint32_t)PL_SMALL : nl <= (uint32_t)PL_SMALL);
+  const bool large = live && nl != PL_WIDE && n > 0 && nl > (uint32_t)PL_SMALL;
+  const bool pack = live && nl != PL_WIDE && n > 0 && (BIG ? large : !large);
+  if constexpr (!BIG) {  // list this block for the second launch
+    if (__syncthreads_or(large) && threadIdx.x == 0) big[1 + atomicAdd(big, 1u)] = (uint32_t)vb;
+  }
   // the run's first PL_PACK_R entries, issued before the LDS set-up and the summary loads
   uint32_t colr[PL_PACK_R];
 #pragma unroll
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
     for (int q = 0; q < 4; ++q)
       base += nib_sum(wd[q] & (q < wsel ? 0xFFFFFFFFu : (q == wsel ? ((1u << sh) - 1u) : 0u)));
   }
-  if (!BIG && blockIdx.x == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
+  if (!BIG && vb == 0 && threadIdx.x < 8) {  // the dummy line, bank-sorted like the others
     uint32_t w[4];
     for (int q = 0; q < 4; ++q) {
       const uint32_t bk = pl_bank(4u * threadIdx.x + q);
@@ -307,6 +306,27 @@ __global__ __launch_bounds__(256) void pl_pack_kernel(PairGeom pg, const uint32_
     for (uint32_t w = b; w < nl * 8; w += 16) lines[(size_t)base * 8 + w] = ((const uint4 *)img[lg])[w];
 }
 
+__global__ __launch_bounds__(256) void pl_pack_small_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
+                                                            const uint16_t *__restrict__ xent,
+                                                            const uint32_t *__restrict__ rbase,
+                                                            uint32_t *__restrict__ summary,
+                                                            uint4 *__restrict__ lines,
+                                                            uint32_t *__restrict__ big) {
+  pl_pack_body<PL_SMALL>(blockIdx.x, pg, xoff, xent, rbase, summary, lines, big);
+}
+__global__ __launch_bounds__(256) void pl_pack_big_kernel(PairGeom pg, const uint32_t *__restrict__ xoff,
+                                                          const uint16_t *__restrict__ xent,
+                                                          const uint32_t *__restrict__ rbase,
+                                                          uint32_t *__restrict__ summary,
+                                                          uint4 *__restrict__ lines,
+                                                          uint32_t *__restrict__ big) {
+  const uint32_t nb = big[0];
+  for (uint32_t t = blockIdx.x; t < nb; t += gridDim.x) {
+    pl_pack_body<KMG_PL_MAXNL>(big[1 + t], pg, xoff, xent, rbase, summary, lines, big);
+    __syncthreads();  // the next block's image reuses the LDS
+  }
+}
+
 hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
                            uint32_t *rtot, hipStream_t s) {
   const int64_t threads = pg.nrec() * 32;
@@ -318,17 +338,21 @@ hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *s
 }
 
 hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
-                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, hipStream_t s) {
+                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, uint32_t *big,
+                          hipStream_t s) {
   const int64_t blocks = (pg.ngroups() + PL_PACK_GROUPS - 1) / PL_PACK_GROUPS;
   if (blocks == 0) return hipSuccess;
   // grid x block < 2^32 work-items (k = 11 at 63 chunks of 8 columns is 14.5 G: the
   // launch wrapped and packed a fraction of the table)
   if (blocks * 256 >= (1LL << 32)) return hipErrorInvalidValue;
   if ((((int64_t)pg.chunk + 3) >> 2 << 2) + 64 > 65536) return hipErrorInvalidValue;  // dummies
-  hipLaunchKernelGGL(pl_pack_kernel<PL_SMALL>, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff,
-                     xent, rbase, summary, lines);
-  hipLaunchKernelGGL(pl_pack_kernel<KMG_PL_MAXNL>, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff,
-                     xent, rbase, summary, lines);
+  // big: [0] count, [1 + t] block indices (pl_pack_blocks(pg) + 1 words)
+  hipError_t e = hipMemsetAsync(big, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pl_pack_small_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pg, xoff, xent,
+                     rbase, summary, lines, big);
+  hipLaunchKernelGGL(pl_pack_big_kernel, dim3((unsigned)std::min<int64_t>(blocks, 1024)), dim3(256),
+                     0, s, pg, xoff, xent, rbase, summary, lines, big);
   return hipGetLastError();
 }
 
