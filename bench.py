@@ -658,8 +658,9 @@ def mm_gather_roofline(n, rows, gram_ms, plan, k=9, P=93):
             "lines_per_window": per_window, "lines_per_launch": lines,
             "achieved_Glines_per_s": rate / 1e9, "ceiling_Glines_per_s": GATHER_CEILING / 1e9,
             "frac": rate / GATHER_CEILING,
-            "source": "profiles/r02_mall_gather.jsonl (78.6 MB table, 128-B lines); "
-                      "PMC of the same launch profiles/r03l_mm_n20000_pmc.txt"}
+            "source": "profiles/r02_mall_gather.jsonl (78.6 MB table, 128-B lines); PMC of the "
+                      "one-chunk launch profiles/r03l_mm_n20000_pmc.txt, of the two-chunk "
+                      "triangle launch profiles/r03af_mm_n20000_pmc.txt"}
 
 
 def _chunked(n, max_chunk):
