@@ -10,13 +10,13 @@ on the configs[3] "count-vector GEMM" wording).  A "step" is one full-K build (S
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`): one
 process per GPU.  The rows of K are independent, so the headline shards them
-with no data-path collective and scales weakly: N = 100000 sqrt(G), every GPU builds the
-replicated index and computes its block-cyclic rows x all N columns (1e10 Gram pairs, the
-one-GPU workload), packed in its own buffer; `value` = N^2 / max-over-ranks step time.
-The north-star's final RCCL all-gather is measured beside it at the fixed N=100000
-(`assembled`: upper-triangle uint8 round slabs all-gathered in place over RCCL/xGMI on a
-second stream while the next round is computed, every GPU unpacking / mirroring them
-into the whole K; `collective_free` is the same fixed-N build without the gather).
+with no data-path collective and scales STRONGLY at the north-star's named N = 100000:
+every GPU builds the replicated index and computes its 1/G share of the rows x all N
+columns, packed in its own buffer; `value` = N^2 / max-over-ranks step time.  The
+north-star's final RCCL all-gather is measured beside it at the same N (`assembled`:
+upper-triangle uint8 round slabs all-gathered in place over RCCL/xGMI on a second stream
+while the next round is computed, every GPU unpacking / mirroring them into the whole K),
+and the weak-scaled build (N = 100000 sqrt(G), every GPU 1e10 pairs) as `weak_scaled`.
 
 Also reported: the mismatch (k=9, m=1) Gram at N=20000 (BASELINE configs[2], float64
 normalised), per-stage device times from HIP events, the HBM roofline of the dominant
@@ -246,6 +246,50 @@ def _rows_product(ab):
     return time.perf_counter() - t0
 
 
+def host_cpus():
+    """The host cores this process may use: os.cpu_count() (the whole machine), the
+    scheduler affinity mask and the cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us), plus the CPU model.  workers = the smallest of them (a
+    GPU box's CPU share is a cgroup quota below the machine's core count: more processes
+    than the quota only time-slice); KMG_BENCH_CPU_WORKERS overrides."""
+    info = {"host_cores": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    info["cgroup_cpu_quota"] = quota
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    info["cpu_model"] = model
+    w = info["affinity_cpus"] or 1
+    if quota:
+        w = min(w, max(1, int(quota)))
+    env = os.environ.get("KMG_BENCH_CPU_WORKERS")
+    info["workers"] = int(env) if env else w
+    info["workers_rule"] = ("KMG_BENCH_CPU_WORKERS" if env else
+                            "min(affinity CPUs, cgroup CPU quota)" if quota else "affinity CPUs")
+    return info
+
+
 def cpu_baseline(name, n, budget_s, seed, workers=None):
     """The strongest CPU restatement of the reference we have, on this box's host cores:
     scipy-sparse Phi Phi^T (oracle/cpu_ref.py spectrum_phi / mismatch_phi = the reference's
@@ -257,7 +301,8 @@ def cpu_baseline(name, n, budget_s, seed, workers=None):
     import multiprocessing as mp
     import cpu_ref
     global _F, _FT
-    workers = workers or min(16, os.cpu_count() or 1)
+    hw = host_cpus()
+    workers = workers or hw["workers"]
     codes, lens = E.synthetic(n, 101, seed=seed)  # the timed workload's own input
     t0 = time.perf_counter()
     _F = (cpu_ref.spectrum_phi(codes, lens, 8) if name == "spectrum_k8"
@@ -275,10 +320,16 @@ def cpu_baseline(name, n, budget_s, seed, workers=None):
     # all workers: each takes a block sized for ~budget/2 of wall time
     per = max(1, min(n // workers, int(rate1 * budget_s / 2)))
     blocks = [(w * per, (w + 1) * per) for w in range(workers) if (w + 1) * per <= n]
+    # forked before this process makes any HIP call (main() runs the CPU baseline first),
+    # and ended by close() + join(): the workers exit on their own, nobody is SIGTERMed
     ctx_mp = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx_mp.Pool(len(blocks)) as pool:
+    pool = ctx_mp.Pool(len(blocks))
+    try:
         pool.map(_rows_product, blocks)
+    finally:
+        pool.close()
+        pool.join()
     t_rows = time.perf_counter() - t0
     rows = per * len(blocks)
     t_job = t_phi + (n / rows) * t_rows
@@ -286,6 +337,9 @@ def cpu_baseline(name, n, budget_s, seed, workers=None):
     _F = _FT = None
     label = "spectrum_phi" if name == "spectrum_k8" else "mismatch_phi"
     return {"value": n * n / t_job, "unit": "Gram pairs/s", "cores": len(blocks), "kind": "port",
+            "host_cores": hw["host_cores"], "cpu_model": hw["cpu_model"],
+            "affinity_cpus": hw["affinity_cpus"], "cgroup_cpu_quota": hw["cgroup_cpu_quota"],
+            "workers": len(blocks), "workers_rule": hw["workers_rule"],
             "sample": f"scipy-sparse Phi Phi^T (oracle/cpu_ref.py {label}): Phi of all {n} "
                       f"sequences {t_phi:.2f} s (1 process) + rows 0..{rows} x {n} over "
                       f"{len(blocks)} forked processes in {t_rows:.2f} s wall, whole job "
@@ -680,14 +734,12 @@ def projection(sp, n, extra):
     out = {"model": "kmgram.shard.scaling_projection (DESIGN.md §5); not measured on >1 GPU",
            "assumptions": {"xgmi_link_GBps": XGMI_IN_PEAK / 7 / 1e9, "link_eff": 1.0,
                            "fill_GBps": fill, "wire_bytes": 1}}
-    # the G > 1 headline (weak: N = n sqrt(G), each GPU its n^2 pairs, no collective): the
-    # Gram per GPU is unchanged, the replicated index grows with N (sqrt(G) x)
-    t1 = sp["ms_per_step"]
-    out["headline_weak_collective_free"] = {
-        str(g): {"N": weak_scaled_n(n, g),
-                 "ms_model": t1 + t_index * (g ** 0.5 - 1.0),
-                 "value_model": weak_scaled_n(n, g) ** 2 / ((t1 + t_index * (g ** 0.5 - 1.0)) / 1e3),
-                 "efficiency_model": t1 / (t1 + t_index * (g ** 0.5 - 1.0))}
+    # the G > 1 headline (strong, N = n, each GPU its 1/G of the rows, no collective): the
+    # replicated index plus 1/G of the Gram (kmgram.shard.scaling_projection collective_free)
+    out["headline_strong_collective_free"] = {
+        str(g): {"N": n, "ms_model": t_index + st["gram"] / g,
+                 "value_model": n * n / ((t_index + st["gram"] / g) / 1e3),
+                 "speedup_model": sp["ms_per_step"] / (t_index + st["gram"] / g)}
         for g in (2, 4, 8)}
     out["config4_spectrum_k8_n%d" % n] = {
         str(g): v for g, v in scaling_projection(
@@ -738,6 +790,16 @@ def main():
     dist = Dist()
     if dist.world != args.gpus and dist.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
+    n1 = args.n
+    sp_seed = 4 if n1 == 100000 else 2
+    # the CPU baseline runs FIRST, before this process makes any HIP call: its workers are
+    # forked, and a fork of a process holding a HIP context is unsafe (round 3's r03s
+    # benchprof saw the forked workers crash in rocprofv3's signal handler)
+    cpu = {}
+    if dist.world == 1 and not args.no_cpu:
+        cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n1, args.cpu_budget, sp_seed)
+        if not args.no_mismatch:
+            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", args.mm_n, args.cpu_budget / 2, 3)
     dev = os.environ.get("KMG_BENCH_DEVICE")
     ctx = L.Context(int(dev) if dev is not None else dist.local)
     # KMG_BENCH_NO_RCCL=1: the collective-free lines only (a rehearsal of the G > 1 headline
@@ -746,21 +808,22 @@ def main():
     if rccl:
         uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
         ctx.comm_init(uid, dist.world, dist.rank)
-    n1 = args.n
-    # G > 1 (the rows of K are independent: SURVEY §8e): weak scaling with no data-path
-    # collective, N = n1 sqrt(G) so every GPU computes n1^2 Gram pairs (its block-cyclic
-    # rows x all N columns, packed in its own buffer); value = N^2 / max-over-ranks time.
-    # The north-star's final RCCL all-gather (K assembled on every GPU) is measured beside
-    # it at the fixed n1 (`assembled`).
-    n = weak_scaled_n(n1, dist.world)
-
-    sp_seed = 4 if n == 100000 else 2
+    # headline at every G: the named N = n1 (strong scaling), rows sharded over the ranks
+    # with no data-path collective (the rows of K are independent: SURVEY §8e); at G > 1
+    # the north-star's final RCCL all-gather (K assembled on every GPU) is `assembled` and
+    # the weak-scaled build (N = n1 sqrt(G)) `weak_scaled`
+    n = n1
     sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
                    sp_seed, args.steps, args.warmup, check_spectrum, gather=0)
     asm = None
     if rccl:
         asm = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n1,
-                        4 if n1 == 100000 else 2, args.steps, args.warmup, check_spectrum)
+                        sp_seed, args.steps, args.warmup, check_spectrum)
+    weak = None
+    if dist.world > 1:
+        nw = weak_scaled_n(n1, dist.world)
+        weak = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, nw,
+                         2, args.steps, args.warmup, check_spectrum, gather=0)
     mm = None
     if not args.no_mismatch:
         mm = run_build(ctx, dist, "mismatch_k9_m1",
@@ -773,11 +836,6 @@ def main():
         c5 = run_build(ctx, dist, "mismatch_k9_m1_raw",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
                        200000, 5, 2, 1, check_mismatch_raw)
-    cpu = {}
-    if dist.world == 1 and not args.no_cpu:
-        cpu["spectrum_k8"] = cpu_baseline("spectrum_k8", n, args.cpu_budget, sp_seed)
-        if mm:
-            cpu["mismatch_k9_m1"] = cpu_baseline("mismatch_k9_m1", args.mm_n, args.cpu_budget / 2, 3)
     extra = None
     if dist.world == 1 and not args.no_extra:
         extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(20, args.steps))
@@ -805,16 +863,17 @@ def main():
         "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
         "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": sp["ms_per_step"], "higher_is_better": True,
-        # weak: every GPU computes n1^2 Gram pairs at any G (N = n1 sqrt(G)), no data-path
-        # collective; the all-gather assembly at fixed N is `assembled`
-        "scaling": "weak",
+        # strong: the named N at every G, each GPU its 1/G of the rows (no data-path
+        # collective); the all-gather assembly is `assembled`, the weak-scaled build
+        # `weak_scaled`
+        "scaling": "strong",
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(%d)" % (4 if n == 100000 else 2),
         "config": {"workload": "spectrum k=8 full-K build, N=%d x L=101 (BASELINE configs[3], the "
-                               "north_star's target config, at G=1; G>1: N = 100000 sqrt(G), each "
-                               "GPU its block-cyclic rows x all N columns = 1e10 Gram pairs, no "
-                               "data-path collective)" % n,
-                   "N": n, "N_per_gpu_work": n1, "L": 101, "k": 8,
+                               "north_star's target config; G>1: each GPU its 1/G of the rows x "
+                               "all N columns, no data-path collective, K assembled over RCCL "
+                               "measured as `assembled`)" % n,
+                   "N": n, "L": 101, "k": 8,
                    "rows_this_rank": sp["rows_this_rank"],
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
@@ -832,6 +891,13 @@ def main():
             "collective_free": asm.get("collective_free"),
             "other_gather_mode": asm.get("other_gather_mode"),
             "gather_roofline": gather_roofline(asm, dist.world, 4)}
+    if weak:
+        line["weak_scaled"] = {
+            "workload": "spectrum k=8, N=%d = 100000 sqrt(G): each GPU its 1/G of the rows x "
+                        "all N columns (~1e10 Gram pairs per GPU), no data-path collective"
+                        % weak["N"],
+            "scaling": "weak", "N": weak["N"], "value": weak["pairs_per_s"],
+            **{k: weak[k] for k in ("ms_per_step", "stages_ms", "rows_this_rank", "spot_check")}}
     if mm:
         mm_rows_launch = mm["rows_this_rank"] / max(1, mm["rounds"])
         mm_bytes = 8.0 * mm_rows_launch * args.mm_n + 52.0 * args.mm_n

@@ -52,8 +52,10 @@ enum {
   KMG_WDS = 4,        /* get_WDShifts_K   kernels.py:138-155 */
   KMG_SUBSTRING = 5,  /* get_string_K     kernels.py:367-382 */
   KMG_LOCALALIGN = 6, /* get_LA_K         kernels.py:273-302 */
-  KMG_GAPPY = 7       /* get_gappy_K      kernels.py:436-455 (k=1,g=0 only: every other
-                         (k,g) raises in the reference under numpy 2) */
+  KMG_GAPPY = 7       /* get_gappy_K      kernels.py:436-455 (la_mode KMG_MODE_REFERENCE: the
+                         reference's behaviour, defined for k=1,g=0 -- every other (k,g) raises
+                         there under numpy 2; KMG_MODE_INTENDED: any 0 <= g < k,
+                         k <= 15, k-g <= 8) */
 };
 
 /* output element types */
@@ -67,7 +69,10 @@ enum { KMG_LA_REFERENCE = 0 /* bit-for-bit the reference: all zeros (kernels.py:
 enum { KMG_MODE_REFERENCE = 0 /* the reference's behaviour (GP: k=1,g=0 only) */,
        KMG_MODE_INTENDED = 1  /* GP: binary (k-g)-mer presence over the gapped subsequences
                                  of every 101-window k-mer, normalised (kernels.py:420-455 as
-                                 report §3.7 describes it); parity unpinned */ };
+                                 report §3.7 describes it); parity unpinned */,
+       KMG_MODE_SS_B = 2      /* SS: the auxiliary B_k(lbda, k, x, y) of the recursion
+                                 (kernels.py:322-342) at the full prefixes instead of
+                                 K_k (kernels.py:344-364); rows <= 127 symbols */ };
 
 #define KMG_MAX_COEF 64
 
@@ -131,6 +136,26 @@ int kmg_gram_device(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
 int kmg_gram_to_host(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
                      const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
                      int64_t slab_rows, void *h_out, int64_t ld_host);
+
+/*
+ * Feature vectors of n sequences over caller-chosen k-mer columns (host buffers): the
+ * reference's per-sequence feature maps, evaluated on the device.  out[i][j] (float64, row
+ * stride ld_out) for column code cols[j] (base-4 k-mer, first letter most significant, the
+ * index of ''.join(c) in itertools.product('ACGT', repeat=k); 0xFFFFFFFF = a beta no window
+ * can equal, value 0):
+ *   KMG_SPECTRUM  get_phi_u(x, k, betas)      kernels.py:12-25: windows range(len(x)-k+1)
+ *                 equal to the beta (a window holding a non-ACGT symbol equals none)
+ *   KMG_MISMATCH  get_phi_km(x, k, m, betas)  kernels.py:161-175: windows range(window-k+1)
+ *                 (window = 101) within Hamming distance m of the beta, a non-ACGT symbol
+ *                 mismatching every letter; rows shorter than the window are KMG_EINVAL
+ *                 (the reference raises while broadcasting the short k-mer)
+ *   KMG_GAPPY     gappy_k(x, 1, 0, betas)     kernels.py:420-433 (k=1, g=0): 1.0 when the
+ *                 letter occurs in x[0:window], else 0.0
+ * k <= 16.
+ */
+int kmg_features(kmg_ctx *ctx, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                 int64_t n, int64_t ldc, const uint32_t *cols, int64_t ncols, double *out,
+                 int64_t ld_out);
 
 /* normalize_K (kernels.py:398-415) in place on a host float64 matrix, including the
  * "K[0,0]==1 -> unchanged" rule (returns 1 in *skipped then). */
@@ -257,7 +282,8 @@ int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *
 
 /* How the last spectrum / mismatch Gram call on ctx was built (for roofline accounting):
  * plan[0] formulation (0 dense count-vector GEMM, 1 all-pairs Hamming, 2 posting lists,
- * 3 mismatch drop-one slot table, 4 drop-two pair table, 5 pair lines; -1 none yet),
+ * 3 mismatch drop-one slot table, 4 drop-two pair table, 5 pair lines, 6 the generic
+ * per-pair kernels of k > 16; -1 none yet or the call failed before choosing),
  * plan[1] columns per chunk, plan[2] column chunks, plan[3] 1 when a full square K was built
  * by its upper block triangle and mirrored, plan[4] Gram workgroup threads (0 where the
  * formulation has no column chunks).  No reference counterpart (diagnostics). */

@@ -200,6 +200,7 @@ struct kmg_ctx {
   rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
+  DevBuf ft_cols;                 // kmg_features: the column k-mer codes
   DevBuf slabs;                   // kmg_gram_to_host: two device row slabs
   hipStream_t d2h_stream = nullptr;             // kmg_gram_to_host: slab copies out
   hipEvent_t ev_slab[2] = {nullptr, nullptr};   // slab Gram done / copied out
@@ -793,6 +794,7 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 // Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
 // kmg_gram_blocks' choice of the round-slab format).
 enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL };
+constexpr int32_t KMG_PLAN_GENERIC = 6;  // kmg_last_plan: the per-pair kernels of k > 16
 SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
@@ -872,10 +874,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (mm && n > 0 && ldc < g.window)
         return fail(KMG_EINVAL, "mismatch: code rows (%lld) shorter than the window %d",
                     (long long)ldc, g.window);
+      // kmg_last_plan: reset first, so no return below reports the previous call's plan
+      c->plan[0] = -1;
+      c->plan[1] = c->plan[2] = c->plan[3] = c->plan[4] = 0;
       if (k > 16) {
         // k-mers past 32 bits: the generic per-pair kernels (kmg_generic.hip)
+        c->plan[0] = KMG_PLAN_GENERIC;
         if (narrow) return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
-        if (dt == KMG_I32 && mm && p->normalize)
+        if (dt == KMG_I32 && p->normalize)
           return fail(KMG_EINVAL, "normalised output needs a floating dtype");
         const SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
         const int sq = (ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
@@ -890,7 +896,17 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         };
         int rc;
         if (!mm) {
-          rc = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          if (p->normalize) {  // normalize_K with the spectrum diagonal K(x, x)
+            KMG_TRY(c->diagv.ensure(sizeof(double) * (size_t)std::max<int64_t>(1, n)));
+            KMG_TRY(c->dsq.ensure(sizeof(double) * (size_t)std::max<int64_t>(1, n)));
+            StageTimer t(c, ST_DIAG);
+            KMG_HIP(run(launch_sp_generic_diag(q, k, c->diagv.as<double>(), c->dsq.as<double>(),
+                                               c->stream)));
+            o.normalize = 1;
+            o.diagv = c->diagv.as<double>();
+            o.dsq = c->dsq.as<double>();
+          }
+          rc = unsupported ? KMG_OK : each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
             return run(launch_gram_sp_generic(q, r0, r1, k, sq, oq, c->stream));
           });
         } else {
@@ -951,7 +967,6 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       };
       // kmg_last_plan: formulation, then chunking / triangle / workgroup once chosen
       c->plan[0] = (int32_t)path;
-      c->plan[1] = c->plan[2] = c->plan[3] = c->plan[4] = 0;
       auto note_plan = [&](int threads) {
         c->plan[1] = g.chunk;
         c->plan[2] = g.nchunks;
@@ -1244,6 +1259,10 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
     case KMG_SUBSTRING: {
       if (p->k < 0) return fail(KMG_EINVAL, "k < 0");
       if (dt == KMG_I32) return fail(KMG_EINVAL, "SS produces float64 values");
+      // la_mode KMG_MODE_SS_B: B_k(lbda, k, x, y) (kernels.py:322-342) instead of K_k
+      if (p->la_mode != KMG_MODE_REFERENCE && p->la_mode != KMG_MODE_SS_B)
+        return fail(KMG_EINVAL, "SS: unknown la_mode %d", p->la_mode);
+      const int bmode = p->la_mode == KMG_MODE_SS_B ? 1 : 0;
       // k <= 33 at sequence lengths <= 127 (grouped sweep), k <= 16 at any length (strips)
       SeqSpec q{d_codes, d_lens, n, ldc, maxlen};
       // one range covering the whole matrix: upper triangle + mirror (kernels.py:378-381)
@@ -1251,7 +1270,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       bool unsupported = false;
       const int r = each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         hipError_t e = launch_gram_ss(q, r0, r1, p->k, p->lambda, p->lambda2, mirror, oq, c->stream,
-                                      c->tune.ss_lpp);
+                                      c->tune.ss_lpp, bmode);
         if (e == hipErrorNotSupported) {
           unsupported = true;
           return hipSuccess;
@@ -1260,7 +1279,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       });
       if (unsupported)
         return fail(KMG_EUNSUPPORTED, "SS: k = %d with sequences of length %d (k <= 33 up to "
-                    "length 127, k <= 16 beyond)", p->k, maxlen);
+                    "length 127, k <= 16 beyond; B_k: k <= 32 up to length 127)", p->k, maxlen);
       return r;
     }
     case KMG_LOCALALIGN: {
@@ -1394,7 +1413,7 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
-                    &c->gcoef, &c->feat32, &c->k32};
+                    &c->gcoef, &c->feat32, &c->k32, &c->ft_cols};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -1444,6 +1463,69 @@ int kmg_gram(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_
                       {RowRange{0, n, c->h_out.p}}, out_dtype, ldd));
   KMG_HIP(hipMemcpy2DAsync(out, (size_t)ld_out * esz, c->h_out.p, (size_t)ldd * esz,
                            (size_t)n * esz, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  KMG_HIP(hipStreamSynchronize(c->stream));
+  return KMG_OK;
+}
+
+int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                 int64_t n, int64_t ldc, const uint32_t *cols, int64_t ncols, double *out,
+                 int64_t ld_out) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  if (!p) return fail(KMG_EINVAL, "params is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n < 0 || ncols < 0 || ldc < 0) return fail(KMG_EINVAL, "negative size");
+  if (n == 0 || ncols == 0) return KMG_OK;
+  if (!codes || !lens || !cols || !out) return fail(KMG_EINVAL, "NULL buffer");
+  if (ld_out < ncols) return fail(KMG_EINVAL, "ld_out < ncols");
+  int k = p->k, m = 0, window = 0, binary = 0;
+  switch (p->kind) {
+    case KMG_SPECTRUM: break;  // get_phi_u: windows range(len(x) - k + 1)
+    case KMG_MISMATCH:         // get_phi_km: windows range(101 - k + 1)
+      m = p->m;
+      window = p->window > 0 ? p->window : 101;
+      if (m < 0) return fail(KMG_EINVAL, "m < 0");
+      break;
+    case KMG_GAPPY:  // gappy_k (k = 1, g = 0): letters of x[0:101]
+      if (!(p->k == 1 && p->g == 0)) return fail(KMG_EUNSUPPORTED, "gappy features: k=1, g=0 only");
+      window = p->window > 0 ? p->window : 101;
+      binary = 1;
+      break;
+    default:
+      return fail(KMG_EUNSUPPORTED, "features: spectrum, mismatch or gappy only");
+  }
+  if (k < 1 || k > 16) return fail(KMG_EUNSUPPORTED, "features: 1 <= k <= 16 (k = %d)", k);
+  for (int64_t i = 0; i < n; ++i) {
+    if (lens[i] < 0 || lens[i] > ldc) return fail(KMG_EINVAL, "lens[%lld] outside [0,ldc]", (long long)i);
+    if (p->kind == KMG_MISMATCH && lens[i] < window)
+      return fail(KMG_EINVAL, "mismatch features need sequences of length >= %d", window);
+    if ((window > 0 ? std::min<int64_t>(window, lens[i]) : lens[i]) - k + 1 > KMG_FEAT_MAXW)
+      return fail(KMG_EUNSUPPORTED, "features: more than %d windows per sequence", KMG_FEAT_MAXW);
+  }
+  KMG_HIP(hipSetDevice(c->device));
+  // rows per launch: the device output slab stays <= 1 GiB (and grid.y <= 65535)
+  const int64_t slab = std::max<int64_t>(1, std::min<int64_t>({n, 65535, (1LL << 27) / ncols}));
+  KMG_TRY(c->h_codes.ensure((size_t)n * std::max<int64_t>(1, ldc)));
+  KMG_TRY(c->h_lens.ensure(sizeof(int32_t) * (size_t)n));
+  KMG_TRY(c->ft_cols.ensure(sizeof(uint32_t) * (size_t)ncols));
+  KMG_TRY(c->h_out.ensure(sizeof(double) * (size_t)slab * ncols));
+  KMG_HIP(hipMemcpyAsync(c->h_codes.p, codes, (size_t)n * ldc, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipMemcpyAsync(c->h_lens.p, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  KMG_HIP(hipMemcpyAsync(c->ft_cols.p, cols, sizeof(uint32_t) * ncols, hipMemcpyHostToDevice,
+                         c->stream));
+  for (int64_t r0 = 0; r0 < n; r0 += slab) {
+    const int64_t rows = std::min(slab, n - r0);
+    {
+      StageTimer t(c, ST_FEATURES);
+      KMG_HIP(launch_features(c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), ldc, r0, rows, k,
+                              m, window, binary, c->ft_cols.as<uint32_t>(), ncols,
+                              c->h_out.as<double>(), ncols, c->stream));
+    }
+    KMG_HIP(hipMemcpy2DAsync(out + (size_t)r0 * ld_out, (size_t)ld_out * sizeof(double), c->h_out.p,
+                             (size_t)ncols * sizeof(double), (size_t)ncols * sizeof(double),
+                             (size_t)rows, hipMemcpyDeviceToHost, c->stream));
+    // (the next slab reuses the device buffer: hipMemcpy2DAsync to pageable memory returns
+    // once the copy has been staged, and the stream orders the next launch behind it)
+  }
   KMG_HIP(hipStreamSynchronize(c->stream));
   return KMG_OK;
 }

@@ -60,27 +60,47 @@ __device__ int64_t spectrum_pair(const uint8_t *x, int Lx, const uint8_t *y, int
   return cnt;
 }
 
-// sum over window pairs of w[ham]: windows start below P = W - k + 1 in both rows
-__device__ int64_t mismatch_pair(const uint8_t *x, const uint8_t *y, int W, int k,
-                                 const int64_t *w, int maxd) {
+// sum over window pairs of w[ham]: windows start below P = W - k + 1 in both rows.  A
+// window that reaches past its row's length or holds a non-ACGT symbol is invalid and
+// weighs nothing, as in the packed k <= 16 kernels (pk_window); x and y are read only
+// below their lengths, so padding bytes never enter.
+__device__ __forceinline__ uint32_t sym_at(const uint8_t *x, int Lx, int p) {
+  return p < Lx ? (uint32_t)x[p] : 0xFFu;  // 0xFF: past the row (invalid)
+}
+
+__device__ int64_t mismatch_pair(const uint8_t *x, int Lx, const uint8_t *y, int Ly, int W,
+                                 int k, const int64_t *w, int maxd) {
   const int P = W - k + 1;
   int64_t tot = 0;
   for (int dlt = -(P - 1); dlt <= P - 1; ++dlt) {
     const int ox = max(dlt, 0), oy = max(-dlt, 0);
     // window starts t = 0 .. P - 1 - max(ox, oy) along this diagonal
     const int nwin = P - max(ox, oy);
-    int h = 0;
-    for (int t = 0; t < k; ++t) h += x[ox + t] != y[oy + t] ? 1 : 0;
+    int h = 0, bad = 0;  // mismatches / invalid symbols (either row) inside the window
+    auto step = [&](int t, int sgn) {
+      const uint32_t a = sym_at(x, Lx, ox + t), b = sym_at(y, Ly, oy + t);
+      h += sgn * (a != b ? 1 : 0);
+      bad += sgn * ((a > 3u ? 1 : 0) + (b > 3u ? 1 : 0));
+    };
+    for (int t = 0; t < k; ++t) step(t, 1);
     for (int t = 0; t < nwin; ++t) {
-      if (t > 0)
-        h += (x[ox + t + k - 1] != y[oy + t + k - 1] ? 1 : 0) - (x[ox + t - 1] != y[oy + t - 1] ? 1 : 0);
-      tot += h <= maxd ? w[h] : 0;
+      if (t > 0) {
+        step(t + k - 1, 1);
+        step(t - 1, -1);
+      }
+      tot += (bad == 0 && h <= maxd) ? w[h] : 0;
     }
   }
   return tot;
 }
 
 }  // namespace
+
+// normalize_K (kernels.py:398-415) as the fused epilogues evaluate it
+__device__ __forceinline__ double gen_norm(const OutSpec &o, int64_t r, int64_t c, int64_t raw) {
+  if (!o.normalize || o.diagv[0] == 1.0) return (double)raw;
+  return r == c ? 1.0 : (double)raw / (o.dsq[r] * o.dsq[c]);
+}
 
 __global__ __launch_bounds__(GEN_THREADS) void gram_sp_generic_kernel(SeqSpec q, int64_t row0,
                                                                       int64_t row1, int k,
@@ -94,8 +114,20 @@ __global__ __launch_bounds__(GEN_THREADS) void gram_sp_generic_kernel(SeqSpec q,
   if (j >= q.n) return;
   const int Ly = q.lens[j];
   const int64_t v = (Lx < k || Ly < k) ? 0 : spectrum_pair(xs, Lx, q.codes + j * q.ldc, Ly, k);
-  gen_store(o, i - row0, j, (double)v);
-  if (mirror && j != i && j >= row0 && j < row1) gen_store(o, j - row0, i, (double)v);
+  gen_store(o, i - row0, j, gen_norm(o, i, j, v));
+  if (mirror && j != i && j >= row0 && j < row1) gen_store(o, j - row0, i, gen_norm(o, j, i, v));
+}
+
+// spectrum K(x, x) of every row (the fused normalize_K's diagonal)
+__global__ __launch_bounds__(GEN_THREADS) void sp_generic_diag_kernel(SeqSpec q, int k,
+                                                                      double *diagv, double *dsq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q.n) return;
+  const uint8_t *x = q.codes + i * q.ldc;
+  const int Lx = min(q.lens[i], GEN_MAXL);
+  const double d = (Lx < k) ? 0.0 : (double)spectrum_pair(x, Lx, x, Lx, k);
+  diagv[i] = d;
+  dsq[i] = sqrt(d);
 }
 
 __global__ __launch_bounds__(GEN_THREADS) void mm_generic_diag_kernel(SeqSpec q, int W, int k,
@@ -105,7 +137,8 @@ __global__ __launch_bounds__(GEN_THREADS) void mm_generic_diag_kernel(SeqSpec q,
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= q.n) return;
   const uint8_t *x = q.codes + i * q.ldc;
-  const double d = (double)mismatch_pair(x, x, W, k, w, maxd);
+  const int Lx = min(q.lens[i], W);
+  const double d = (double)mismatch_pair(x, Lx, x, Lx, W, k, w, maxd);
   diagv[i] = d;
   dsq[i] = sqrt(d);
 }
@@ -119,17 +152,13 @@ __global__ __launch_bounds__(GEN_THREADS) void gram_mm_generic_kernel(SeqSpec q,
   const int64_t i = row0 + blockIdx.y;
   const int64_t jb = (mirror ? i : 0) + (int64_t)blockIdx.x * blockDim.x;
   if (i >= row1 || jb >= q.n) return;  // block-uniform
-  (void)stage_row(q, i, xs, W);
+  const int Lx = stage_row(q, i, xs, W);
   const int64_t j = jb + threadIdx.x;
   if (j >= q.n) return;
-  const int64_t raw = mismatch_pair(xs, q.codes + j * q.ldc, W, k, w, maxd);
-  auto val = [&](int64_t r, int64_t c) -> double {
-    // normalize_K (kernels.py:398-415) as the fused epilogues evaluate it
-    if (!o.normalize || o.diagv[0] == 1.0) return (double)raw;
-    return r == c ? 1.0 : (double)raw / (o.dsq[r] * o.dsq[c]);
-  };
-  gen_store(o, i - row0, j, val(i, j));
-  if (mirror && j != i && j >= row0 && j < row1) gen_store(o, j - row0, i, val(j, i));
+  const int64_t raw =
+      mismatch_pair(xs, Lx, q.codes + j * q.ldc, min(q.lens[j], W), W, k, w, maxd);
+  gen_store(o, i - row0, j, gen_norm(o, i, j, raw));
+  if (mirror && j != i && j >= row0 && j < row1) gen_store(o, j - row0, i, gen_norm(o, j, i, raw));
 }
 
 // Python slice equality x[a:a+k] == y[b:b+k]: both clipped to their row, equal iff the
@@ -197,6 +226,15 @@ hipError_t launch_gram_sp_generic(const SeqSpec &q, int64_t row0, int64_t row1, 
   if (rows > 65535 || q.maxlen > GEN_MAXL) return hipErrorNotSupported;
   hipLaunchKernelGGL(gram_sp_generic_kernel, gen_grid(q, row0, rows, mirror), dim3(GEN_THREADS), 0,
                      s, q, row0, row1, k, mirror, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_sp_generic_diag(const SeqSpec &q, int k, double *diagv, double *dsq,
+                                  hipStream_t s) {
+  if (q.n == 0) return hipSuccess;
+  if (q.maxlen > GEN_MAXL) return hipErrorNotSupported;
+  hipLaunchKernelGGL(sp_generic_diag_kernel, dim3((unsigned)((q.n + GEN_THREADS - 1) / GEN_THREADS)),
+                     dim3(GEN_THREADS), 0, s, q, k, diagv, dsq);
   return hipGetLastError();
 }
 

@@ -286,6 +286,8 @@ struct SeqSpec {
 // specialised kernels' shift and length limits)
 hipError_t launch_gram_sp_generic(const SeqSpec &q, int64_t row0, int64_t row1, int k, int mirror,
                                   const OutSpec &o, hipStream_t s);
+hipError_t launch_sp_generic_diag(const SeqSpec &q, int k, double *diagv, double *dsq,
+                                  hipStream_t s);
 hipError_t launch_mm_generic_diag(const SeqSpec &q, int W, int k, const int64_t *w, int maxd,
                                   double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_gram_mm_generic(const SeqSpec &q, int64_t row0, int64_t row1, int W, int k,
@@ -303,9 +305,11 @@ hipError_t launch_gram_wd_packed(const SeqSpec &q, const Packed &pk, int64_t row
 hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, int S, int span,
                            const double *beta, const double *delta, const OutSpec &o,
                            hipStream_t s);
-// lpp: lanes a pair of the grouped sweep (0 auto; 16 / 32 force the wider groups)
+// lpp: lanes a pair of the grouped sweep (0 auto; 16 / 32 force the wider groups);
+// bmode: B_kk(x, y) of the recursion (kernels.py:322-342) instead of K_kk (grouped sweep only)
 hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
-                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp = 0);
+                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp = 0,
+                          int bmode = 0);
 // LA kernel, intended semantics (KMG_LA_INTENDED): five-array affine-gap DP per pair
 hipError_t launch_gram_la(const SeqSpec &q, int64_t row0, int64_t row1, double e, double d,
                           double beta, int smith, int mirror, const OutSpec &o, hipStream_t s,
@@ -316,6 +320,14 @@ hipError_t launch_row_stats(const SeqSpec &q, uint32_t *stats, hipStream_t s);
 hipError_t launch_gram_gappy1(const SeqSpec &q, int64_t row0, int64_t row1, int window,
                               const OutSpec &o, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double value, hipStream_t s);
+
+// per-sequence feature vectors over caller-chosen k-mer columns (kmg_features.hip):
+// out[r][j] for sequences row0 + r, r < rows; window 0 = every window of the row
+#define KMG_FEAT_MAXW 4096
+hipError_t launch_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t row0,
+                           int64_t rows, int k, int m, int window, int binary,
+                           const uint32_t *cols, int64_t ncols, double *out, int64_t ld,
+                           hipStream_t s);
 
 // gappy (k, g), intended semantics: binary (k-g)-mer presence features (kmg_dense.hip)
 hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, int k, int kk,

@@ -596,7 +596,7 @@ __global__ __launch_bounds__(256) void gram_ss_kernel(SeqSpec q, int64_t row0, i
 template <int LPP, int R, int NL>
 __global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, int64_t row1,
                                                        int kk, double lam, double lam2,
-                                                       int mirror, OutSpec o) {
+                                                       int mirror, OutSpec o, int bmode) {
   constexpr int G = 64 / LPP;
   extern __shared__ __align__(16) double gsm[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -614,8 +614,11 @@ __global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, 
   const uint8_t *xs = q.codes + ia * q.ldc;
   const uint8_t *ys = q.codes + ib * q.ldc;
   const int nx = pv ? q.lens[ia] : -1, ny = pv ? q.lens[ib] : -1;
-  // a pair takes part in the sweep unless its value is a constant (kernels.py:354-358)
-  const bool dp = pv && kk >= 1 && nx >= kk && ny >= kk;
+  // a pair takes part in the sweep unless its value is a constant (kernels.py:354-358);
+  // bmode (B_{kk-1}, levels 1..kk-1 computed, kernels.py:331-335): prefixes of >= kk-1
+  const bool dp = bmode ? (pv && kk >= 2 && nx >= kk - 1 && ny >= kk - 1)
+                        : (pv && kk >= 1 && nx >= kk && ny >= kk);
+  double bval = 0.0;  // bmode: B_{kk-1}(x, y) at the cell (n_x, n_y), held by its row's lane
   for (int c = s; c < ny; c += LPP) ysh[c] = ys[c];
   // x_{r-1} and x_r of the lane's rows, packed 4 a word (0x1FF-like sentinel 0xFF:
   // never equal to a code of y, which the match tests compare as bytes)
@@ -686,6 +689,11 @@ __global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, 
               if (t == kk - 2) bkm1 = cur[t];
             sacc[k] = __dadd_rn(sacc[k], bkm1);
           }
+          if (bmode && r == nx && c == ny) {
+#pragma unroll
+            for (int t = 0; t < NL; ++t)
+              if (t == kk - 2) bval = cur[t];
+          }
 #pragma unroll
           for (int t = 0; t < NL; ++t) {
             adiag[t] = last[k][t];
@@ -704,10 +712,13 @@ __global__ __launch_bounds__(256) void gram_ssg_kernel(SeqSpec q, int64_t row0, 
 #pragma unroll
   for (int k = 0; k < R; ++k)
     if (dp && r0 + k < nx) Ssh[r0 + k + 1] = sacc[k];
+  if (bmode && dp && nx >= r0 && nx < r0 + R) Ssh[0] = bval;
   __builtin_amdgcn_wave_barrier();
   if (s == 0 && pv) {
     double K = 0.0;
-    if (kk == 0) {
+    if (bmode) {
+      K = kk == 1 ? 1.0 : dp ? Ssh[0] : 0.0;  // B_0 == 1; short prefixes: 0 (kernels.py:331-335)
+    } else if (kk == 0) {
       K = 1.0;  // K_k(.., 0, ..) returns 1 (kernels.py:354-355)
     } else if (dp) {
       for (int ii = kk; ii <= nx; ++ii) K = __dadd_rn(K, __dmul_rn(lam2, Ssh[ii]));
@@ -1198,11 +1209,17 @@ hipError_t launch_gram_wds(const SeqSpec &q, int64_t row0, int64_t row1, int d, 
 }
 
 hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, double lam,
-                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp) {
+                          double lam2, int mirror, const OutSpec &o, hipStream_t s, int lpp,
+                          int bmode) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || q.n == 0) return hipSuccess;
   const int ML = q.maxlen;
   if (rows > 65535) return hipErrorInvalidValue;
+  if (bmode) {
+    // B_kk needs levels 1..kk: the sweep of K_{kk+1}, reading level kk at the corner
+    if (kk < 0 || kk > 32) return hipErrorNotSupported;
+    kk += 1;
+  }
   // grouped sweep whenever the rows fit one group (LPP x R >= ML + 1) and kk - 1 <= 32
   // levels: NL levels exactly for kk <= 9, rounded up to 12 / 16 / 24 / 32 above
   const int nl = kk >= 2 ? kk - 1 : 1;
@@ -1213,7 +1230,7 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
     const int64_t cols = mirror ? q.n - row0 : q.n;  // mirror: columns from row i on
     const dim3 grid((unsigned)((cols + 4 * G - 1) / (4 * G)), (unsigned)rows);
     hipLaunchKernelGGL((gram_ssg_kernel<LPP, R, NL>), grid, dim3(256), (lds + 15) & ~(size_t)15, s,
-                       q, row0, row1, kk, lam, lam2, mirror, o);
+                       q, row0, row1, kk, lam, lam2, mirror, o, bmode);
     return hipGetLastError();
   };
 #define KMG_SSG(LPP_, R_, NL_) \
@@ -1247,6 +1264,7 @@ hipError_t launch_gram_ss(const SeqSpec &q, int64_t row0, int64_t row1, int kk, 
     return nl <= 12 ? KMG_SSG(64, 2, 12) : nl <= 16 ? KMG_SSG(64, 2, 16)
                     : nl <= 24 ? KMG_SSG(64, 2, 24) : KMG_SSG(64, 2, 32);
 #undef KMG_SSG
+  if (bmode) return hipErrorNotSupported;
   // longer sequences: the strip kernel (64-row strips, the boundary row in LDS), as many
   // waves (pairs) a block as their LDS allows (4 up to length ~300 at k = 16, 1 to ~1200)
   const int kmx = kk <= 2 ? 2 : kk <= 4 ? 4 : kk <= 8 ? 8 : 16;

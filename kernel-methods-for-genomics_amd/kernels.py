@@ -10,8 +10,11 @@ for gfx950).  Put this directory on ``sys.path`` ahead of the reference and
 There is no CPU fallback: without the built library or a visible HIP device every
 Gram call raises.
 """
+import functools
+
 import numpy as np
 
+from kmgram import _lib as _L
 from kmgram import engine as _engine
 from kmgram.encode import as_sequence_list as _seqs
 from kmgram.params import beta, delta  # noqa: F401  (reference helpers, kernels.py:53,106)
@@ -20,7 +23,7 @@ __all__ = [
     "get_spectrum_K", "get_WD_K", "get_WDShifts_K", "get_mismatch_K", "get_LA_K",
     "get_string_K", "get_gappy_K", "center_K", "normalize_K", "select_method", "beta",
     "delta", "letter_to_num", "format", "S", "get_WD_d", "get_WDShifts_d", "K_k",
-    "affine_align", "Smith_Waterman",
+    "affine_align", "Smith_Waterman", "get_phi_u", "get_phi_km", "gappy_k", "B_k", "rec",
 ]
 
 # substitution matrix extracted from BLOSUM62 (kernels.py:223)
@@ -129,6 +132,170 @@ def Smith_Waterman(x, y, e=11, d=1, beta=0.5):
     """Reference Smith-Waterman LA value of one pair: always 0.0 (kernels.py:249-270)."""
     _engine.GramEngine._require_acgt([x, y])
     return 0.0
+
+
+# ----------------------------------------------------------------------- feature maps
+# The reference's per-sequence feature maps, evaluated on the device (kmg_features): the
+# host only maps each beta to its base-4 k-mer code (the column the device scores).
+_NO_MATCH = 0xFFFFFFFF
+_ACGT_CODE = np.full(256, 255, dtype=np.uint8)
+for _i, _c in enumerate(b"ACGT"):
+    _ACGT_CODE[_c] = _i
+
+
+def _codes_of_rows(rows, k):
+    """int letter rows (values 0..3) [nb, k] -> base-4 codes, first letter most significant."""
+    out = np.zeros(rows.shape[0], dtype=np.uint64)
+    for q in range(k):
+        out = out * np.uint64(4) + rows[:, q].astype(np.uint64)
+    return out.astype(np.uint32)
+
+
+def _string_beta_cols(betas, k):
+    """get_phi_u's string betas -> column codes.  A beta of another length than k equals
+    no window (x[i:i+k] always holds k symbols); the device scores ACGT k-mers."""
+    if not all(isinstance(b, str) for b in betas):
+        raise TypeError("get_phi_u: betas must be strings (kernels.py:37)")
+    cols = np.full(len(betas), _NO_MATCH, dtype=np.uint32)
+    sel = np.fromiter((len(b) == k for b in betas), dtype=bool, count=len(betas))
+    if sel.any():
+        try:
+            raw = "".join(b for b, t in zip(betas, sel) if t).encode("ascii")
+        except UnicodeEncodeError:
+            raw = None
+        letters = None if raw is None else _ACGT_CODE[np.frombuffer(raw, dtype=np.uint8)]
+        if letters is None or (letters > 3).any():
+            raise NotImplementedError("get_phi_u: betas outside the A/C/G/T alphabet")
+        cols[sel] = _codes_of_rows(letters.reshape(-1, k), k)
+    return cols
+
+
+def _format_rows(a):
+    """format()ed letters (1..4 for A, C, G, T) -> 0..3; anything else -> 4 (a symbol that
+    mismatches every letter, as an integer outside 1..4 compares in kernels.py:174)."""
+    a = np.asarray(a)
+    ok = (a >= 1) & (a <= 4)
+    return np.where(ok, a - 1, 4).astype(np.uint8), bool(ok.all())
+
+
+def _formatted(x):
+    """x as get_phi_km / gappy_k receive it, format(x) (kernels.py:209, 448); a str is
+    format()ed here first (the reference's own callers always pass format(x))."""
+    return format(x) if isinstance(x, str) else np.asarray(x)
+
+
+def _decoded(x):
+    """format()ed integer letters back to the sequence string the encoder takes; symbols
+    outside 1..4 become 'N' (they equal no letter of a beta)."""
+    codes, _ = _format_rows(x)
+    return "".join("ACGTN"[c] for c in codes.reshape(-1))
+
+
+def _formatted_beta_cols(betas, k, who):
+    B = np.asarray(betas)
+    if B.ndim == 1 and k == 1:
+        B = B.reshape(-1, 1)
+    if B.size == 0:
+        return np.zeros(len(betas), dtype=np.uint32)
+    if B.ndim != 2 or B.shape[1] != k:
+        raise NotImplementedError(f"{who}: betas must be format()ed {k}-mers")
+    rows, ok = _format_rows(B)
+    if not ok:
+        raise NotImplementedError(f"{who}: betas outside the A/C/G/T alphabet")
+    return _codes_of_rows(rows, k)
+
+
+def get_phi_u(x, k, betas):
+    """Spectrum feature vector of x (kernels.py:12-25): phi[j] = #{i < len(x)-k+1 :
+    x[i:i+k] == betas[j]}, float64[len(betas)].  Computed on the device."""
+    k = int(k)
+    if k < 1:
+        raise ValueError("k must be >= 1")
+    if not isinstance(x, str):
+        raise TypeError("get_phi_u: x must be a DNA string (kernels.py:39-40)")
+    betas = list(betas)
+    if not betas:
+        return np.zeros(0)
+    cols = _string_beta_cols(betas, k)
+    return _eng().features(_L.KMG_SPECTRUM, [x], k, cols)[0]
+
+
+def get_phi_km(x, k, m, betas):
+    """Mismatch feature vector of format(x) (kernels.py:161-175): phi[j] = #{i < 101-k+1 :
+    sum(x[i:i+k] != betas[j]) <= m}, float64[len(betas)].  Computed on the device.  A row
+    shorter than the 101 window raises the ValueError numpy raises comparing its first
+    short k-mer (kernels.py:174)."""
+    k, m = int(k), int(m)
+    if k < 1:
+        raise ValueError("k must be >= 1")
+    xa = _formatted(x).reshape(-1)
+    n_x = len(xa)
+    if len(betas) == 0:
+        return np.zeros(0)
+    if n_x < 101:
+        # window lengths min(k, n_x - i), i in range(101 - k + 1): numpy broadcasts a
+        # short k-mer of 1 symbol (or 0 at k = 1) against the beta and raises for others
+        quirk = False
+        for i in range(101 - k + 1):
+            ln = max(0, min(k, n_x - i))
+            if ln == k:
+                continue
+            if ln == 1 or k == 1:
+                quirk = True
+                continue
+            raise ValueError(f"operands could not be broadcast together with shapes ({ln},) "
+                             f"({k},) ")
+        if quirk:
+            raise NotImplementedError("get_phi_km: a row shorter than 101 whose short k-mers "
+                                      "numpy broadcasts (1 symbol) is not supported")
+    cols = _formatted_beta_cols(betas, k, "get_phi_km")
+    return _eng().features(_L.KMG_MISMATCH, [_decoded(xa)], k, cols, m=m)[0]
+
+
+def gappy_k(x, k, g, betas):
+    """Gappy feature vector of format(x) (kernels.py:420-433): phi[j] = [betas[j] in
+    gap_set], gap_set = the (k-g)-combinations of every window x[i:i+k], i < 101-k+1.
+    Under numpy 2 `b in gap_set` compares a length-k array with (k-g)-tuples, which raises
+    for every (k, g) but k=1, g=0 once gap_set is non-empty (engine.gappy_reference_errors,
+    pinned to the reference's own failures); k=1, g=0 (letter presence in x[0:101]) is
+    computed on the device."""
+    k, g = int(k), int(g)
+    xa = _formatted(x).reshape(-1)
+    if k - g < 0 or len(betas) > 0:
+        _engine.gappy_reference_errors(len(xa), k, g)
+    if len(betas) == 0:
+        return np.zeros(0)
+    if not (k == 1 and g == 0):
+        return np.zeros(len(betas))  # gap_set is empty (no error above): no beta is in it
+    cols = _formatted_beta_cols(betas, 1, "gappy_k")
+    return _eng().features(_L.KMG_GAPPY, [_decoded(xa)], 1, cols, g=0)[0]
+
+
+def rec(func):
+    """Memoise ``func`` on the printed form of its arguments, '[a]-[b]-...' (the key of
+    kernels.py:308-319): calls whose arguments print alike share one result."""
+    memo = {}
+
+    @functools.wraps(func)
+    def recd(*args):
+        key = "-".join("[%s]" % (a,) for a in args)
+        if key not in memo:
+            memo[key] = func(*args)
+        return memo[key]
+    return recd
+
+
+@rec
+def B_k(lbda, k, x, y):
+    """Auxiliary B_k(x, y) of the substring kernel's recursion (kernels.py:322-342), read
+    off the device sweep (KMG_MODE_SS_B): 1 for k = 0, 0 when a string is shorter than k
+    (the reference's integer base cases), else the float64 recursion value."""
+    k = int(k)
+    if k == 0:
+        return 1
+    if len(x) < k or len(y) < k:
+        return 0
+    return _eng().substring_b_pair(x, y, lbda, k)
 
 
 # ----------------------------------------------------------------------- dispatch

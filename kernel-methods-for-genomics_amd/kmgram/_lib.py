@@ -20,6 +20,7 @@ KMG_SPECTRUM, KMG_MISMATCH, KMG_WD, KMG_WDS, KMG_SUBSTRING, KMG_LOCALALIGN, KMG_
 KMG_I32, KMG_F32, KMG_F64 = 1, 2, 3
 KMG_LA_REFERENCE, KMG_LA_INTENDED = 0, 1
 KMG_MODE_REFERENCE, KMG_MODE_INTENDED = 0, 1  # GP semantics (include/kmgram.h)
+KMG_MODE_SS_B = 2  # SS: B_k of the recursion instead of K_k (include/kmgram.h)
 KMG_MAX_COEF = 64
 
 DTYPES = {KMG_I32: np.int32, KMG_F32: np.float32, KMG_F64: np.float64}
@@ -34,7 +35,7 @@ EXPORTS = (
     "kmg_nlck_grad_device", "kmg_alignf", "kmg_alignf_device", "kmg_krr_solve",
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
-    "kmg_gram_to_host", "kmg_gram_blocks_wire", "kmg_last_plan",
+    "kmg_gram_to_host", "kmg_gram_blocks_wire", "kmg_last_plan", "kmg_features",
 )
 
 
@@ -89,6 +90,8 @@ def load():
             "kmg_gram": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64], ctypes.c_int),
             "kmg_gram_device": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I64, I64, I32, P,
                                  I64], ctypes.c_int),
+            "kmg_features": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, P, I64, P, I64],
+                             ctypes.c_int),
             "kmg_normalize": ([P, P, I64, I64, ctypes.POINTER(I32)], ctypes.c_int),
             "kmg_center": ([P, P, I64, P, I64, I64], ctypes.c_int),
             "kmg_dmalloc": ([P, ctypes.POINTER(P), SZ], ctypes.c_int),
@@ -195,6 +198,18 @@ class Context:
         lens = np.ascontiguousarray(lens, dtype=np.int32)
         check(self.lib.kmg_gram(self._h, ctypes.byref(params), ptr(codes), ptr(lens), n, ldc,
                                 out_dtype, ptr(out), n))
+        return out
+
+    def features(self, params, codes, lens, cols):
+        """float64 [n, len(cols)] feature rows (kmg_features): column j scores the k-mer code
+        cols[j] (0xFFFFFFFF: a beta no window can equal)."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        cols = np.ascontiguousarray(cols, dtype=np.uint32)
+        n, ldc = codes.shape
+        out = np.empty((n, len(cols)), dtype=np.float64)
+        check(self.lib.kmg_features(self._h, ctypes.byref(params), ptr(codes), ptr(lens), n, ldc,
+                                    ptr(cols), len(cols), ptr(out), len(cols)))
         return out
 
     def gram_device(self, params, d_codes, d_lens, n, ldc, row0, row1, out_dtype, d_out, ld):
@@ -371,7 +386,7 @@ class Context:
         """How the last spectrum / mismatch call was built (include/kmgram.h kmg_last_plan)."""
         v = (ctypes.c_int32 * 5)()
         check(self.lib.kmg_last_plan(self._h, v))
-        names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines")
+        names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines", "generic")
         return {"formulation": names[v[0]] if 0 <= v[0] < len(names) else None,
                 "chunk": v[1], "nchunks": v[2], "triangle": bool(v[3]), "threads": v[4]}
 

@@ -174,20 +174,26 @@ class GramEngine:
             p = P.make(L.KMG_GAPPY, k=k, g=g, window=101, normalize=1,
                        la_mode=L.KMG_MODE_INTENDED)
             return self._run(p, seqs)
-        if g > k:
-            raise ValueError("r must be non-negative")  # itertools.combinations(..., k-g)
-        if not (k == 1 and g == 0) and any(len(s) > 0 for s in seqs):
-            # `b in gap_set` compares a length-k array with (k-g)-tuples (kernels.py:432):
-            # numpy 2 raises for every (k, g) except k=1, g=0.
-            if k - g == 0:
-                raise ValueError("The truth value of an empty array is ambiguous. Use "
-                                 "`array.size > 0` to check that an array is not empty.")
-            if k - g == k or k - g == 1:
-                raise ValueError("The truth value of an array with more than one element is "
-                                 "ambiguous. Use a.any() or a.all()")
-            raise ValueError(f"operands could not be broadcast together with shapes ({k},) "
-                             f"({k - g},) ")
+        for s in seqs:
+            gappy_reference_errors(len(s), k, g)
         return self._run(P.make(L.KMG_GAPPY, k=k, g=g, window=101), seqs)
+
+    # ------------------------------------------------------------------ feature maps
+    def features(self, kind, seqs, k, cols, m=0, g=0):
+        """float64 [len(seqs), len(cols)]: the reference's per-sequence feature map of each
+        sequence at the k-mer codes cols (uint32, base 4, first letter most significant;
+        0xFFFFFFFF = a beta no window can equal), on the device (kmg_features):
+        KMG_SPECTRUM get_phi_u (kernels.py:12-25), KMG_MISMATCH get_phi_km (161-175),
+        KMG_GAPPY gappy_k at k=1, g=0 (420-433)."""
+        codes, lens = E.encode(seqs)
+        p = P.make(kind, k=int(k), m=int(m), g=int(g), window=101)
+        return self.ctx.features(p, codes, lens, cols)
+
+    def substring_b_pair(self, x, y, lbda, k):
+        """B_k(lbda, k, x, y) of the substring kernel's recursion (kernels.py:322-342) at the
+        full strings, from the device sweep (la_mode KMG_MODE_SS_B)."""
+        p = P.make(L.KMG_SUBSTRING, k=int(k), lbda=lbda, la_mode=L.KMG_MODE_SS_B)
+        return float(self._run(p, [x, y])[0, 1])
 
     def normalize(self, K):
         """normalize_K (kernels.py:398-415) in place on a float64 C-contiguous matrix."""
@@ -196,6 +202,33 @@ class GramEngine:
     def center(self, K):
         """center_K (kernels.py:387-395)."""
         return self.ctx.center(np.ascontiguousarray(K, dtype=np.float64))
+
+
+def gappy_reference_errors(n_x, k, g, window=101):
+    """Raise what gappy_k (kernels.py:420-433) raises under numpy 2 for a sequence of
+    length n_x, before any work: combinations(x[i:i+k], k-g) refuses r = k-g < 0 once a
+    window exists, and `b in gap_set` compares a length-k beta array with each (k-g)-tuple:
+    the shapes (k,) and (r,) broadcast only when r == k, r == 1 or k == 1, and the result's
+    truth value is defined only for one element.  Returns quietly when gap_set is empty
+    (nothing is compared) or k=1, g=0."""
+    r = k - g
+    if window - k + 1 <= 0:
+        return  # no window: gap_set = []
+    if r < 0:
+        raise ValueError("r must be non-negative")
+    # the longest slice x[0:k] holds min(n_x, k) symbols: gap_set is non-empty iff r fits
+    if min(n_x, k) < r:
+        return
+    if r in (k, 1) or k == 1:
+        size = 0 if r == 0 else max(r, k)
+        if size == 1:
+            return
+        if size == 0 or r == 0:
+            raise ValueError("The truth value of an empty array is ambiguous. Use "
+                             "`array.size > 0` to check that an array is not empty.")
+        raise ValueError("The truth value of an array with more than one element is "
+                         "ambiguous. Use a.any() or a.all()")
+    raise ValueError(f"operands could not be broadcast together with shapes ({k},) ({r},) ")
 
 
 _default = None

@@ -123,6 +123,28 @@ def mismatch_raw(codes, lens, k, m, window=101):
     return K
 
 
+def mismatch_raw_windows(codes, lens, k, m, window=101):
+    """The C ABI's mismatch (k, m) over any rows (beyond the reference, which raises for
+    rows shorter than the window or holding a non-ACGT symbol, kernels.py:171-174, 193):
+    sum_{a,b} w[ham(x_a, y_b)] over the windows a, b < window - k + 1 that lie inside their
+    row and hold only A/C/G/T (the k <= 16 kernels' pk_window rule).  Explicit window
+    pairs, small cases only."""
+    w = mismatch_weights(k, m)
+    P = window - k + 1
+    wins = []
+    for i in range(len(lens)):
+        s = codes[i, : lens[i]].astype(np.int64)
+        ws = [s[a:a + k] for a in range(P) if a + k <= len(s) and np.all(s[a:a + k] < 4)]
+        wins.append(np.stack(ws) if ws else np.zeros((0, k), dtype=np.int64))
+    n = len(lens)
+    K = np.zeros((n, n), dtype=np.int64)
+    for i in range(n):
+        for j in range(i, n):
+            H = (wins[i][:, None, :] != wins[j][None, :, :]).sum(axis=2)
+            K[i, j] = K[j, i] = int(w[np.minimum(H, k)].sum()) if H.size else 0
+    return K
+
+
 def normalize(K):
     """normalize_K (kernels.py:398-415) on a copy: K_ij / (d_i * d_j), d = sqrt(diag),
     upper triangle mirrored, diagonal := 1; unchanged if K[0,0] == 1."""
@@ -266,6 +288,27 @@ def ss_pair(x, y, lbda, k):
         s = sum(Bk1[i - 1][c] for c in range(m) if y[c] == a)
         K = K + lam2 * s
     return K
+
+
+def ss_b(x, y, lbda, k):
+    """B_k(lbda, k, x, y) (kernels.py:322-342) by the bottom-up table of ss_pair: the level-k
+    value at the full prefixes; 1 for k = 0, 0 when a string is shorter than k."""
+    if k == 0:
+        return 1
+    n, m = len(x), len(y)
+    if n < k or m < k:
+        return 0
+    lam2 = lbda ** 2
+    prev = [[1] * (m + 1) for _ in range(n + 1)]
+    for t in range(1, k + 1):
+        Bt = [[0] * (m + 1) for _ in range(n + 1)]
+        for r in range(t, n + 1):
+            for c in range(t, m + 1):
+                v = lbda * Bt[r - 1][c] + lbda * Bt[r][c - 1] - lam2 * Bt[r - 1][c - 1]
+                v = v + (lam2 * prev[r - 1][c - 1] if x[r - 1] == y[c - 1] else 0)
+                Bt[r][c] = v
+        prev = Bt
+    return prev[n][m]
 
 
 def substring(codes, lens, lbda, k):
@@ -440,6 +483,29 @@ def spectrum_phi(codes, lens, k):
     valid = (np.arange(P)[None, :] <= (lens[:, None] - k)) & ~bad
     r, c = np.nonzero(valid)
     return sp.csr_matrix((np.ones(r.size, dtype=np.int32), (r, km[r, c])), shape=(n, 4 ** k))
+
+
+def phi_u(x, k, betas):
+    """get_phi_u (kernels.py:12-25) for one string: phi[j] = #{i : x[i:i+k] == betas[j]}."""
+    from collections import Counter
+    cnt = Counter(x[i:i + k] for i in range(len(x) - k + 1))
+    return np.array([float(cnt.get(b, 0)) for b in betas])
+
+
+def phi_km(x, k, m, betas):
+    """get_phi_km (kernels.py:161-175) for one format()ed row (len >= 101): phi[j] =
+    #{i < 101-k+1 : #(x[i:i+k] != betas[j]) <= m}."""
+    x = np.asarray(x).reshape(-1)
+    B = np.asarray(betas).reshape(len(betas), -1)
+    W = np.stack([x[i:i + k] for i in range(101 - k + 1)])       # windows x k
+    H = (W[:, None, :] != B[None, :, :]).sum(axis=2)                # windows x betas
+    return (H <= m).sum(axis=0).astype(np.float64)
+
+
+def gappy1_phi(x, betas):
+    """gappy_k(x, 1, 0, betas) (kernels.py:420-433): 1.0 where the letter occurs in x[0:101]."""
+    present = set(int(v) for v in np.asarray(x).reshape(-1)[:101])
+    return np.array([1.0 if int(np.asarray(b).reshape(-1)[0]) in present else 0.0 for b in betas])
 
 
 def neighbour_masks(k, m):

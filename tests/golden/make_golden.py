@@ -50,6 +50,30 @@ def _sha(a):
 
 
 # --------------------------------------------------------------------------- jobs
+FEATURE_FNS = ("get_phi_u", "get_phi_km", "gappy_k", "B_k")
+
+
+def feature_call(km, fn, kwargs, seqs):
+    """The reference's module-level feature maps called the way its own Gram functions
+    call them: get_phi_u on the string with string betas (kernels.py:37-40), get_phi_km and
+    gappy_k on format(x) with format()ed betas (kernels.py:206-210, 446-449), B_k on two
+    strings (kernels.py:322-342).  kwargs["betas"] == "canonical": all 4^k k-mers in
+    itertools.product order; otherwise the explicit list."""
+    from itertools import product
+    k = kwargs.get("k")
+    betas = kwargs.get("betas")
+    if fn == "get_phi_u":
+        b = [''.join(c) for c in product('ACGT', repeat=k)] if betas == "canonical" else list(betas)
+        return km.get_phi_u(seqs[0], k, b)
+    if fn == "B_k":
+        return np.array([km.B_k(kwargs["lbda"], k, seqs[0], seqs[1])], dtype=np.float64)
+    b = (np.array([km.format(''.join(c)) for c in product('ACGT', repeat=k)])
+         if betas == "canonical" else np.array(betas))
+    if fn == "get_phi_km":
+        return km.get_phi_km(km.format(seqs[0]), k, kwargs["m"], b)
+    return km.gappy_k(km.format(seqs[0]), k, kwargs["g"], b)
+
+
 def job(spec):
     """Run one reference call; returns (name, dict of arrays/meta)."""
     name, fn, kwargs, seqs = spec
@@ -61,6 +85,8 @@ def job(spec):
         try:
             if fn == "select_method":
                 K = km.select_method(X, kwargs["method"])
+            elif fn in FEATURE_FNS:  # module-level feature maps / the SS auxiliary
+                K = feature_call(km, fn, kwargs, seqs)
             elif fn in ("get_WD_d", "get_WDShifts_d"):  # one pair: (x, y, ..., L)
                 K = np.array([getattr(km, fn)(seqs[0], seqs[1], **kwargs)], dtype=np.float64)
             else:
@@ -140,12 +166,41 @@ def main():
     for meth in ("SP_k4", "WD_k5", "WD_d4", "MM_k4_m1", "WDS_d3_s1", "SS_l0.5_k2",
                  "LA_e11_d1_b0.5_smith0_eig0", "GP_k3_g1", "XX_k3"):
         jobs.append((f"select_{meth}_n6", "select_method", {"method": meth}, seqs[:6]))
+    # module-level feature maps and the SS auxiliary (kernels.py:12-25, 161-175, 308-342,
+    # 420-433), round 4
+    phx = [seqs[0], seqs[1][:50], "ACGTNACGT", "", "acgtACGT", seqs[2] + "ACGTTG", "A" * 30]
+    for xi, x in enumerate(phx):
+        for k in (1, 3, 5):
+            jobs.append((f"PHIU_x{xi}_k{k}", "get_phi_u", {"k": k, "betas": "canonical"}, [x]))
+    jobs.append(("PHIU_x0_k8", "get_phi_u", {"k": 8, "betas": "canonical"}, [seqs[0]]))
+    custom = ["ACG", "TTT", "AAA", "GA", "ACGT", "CCC", "GGG", "TGC", "ACG", ""]
+    for xi in (0, 2, 6):
+        jobs.append((f"PHIU_x{xi}_k3_custom", "get_phi_u", {"k": 3, "betas": custom}, [phx[xi]]))
+    kmx = [seqs[0], seqs[3] + "ACG", seqs[4][:50]]
+    for xi, x in enumerate(kmx):
+        for k, m in ((3, 0), (3, 1), (5, 1), (5, 2), (6, 1)):
+            jobs.append((f"PHIKM_x{xi}_k{k}_m{m}", "get_phi_km", {"k": k, "m": m, "betas": "canonical"}, [x]))
+    kcustom = [[1, 2, 3], [4, 4, 4], [2, 2, 1], [3, 1, 4]]
+    jobs.append(("PHIKM_x0_k3_m1_custom", "get_phi_km", {"k": 3, "m": 1, "betas": kcustom}, [kmx[0]]))
+    for xi, x in enumerate([seqs[0], "ACGA", "", seqs[5][:60]]):
+        jobs.append((f"GAPK_x{xi}_k1_g0", "gappy_k", {"k": 1, "g": 0, "betas": "canonical"}, [x]))
+    for k, g in ((3, 1), (3, 0), (2, 3), (3, 2), (3, 3), (1, 1)):
+        jobs.append((f"GAPK_x0_k{k}_g{g}", "gappy_k", {"k": k, "g": g, "betas": "canonical"}, [seqs[0]]))
+    jobs.append(("GAPK_xe_k3_g1", "gappy_k", {"k": 3, "g": 1, "betas": "canonical"}, [""]))
+    bpairs = [("ACGTAC", "GATTACA"), (seqs[0][:20], seqs[1][:25]), (seqs[2][:30], seqs[3][:30]),
+              ("AC", "ACGTAC"), ("ACGNAC", "NACGT"), (seqs[4][:40], seqs[4][:40])]
+    for pi, (x, y) in enumerate(bpairs):
+        for lb, k in ((0.5, 3), (0.7, 2), (1.0, 4), (0.5, 0), (0.3, 1)):
+            jobs.append((f"BK_p{pi}_l{lb}_k{k}", "B_k", {"lbda": lb, "k": k}, [x, y]))
+
     # config 1 (BASELINE configs[0]): SP k=6 on all of Xtr0
     jobs.append(("SP_k6_xtr0_full", "get_spectrum_K", {"k": 6}, seqs))
 
     only = set(sys.argv[1:])
     if only:
-        jobs = [j for j in jobs if j[0] in only]
+        # exact names, or prefixes ending in '*' (e.g. 'PHIU*')
+        jobs = [j for j in jobs if j[0] in only or
+                any(o.endswith("*") and j[0].startswith(o[:-1]) for o in only)]
     # longest first
     order = {"SP_k6_xtr0_full": 0, "MM_k9_m1_xtr0_n8": 1}
     jobs.sort(key=lambda j: order.get(j[0], 9))

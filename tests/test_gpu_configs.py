@@ -111,6 +111,62 @@ def test_config5_mismatch_k9_n200000_rank_slab(ctx, r0):
             ctx.dfree(p)
 
 
+def _row_sums_parallel(blk, pool):
+    """int64 row sums of an int32 block, split over a thread pool (numpy releases the GIL)."""
+    parts = np.array_split(np.arange(blk.shape[0]), 8)
+    return np.concatenate(list(pool.map(lambda r: blk[r].sum(axis=1, dtype=np.int64), parts)))
+
+
+def test_config5_mismatch_k9_n200000_full_one_gpu(ctx):
+    """BASELINE configs[4] on ONE GPU, the G=1 point of its strong-scaling line: the full
+    200000 x 200000 raw int32 K (160 GB) in one kmg_gram_device call -- the upper block
+    triangle of column chunks plus the in-place mirror (mirror_chunks_kernel, 64-bit
+    offsets past 2^32 entries).  Every row sum exact, the exact diagonal, oracle rows on both
+    sides of every chunk edge, symmetric 256 x 256 blocks straddling chunk edges, and the
+    plan the library reports (kernels.py:211-215: K[j, i] = K[i, j])."""
+    from concurrent.futures import ThreadPoolExecutor
+    n, k, piece = 200000, 9, 2000
+    codes, lens = E.synthetic(n, 101, seed=5)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_K = ctx.dmalloc(n * n * 4)
+    pool = ThreadPoolExecutor(8)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), d_codes,
+                        d_lens, n, codes.shape[1], 0, n, L.KMG_I32, d_K, n)
+        ctx.synchronize()
+        plan = ctx.last_plan()
+        assert plan["formulation"] in ("slots", "pair_lines") and plan["triangle"], plan
+        assert plan["nchunks"] >= 2 and plan["chunk"] * plan["nchunks"] >= n, plan
+        ch = plan["chunk"]
+        edges = [c * ch for c in range(1, plan["nchunks"]) if c * ch < n]
+        sums = I.mismatch1_row_sums(codes, k)
+        diag = cref.mismatch_diag(codes, lens, k, 1)
+        buf = np.empty((piece, n), dtype=np.int32)
+        for a in range(0, n, piece):
+            blk = _fetch_rows(ctx, d_K, a, a + piece, n, np.int32, buf)
+            assert np.array_equal(_row_sums_parallel(blk, pool), sums[a:a + piece]), a
+            assert np.array_equal(blk[np.arange(piece), a + np.arange(piece)].astype(np.int64),
+                                  diag[a:a + piece]), a
+        # oracle rows on both sides of every chunk edge (and the first / last row)
+        pairs = [(e - 1, e + 1) for e in edges] + [(0, 1), (n - 1, n)]
+        refs = list(pool.map(lambda ab: cref.mismatch_raw(codes, lens, k, 1, rows=ab), pairs))
+        for (a, b), ref in zip(pairs, refs):
+            got = _fetch_rows(ctx, d_K, a, b, n, np.int32)
+            assert np.array_equal(got.astype(np.int64), ref), (a, b)
+        # symmetric blocks straddling chunk edges (mirrored entries against computed ones)
+        for e0, e1 in zip(edges, edges[1:] + [edges[0]]):
+            a, b = e0 - 128, e1 - 128
+            A = _fetch_rows(ctx, d_K, a, a + 256, n, np.int32)
+            B = _fetch_rows(ctx, d_K, b, b + 256, n, np.int32)
+            assert np.array_equal(A[:, b:b + 256], B[:, a:a + 256].T), (a, b)
+    finally:
+        pool.shutdown()
+        for p in (d_K, d_codes, d_lens):
+            ctx.dfree(p)
+
+
 def test_mismatch_k9_n20000_row_sums(ctx):
     """BASELINE configs[2] at full size: the raw (9,1) Gram of all 20000 rows, every row
     sum exact, symmetric, exact self-kernels from the oracle's diagonal."""

@@ -55,3 +55,18 @@ def test_bench_gather_model_matches_pmc():
     for w in (2, 4, 8):
         n = weak_scaled_n(100000, w)
         assert abs(n * n / w - 1e10) / 1e10 < 1e-3
+
+
+def test_bench_headline_projection_is_strong_at_named_n():
+    """At G > 1 the headline keeps N = 100000 (strong scaling): the projection bench.py
+    emits for it is index + gram / G at that N."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    sp = {"ms_per_step": 6.5, "write_ceiling_GBps": 6100.0,
+          "stages_ms": {"count": 0.05, "scan": 0.01, "place": 0.04, "fine": 0.03, "pack": 0.0,
+                        "gram": 6.3}}
+    p = bench.projection(sp, 100000, None)["headline_strong_collective_free"]
+    for g in ("2", "4", "8"):
+        assert p[g]["N"] == 100000
+        assert abs(p[g]["ms_model"] - (0.13 + 6.3 / int(g))) < 1e-9
+    assert p["8"]["speedup_model"] > 6.0
