@@ -105,7 +105,10 @@ struct Tuning {
   int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
   int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
   int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table,
-                            // 3 drop-two pair lines (kmg_pairs.hip)
+                            // 3 drop-two pair lines (kmg_pairs.hip), 4 neighbourhood lists
+                            // (kmg_nbhd.hip)
+  int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
+                            // (0 auto)
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
                             // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
@@ -162,6 +165,8 @@ void read_tuning(Tuning &t) {
   t.ss_lpp = env_or("KMG_SS_LPP", d.ss_lpp);
   t.pl_threads = env_or("KMG_PL_THREADS", d.pl_threads);
   if (t.pl_threads != 512 && t.pl_threads != 1024) t.pl_threads = 0;
+  t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
+  if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
@@ -194,6 +199,7 @@ struct kmg_ctx {
   int32_t plan[5] = {-1, 0, 0, 0, 0};  // last spectrum / mismatch call (kmg_last_plan)
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   DevBuf pr_big;                  // pair lines: blocks with groups past the small image
+  DevBuf nb_seg, nb_lines;        // neighbourhood lists: segment ends, the lists
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -595,6 +601,41 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
   return (int)std::max<int64_t>(8, best);
 }
 
+// Columns per chunk of the neighbourhood-list Gram (kmg_nbhd.hip).  A row reads, per chunk,
+// its windows' lists: ~2 B x (1 + 3k + 9k(k-1)/2) x P x chunk x P / 4^k plus three padded
+// segment tails per list, so the chunk count barely changes the bytes a full row reads; it
+// only matters for a square K built by its upper block triangle (tri_esz > 0), where a row
+// reads (nch + 1) / (2 nch) of them and writes as much of its K row, and the mirror moves
+// 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
+// mirror; the largest chunk is the int32 LDS accumulator beside the row tables.
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads) {
+  const int64_t lds_words = (threads == 512 ? 80 : 160) * 1024 / 4;
+  int64_t max_chunk = (lds_words - 64 - 4 * (int64_t)pmax - 1 - ldp - 8) & ~7LL;
+  max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
+  if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
+  if (max_chunk < 8) return 8;
+  const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
+  const int64_t nb = 1 + 3 * k + 9 * (int64_t)k * (k - 1) / 2;
+  const double dens = (double)pmax / (double)pow4(k);  // occurrences of a k-mer per column
+  const int esz = tri_esz > 0 ? tri_esz : 4;
+  int64_t best = std::min<int64_t>(std::max<int64_t>(n, 8), max_chunk);
+  double best_cost = 1e300;
+  for (int64_t nch = nch0; nch <= (tri_esz > 0 ? nch0 + 8 : nch0); ++nch) {
+    const int64_t ch = ((n + nch - 1) / nch + 7) & ~7LL;
+    if (ch > max_chunk) continue;
+    const double f = tri_esz > 0 ? (double)(nch + 1) / (2.0 * nch) : 1.0;
+    const double row_reads = 2.0 * nb * pmax * dens * (double)n + 2.0 * 10.5 * pmax * nch;
+    const double gram = (double)n * (row_reads + esz * (double)n) * f;
+    const double mirror = tri_esz > 0 ? 2.0 * esz * (double)n * n * (double)(nch - 1) / (2.0 * nch) : 0.0;
+    const double cost = gram / 6e12 + mirror / 5e12;
+    if (cost < best_cost * (1.0 - 1e-12)) {
+      best_cost = cost;
+      best = ch;
+    }
+  }
+  return (int)std::max<int64_t>(8, best);
+}
+
 // Row ranges of one Gram call: every range [row0, row1) x all n columns is written at
 // `out` (row row0); the index / features / diagonal are built once per call.  `after(q)`
 // runs once range q's Gram launch is enqueued (the multi-GPU path hangs its all-gather of a
@@ -793,8 +834,8 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 // ----------------------------------------------------------------- dispatch
 // Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
 // kmg_gram_blocks' choice of the round-slab format).
-enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL };
-constexpr int32_t KMG_PLAN_GENERIC = 6;  // kmg_last_plan: the per-pair kernels of k > 16
+enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL, SM_NB };
+constexpr int32_t KMG_PLAN_GENERIC = 7;  // kmg_last_plan: the per-pair kernels of k > 16
 SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
@@ -807,12 +848,13 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   //   k = 8 and 12: the drop-one slot table (k = 8: 6.70 vs 7.78 pair lines, 15.8 pairs).
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
+  const bool use_nb = s1 && k >= 3 && k <= 12 && form == 4;
   const bool use_pl =
-      s1 && k >= 3 && k <= 12 && (form == 3 || (form == 0 && k == 9 && n <= 24000));
-  const bool use_pairs =
-      s1 && !use_pl && (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
-  const bool use_slots = s1 && !use_pairs && !use_pl && k >= 8 && k <= 12 && form != 2;
-  const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_pl;
+      s1 && !use_nb && k >= 3 && k <= 12 && (form == 3 || (form == 0 && k == 9 && n <= 24000));
+  const bool use_pairs = s1 && !use_pl && !use_nb &&
+                         (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
+  const bool use_slots = s1 && !use_pairs && !use_pl && !use_nb && k >= 8 && k <= 12 && form != 2;
+  const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_pl || use_nb;
   // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
   // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
   // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
@@ -824,6 +866,7 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   if (!use_index) return SM_HAMMING;
   if (use_pairs) return SM_PAIRS;
   if (use_pl) return SM_PL;
+  if (use_nb) return SM_NB;
   return exact ? SM_POSTING : SM_SLOTS;
 }
 
@@ -950,13 +993,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const SmPath path = sm_path(c->tune, p, g.pmax, n);
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS, use_pl = path == SM_PL;
-      const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl;
+      const bool use_nb = path == SM_NB;
+      const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl || use_nb;
       // a full square K (one range over [0, n), every column written) of a mismatch
       // posting-list formulation: built by its upper block triangle, then mirrored
       // (OutSpec::tri; set below once the chunking is known)
       const bool square = ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
                           ranges[0].col_lo == 0 && !after && !narrow && n > 0;
-      const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_pl))
+      const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_pl || use_nb))
                               ? (int)dtype_size(dt) : 0;
       auto mirror = [&]() -> int {
         if (!o.tri) return KMG_OK;
@@ -1138,6 +1182,50 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                           c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
                                           c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
                                           (int)w[2], oq, c->stream, 4, c->tune.pl_dbg, plt);
+        }, true));
+        return mirror();
+      }
+      if (use_nb) {
+        // exact k-mer index over the mismatch window (kernels.py:171), then every (chunk,
+        // k-mer)'s neighbourhood list assembled from it (kmg_nbhd.hip)
+        g.copies = 1;
+        g.nkeys = (uint32_t)pow4(k);
+        const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
+        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt));
+        o.tri = tri_esz > 0 && g.nchunks > 1;
+        note_plan(nbt);
+        KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
+        const int64_t nbins = g.nbins();
+        const int64_t bound = nb_list_entries_bound(k, n * (int64_t)g.pmax, nbins);
+        if (bound / 8 + nbins >= 0xFFFFFFF0LL)
+          return fail(KMG_EUNSUPPORTED, "neighbourhood lists: more than 2^32 pieces");
+        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nbins)));
+        KMG_TRY(c->nb_seg.ensure(sizeof(uint2) * (size_t)nbins));
+        KMG_TRY(c->nb_lines.ensure(sizeof(uint16_t) * (size_t)(bound + 8)));
+        {
+          StageTimer t(c, ST_SLOTS);
+          KMG_HIP(launch_nb_build(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                  c->pr_rtot.as<uint32_t>(), c->pr_rbase.as<uint32_t>(),
+                                  c->pr_cursor.as<uint32_t>(), c->nb_seg.as<uint2>(),
+                                  c->partials.as<uint32_t>(), c->nb_lines.as<uint16_t>(),
+                                  c->stream));
+        }
+        if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
+          KMG_TRY(upload_wtab(c, w));
+          KMG_TRY(diag_hamming(c, g, pkd));
+          if (p->normalize) {
+            o.normalize = 1;
+            o.diagv = c->diagv.as<double>();
+            o.dsq = c->dsq.as<double>();
+          }
+        }
+        KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+          return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
+                                          c->nb_lines.as<uint4>(), r0, r1, (int)w[0], (int)w[1],
+                                          (int)w[2], oq, c->stream, nbt);
         }, true));
         return mirror();
       }
@@ -1413,7 +1501,8 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
-                    &c->gcoef, &c->feat32, &c->k32, &c->ft_cols};
+                    &c->gcoef, &c->feat32, &c->k32, &c->ft_cols,
+                    &c->nb_seg, &c->nb_lines};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);

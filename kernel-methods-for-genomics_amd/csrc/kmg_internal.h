@@ -268,6 +268,19 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
                                     hipStream_t s, int depth = 4, int dbg = 0,
                                     int threads = 1024);
+// mismatch (k, 1), 3 <= k <= 12, through neighbourhood lists (kmg_nbhd.hip): from the exact
+// index (xoff / xent over [chunk][4^k]) every (chunk, k-mer)'s list of the column windows at
+// Hamming distance 0 | 1 | 2 (uint16 columns, 3 segments padded to 8); hist / nboff / cursor
+// nbins + 1 words, nbseg nbins, table nb_list_entries_bound(...) uint16
+int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins);
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk);
+hipError_t launch_nb_build(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
+                           uint32_t *hist, uint32_t *nboff, uint32_t *cursor, uint2 *nbseg,
+                           uint32_t *partials, uint16_t *table, hipStream_t s);
+hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
+                                    const uint2 *nbseg, const uint4 *table, int64_t row0,
+                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                    hipStream_t s, int threads);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -1,0 +1,364 @@
+// kmg_nbhd.hip — mismatch (k, 1) Gram through NEIGHBOURHOOD LISTS (gfx950).
+//
+// get_mismatch_K (kernels.py:196-217) reduces to the closed form
+//   K(x, y) = sum_{a, b} w[ham(x_a, y_b)],  w = (1 + 3k, 4, 2) for m = 1
+// (kmgram.params.mismatch_weights), i.e. for row i's window k-mer u every column window at
+// Hamming distance <= 2 of u adds w[ham] to its column.  The drop-one slot table and the
+// drop-two pair lines (kmg_gram.hip, kmg_pairs.hip) read those column windows as many
+// short posting groups (117 or 36 random 128-byte lines a window and chunk, 1.6-2x the
+// entries a window needs: a Hamming-1 neighbour sits in k - 1 pair groups, Hamming 0 in all
+// of them).  This formulation materialises, once per build, for every (column chunk c,
+// k-mer u) the NEIGHBOURHOOD LIST of u:
+//
+//   [ occurrences of u | of its 3k Hamming-1 neighbours | of its 9 k(k-1)/2 Hamming-2 ]
+//
+// as uint16 columns inside the chunk, each of the three segments padded to whole 16-byte
+// pieces (8 columns) with dummy columns (LDS words past the accumulator).  Every column
+// window then appears exactly once per list, and a row window reads ONE contiguous list
+// (N=200000, k=9: ~25000 entries, 50 KB over all chunks) instead of 117 random lines per
+// chunk: the Gram kernel streams HBM, 16 bytes a lane, 1 KB per wave instruction.
+//
+//   nb_count_kernel   per (c, u): n0, n1, n2 from the exact index (1 + 3k + 9k(k-1)/2
+//                     lookups of its bin offsets, L2-resident) -> pieces and segment ends
+//   launch_scan       list starts (in pieces; < 2^32: checked by the host)
+//   nb_fill_kernel    per (c, u), one 256-thread workgroup: block scan of the neighbour
+//                     counts, copy of each neighbour's posting list into its slot of the list
+//                     (staged in LDS and written with 16-byte stores when it fits)
+//   gram_nb_kernel    per (row i, chunk c): row windows -> (list start, pieces, segment
+//                     ends) in LDS, a prefix sum over the row's lists, then every wave streams
+//                     an equal share of the row's pieces (four 16-byte loads in flight per
+//                     lane), adding the segment's weight for each of the 8 columns of a piece
+//                     into the LDS accumulator; fused normalize_K epilogue (emit_row).
+//
+// Roofline: the lists are read from HBM once per (row, chunk) -- 2 B per (row window,
+// neighbour occurrence): N=20000 ~466 KB a row against the 160 KB float64 K row; the bound is
+// HBM (table reads + K writes), not the Infinity-Cache line rate of the table formulations.
+#include "kmg_rowacc.h"
+
+namespace kmg {
+
+namespace {
+constexpr int NB_FILL_THREADS = 256;
+constexpr int NB_STAGE = 12288;  // entries of one list staged in LDS by nb_fill_kernel (24 KB)
+constexpr int NB_UNROLL = 4;     // 16-byte pieces in flight per lane in gram_nb_kernel
+
+__device__ __forceinline__ int nb_neighbours(int k) { return 1 + 3 * k + 9 * k * (k - 1) / 2; }
+
+// neighbour t of u (t < nb_neighbours(k)) and its segment: t = 0 u itself; then the 3k
+// Hamming-1 k-mers (position p, letter xor d = 1..3); then the Hamming-2 k-mers of the pairs
+// p < q in order (0,1), (0,2), (1,2), (0,3), ... (q-major), 9 letter xors each
+__device__ __forceinline__ uint32_t nb_neighbour(uint32_t u, int k, int t, int &seg) {
+  if (t == 0) {
+    seg = 0;
+    return u;
+  }
+  t -= 1;
+  if (t < 3 * k) {
+    seg = 1;
+    const int p = t / 3, d = t - 3 * p + 1;
+    return u ^ ((uint32_t)d << (2 * (k - 1 - p)));
+  }
+  seg = 2;
+  t -= 3 * k;
+  const int pi = t / 9, r = t - 9 * pi;
+  int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);  // pi = q(q-1)/2 + p
+  while (q * (q - 1) / 2 > pi) --q;
+  while ((q + 1) * q / 2 <= pi) ++q;
+  const int p = pi - q * (q - 1) / 2;
+  const int d1 = r / 3 + 1, d2 = r - 3 * (r / 3) + 1;
+  return u ^ ((uint32_t)d1 << (2 * (k - 1 - p))) ^ ((uint32_t)d2 << (2 * (k - 1 - q)));
+}
+
+__device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+}  // namespace
+
+// per (chunk, k-mer): pieces of its neighbourhood list and the segment ends (in pieces)
+__global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
+                                                       const uint32_t *__restrict__ xoff,
+                                                       uint32_t *__restrict__ hist,
+                                                       uint2 *__restrict__ seg) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbins) return;
+  const uint32_t nkeys = 1u << (2 * k);
+  const uint32_t u = (uint32_t)b & (nkeys - 1u);
+  const uint32_t *off = xoff + (b - u);
+  auto cnt = [&](uint32_t v) { return off[v + 1] - off[v]; };
+  const uint32_t n0 = cnt(u);
+  uint32_t n1 = 0, n2 = 0;
+  for (int p = 0; p < k; ++p) {
+    const int sp = 2 * (k - 1 - p);
+#pragma unroll
+    for (uint32_t d = 1; d <= 3; ++d) n1 += cnt(u ^ (d << sp));
+    for (int q = p + 1; q < k; ++q) {
+      const int sq = 2 * (k - 1 - q);
+#pragma unroll
+      for (uint32_t d1 = 1; d1 <= 3; ++d1)
+#pragma unroll
+        for (uint32_t d2 = 1; d2 <= 3; ++d2) n2 += cnt(u ^ (d1 << sp) ^ (d2 << sq));
+    }
+  }
+  const uint32_t p0 = (n0 + 7) >> 3, p1 = (n1 + 7) >> 3, p2 = (n2 + 7) >> 3;
+  hist[b] = p0 + p1 + p2;
+  seg[b] = make_uint2(p0, p0 + p1);
+}
+
+// one workgroup per (chunk, k-mer): the neighbourhood list into table[nboff[b] * 8 ..]
+__global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
+    int k, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
+    uint32_t pad_col) {
+  __shared__ __align__(16) uint16_t stage[NB_STAGE];
+  __shared__ uint32_t wsum[NB_FILL_THREADS / 64];
+  __shared__ uint32_t pre2;
+  const int64_t b = blockIdx.x;
+  const uint32_t nkeys = 1u << (2 * k);
+  const uint32_t u = (uint32_t)b & (nkeys - 1u);
+  const uint32_t *off = xoff + (b - u);
+  const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+  if (tot == 0) return;  // block-uniform
+  const uint2 sg = nbseg[b];
+  const int nbn = nb_neighbours(k);
+  const int per = (nbn + NB_FILL_THREADS - 1) / NB_FILL_THREADS;  // <= 3 (k <= 12)
+  const int t0 = threadIdx.x * per;
+  uint32_t cnt[3], src[3];
+  int sgm[3];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    cnt[j] = 0;
+    src[j] = 0;
+    sgm[j] = 0;
+    if (j < per && t0 + j < nbn) {
+      const uint32_t v = nb_neighbour(u, k, t0 + j, sgm[j]);
+      src[j] = off[v];
+      cnt[j] = off[v + 1] - src[j];
+    }
+    s += cnt[j];
+  }
+  // block exclusive scan of the per-thread sums (neighbour order = list order)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t inc = nb_wave_incl_scan(s);
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t run = inc - s;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+  // the unpadded prefix where segment 2 starts (neighbour index 1 + 3k)
+  {
+    uint32_t r = run;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j < per && t0 + j == 1 + 3 * k) pre2 = r;
+      r += cnt[j];
+    }
+  }
+  uint32_t total = 0;
+  for (int w = 0; w < NB_FILL_THREADS / 64; ++w) total += wsum[w];
+  if (1 + 3 * k >= nbn) pre2 = total;  // (k = 0 never reaches here)
+  __syncthreads();
+  const uint32_t n0 = off[u + 1] - off[u], p2s = pre2;
+  const uint32_t segbase[3] = {0u, sg.x * 8u, sg.y * 8u};
+  const uint32_t segpre[3] = {0u, n0, p2s};
+  const uint32_t segn[3] = {n0, p2s - n0, total - p2s};
+  const uint32_t segend[3] = {sg.x * 8u, sg.y * 8u, tot * 8u};
+  const bool lds = tot * 8u <= (uint32_t)NB_STAGE;
+  uint16_t *gdst = table + (size_t)start * 8u;
+  auto put = [&](uint32_t pos, uint16_t v) {
+    if (lds)
+      stage[pos] = v;
+    else
+      gdst[pos] = v;
+  };
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (cnt[j]) {
+      const uint32_t d = segbase[sgm[j]] + (run - segpre[sgm[j]]);
+      for (uint32_t e = 0; e < cnt[j]; ++e) put(d + e, xent[src[j] + e]);
+    }
+    run += cnt[j];
+  }
+  // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+  if (threadIdx.x < 24) {
+    const int sgi = threadIdx.x >> 3, e = threadIdx.x & 7;
+    const uint32_t pos = segbase[sgi] + segn[sgi] + (uint32_t)e;
+    if (pos < segend[sgi]) put(pos, (uint16_t)(pad_col + (pos & 63u)));
+  }
+  if (lds) {
+    __syncthreads();
+    uint4 *g4 = (uint4 *)gdst;
+    const uint4 *s4 = (const uint4 *)stage;
+    for (uint32_t q = threadIdx.x; q < tot; q += NB_FILL_THREADS) g4[q] = s4[q];
+  }
+}
+
+// One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
+// triangle for a full square K).
+template <int K>
+__global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
+                                                       const uint32_t *__restrict__ nboff,
+                                                       const uint2 *__restrict__ nbseg,
+                                                       const uint4 *__restrict__ table,
+                                                       int64_t row0, int64_t rows, int w0, int w1,
+                                                       int w2, OutSpec o) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  int c;
+  int64_t il;
+  rowacc_block(g, o, row0, rows, c, il);
+  const int64_t i = row0 + il;
+  const int64_t col0 = (int64_t)c * g.chunk;
+  const int cw = (int)min((int64_t)g.chunk, g.n - col0);
+  if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int P = g.pmax;
+  int32_t *acc = (int32_t *)smem;     // [accw] + 64 dummy words (list padding)
+  uint32_t *wst = smem + accw + 64;   // [P] list start of window a (pieces)
+  uint32_t *wcum = wst + P;           // [P + 1] pieces of windows < a
+  uint32_t *ws0 = wcum + P + 1;       // [P] end of segment 0 (pieces, list-relative)
+  uint32_t *ws1 = ws0 + P;            // [P] end of segment 1
+  uint32_t *srec = ws1 + P;           // packed row record
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  uint4 *acc4 = (uint4 *)acc;
+  for (int w = threadIdx.x; w < (accw >> 2) + 16; w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  stage_record(pk, i, srec);
+  __syncthreads();
+  const uint32_t cbase = (uint32_t)c << (2 * K);
+  for (int a = threadIdx.x; a < P; a += blockDim.x) {
+    const uint32_t u = pk_window(srec, pk.cw, a, K);
+    uint32_t st = 0, n = 0, s0 = 0, s1 = 0;
+    if (u != KMG_INVALID) {
+      const uint32_t b = cbase + u;
+      st = nboff[b];
+      n = nboff[b + 1] - st;
+      const uint2 sg = nbseg[b];
+      s0 = sg.x;
+      s1 = sg.y;
+    }
+    wst[a] = st;
+    wcum[a + 1] = n;
+    ws0[a] = s0;
+    ws1[a] = s1;
+  }
+  __syncthreads();
+  if (wave == 0) {  // inclusive prefix of wcum[1 .. P] (one wave, contiguous runs a lane)
+    const int per = (P + 63) >> 6, lo = lane * per, hi = min(P, lo + per);
+    uint32_t s = 0;
+    for (int a = lo; a < hi; ++a) s += wcum[a + 1];
+    uint32_t run = nb_wave_incl_scan(s) - s;
+    for (int a = lo; a < hi; ++a) {
+      run += wcum[a + 1];
+      wcum[a + 1] = run;
+    }
+    if (lane == 0) wcum[0] = 0;
+  }
+  __syncthreads();
+  // this wave's share of the row's pieces; lane l takes pieces qb + l, qb + l + 64, ...
+  const uint32_t T = wcum[P];
+  const uint32_t qb = (uint32_t)(((uint64_t)T * wave) / nw), qe = (uint32_t)(((uint64_t)T * (wave + 1)) / nw);
+  uint32_t q = qb + lane;
+  int a = 0;  // window of piece q: the last a with wcum[a] <= q
+  {
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (wcum[mid] <= q) lo = mid;
+      else hi = mid - 1;
+    }
+    a = lo;
+  }
+  uint32_t abeg = wcum[a], aend = wcum[a + 1], ast = wst[a], as0 = ws0[a], as1 = ws1[a];
+  for (; q < qe; q += 64 * NB_UNROLL) {
+    uint4 v[NB_UNROLL];
+    int wt[NB_UNROLL];
+#pragma unroll
+    for (int t = 0; t < NB_UNROLL; ++t) {
+      const uint32_t qq = q + 64u * t;
+      wt[t] = 0;
+      if (qq < qe) {
+        while (qq >= aend) {
+          ++a;
+          abeg = aend;
+          aend = wcum[a + 1];
+          ast = wst[a];
+          as0 = ws0[a];
+          as1 = ws1[a];
+        }
+        const uint32_t rel = qq - abeg;
+        v[t] = table[(uint64_t)ast + rel];
+        wt[t] = rel < as0 ? w0 : rel < as1 ? w1 : w2;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NB_UNROLL; ++t) {
+      if (wt[t]) {
+        const uint32_t x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          atomicAdd(&acc[x[h] & 0xFFFFu], wt[t]);
+          atomicAdd(&acc[x[h] >> 16], wt[t]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  emit_row<true>(o, il, i, col0, cw, (const int32_t *)acc, norm);
+}
+
+int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
+  return (int64_t)(1 + 3 * k + 9 * k * (k - 1) / 2) * occurrences + 21 * nbins;
+}
+
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk) {
+  return (size_t)((((g.chunk + 3) >> 2) << 2) + 64 + 4 * g.pmax + 1 + pk.ldp) * 4;
+}
+
+hipError_t launch_nb_build(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
+                           uint32_t *hist, uint32_t *nboff, uint32_t *cursor, uint2 *nbseg,
+                           uint32_t *partials, uint16_t *table, hipStream_t s) {
+  const int64_t nbins = g.nbins();
+  if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(nb_count_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, g.k,
+                     nbins, xoff, hist, nbseg);
+  hipError_t e = launch_scan(hist, nboff, cursor, nbins, partials, s);
+  if (e != hipSuccess) return e;
+  const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
+  hipLaunchKernelGGL(nb_fill_kernel, dim3((unsigned)nbins), dim3(NB_FILL_THREADS), 0, s, g.k, xoff,
+                     xent, nboff, nbseg, table, pad_col);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
+                                    const uint2 *nbseg, const uint4 *table, int64_t row0,
+                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
+                                    hipStream_t s, int threads) {
+  const int64_t rows = row1 - row0;
+  if (rows <= 0 || g.n == 0) return hipSuccess;
+  if (g.k < 3 || g.k > 12 || g.copies != 1) return hipErrorNotSupported;
+  if (threads != 512 && threads != 1024) return hipErrorInvalidValue;
+  const int64_t nblk = rowacc_blocks(g, o, row0, rows);
+  if (nblk * threads >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
+  if (g.chunk + 64 + 63 >= 65536) return hipErrorInvalidValue;      // uint16 columns + dummies
+  const size_t lds = nb_gram_lds(g, pk);
+  if (lds > (threads == 512 ? 80 : 160) * 1024) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nblk);
+  switch (g.k) {
+#define KMG_NB(KK)                                                                              \
+  case KK:                                                                                      \
+    hipLaunchKernelGGL((gram_nb_kernel<KK>), grid, dim3(threads), lds, s, g, pk, nboff, nbseg,  \
+                       table, row0, rows, w0, w1, w2, o);                                       \
+    break;
+    KMG_NB(3) KMG_NB(4) KMG_NB(5) KMG_NB(6) KMG_NB(7) KMG_NB(8) KMG_NB(9) KMG_NB(10) KMG_NB(11)
+    KMG_NB(12)
+#undef KMG_NB
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kmg

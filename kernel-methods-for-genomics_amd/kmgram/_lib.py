@@ -386,7 +386,8 @@ class Context:
         """How the last spectrum / mismatch call was built (include/kmgram.h kmg_last_plan)."""
         v = (ctypes.c_int32 * 5)()
         check(self.lib.kmg_last_plan(self._h, v))
-        names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines", "generic")
+        names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines", "neighbourhood",
+                 "generic")
         return {"formulation": names[v[0]] if 0 <= v[0] < len(names) else None,
                 "chunk": v[1], "nchunks": v[2], "triangle": bool(v[3]), "threads": v[4]}
 

@@ -68,12 +68,14 @@ def test_config4_spectrum_k8_n100000(ctx):
             ctx.dfree(p)
 
 
+@pytest.mark.parametrize("form", ["0", "4"])
 @pytest.mark.parametrize("r0", [0, 100000])
-def test_config5_mismatch_k9_n200000_rank_slab(ctx, r0):
+def test_config5_mismatch_k9_n200000_rank_slab(ctx, tune, r0, form):
     """BASELINE configs[4] per-GPU share: rows [r0, r0 + 25000) of the N=200000 mismatch
     (9,1) Gram (ranks 0 and 4 of 8).  Raw int32 counts: every row sum exact (<Phi_i, C>),
     oracle rows at the slab edges, a symmetric block inside the slab; then the normalised
     float64 rows at the slab edges bit-exact against the oracle."""
+    tune(KMG_MM_FORM=form)
     n, k, rows, piece = 200000, 9, 25000, 2500
     codes, lens = E.synthetic(n, 101, seed=5)
     sums = I.mismatch1_row_sums(codes, k, rows=(r0, r0 + rows))
@@ -117,7 +119,8 @@ def _row_sums_parallel(blk, pool):
     return np.concatenate(list(pool.map(lambda r: blk[r].sum(axis=1, dtype=np.int64), parts)))
 
 
-def test_config5_mismatch_k9_n200000_full_one_gpu(ctx):
+@pytest.mark.parametrize("form", ["0", "4"])
+def test_config5_mismatch_k9_n200000_full_one_gpu(ctx, tune, form):
     """BASELINE configs[4] on ONE GPU, the G=1 point of its strong-scaling line: the full
     200000 x 200000 raw int32 K (160 GB) in one kmg_gram_device call -- the upper block
     triangle of column chunks plus the in-place mirror (mirror_chunks_kernel, 64-bit
@@ -125,6 +128,7 @@ def test_config5_mismatch_k9_n200000_full_one_gpu(ctx):
     sides of every chunk edge, symmetric 256 x 256 blocks straddling chunk edges, and the
     plan the library reports (kernels.py:211-215: K[j, i] = K[i, j])."""
     from concurrent.futures import ThreadPoolExecutor
+    tune(KMG_MM_FORM=form)
     n, k, piece = 200000, 9, 2000
     codes, lens = E.synthetic(n, 101, seed=5)
     d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
@@ -137,7 +141,7 @@ def test_config5_mismatch_k9_n200000_full_one_gpu(ctx):
                         d_lens, n, codes.shape[1], 0, n, L.KMG_I32, d_K, n)
         ctx.synchronize()
         plan = ctx.last_plan()
-        assert plan["formulation"] in ("slots", "pair_lines") and plan["triangle"], plan
+        assert plan["formulation"] in ("slots", "pair_lines", "neighbourhood") and plan["triangle"], plan
         assert plan["nchunks"] >= 2 and plan["chunk"] * plan["nchunks"] >= n, plan
         ch = plan["chunk"]
         edges = [c * ch for c in range(1, plan["nchunks"]) if c * ch < n]

@@ -45,17 +45,17 @@ def test_phi_u_random_rows():
 def test_phi_km_random_rows(k, m):
     rng = np.random.default_rng(100 + k)
     x = rng.integers(1, 5, size=120)
-    if k == 7:
-        x[30] = 0  # a symbol outside 1..4 mismatches every letter
     betas = rng.integers(1, 5, size=(3000, k))
     betas[:50] = np.stack([x[a:a + k] for a in range(50)])  # exact hits
+    if k == 7:
+        x[30] = 0  # a symbol outside 1..4 mismatches every letter
     got = km.get_phi_km(x, k, m, betas)
     assert np.array_equal(got, cpu_ref.phi_km(x, k, m, betas))
     assert got[:50].min() >= 1
 
 
 def test_gappy_k_letters():
-    x = F.fmt("ACCA" * 20 + "G" + "T" * 40)  # T only past position 101
+    x = F.fmt("ACCA" * 25 + "G" + "T" * 40)  # T only past x[0:101]
     b = np.array([[1], [2], [3], [4]])
     assert np.array_equal(km.gappy_k(x, 1, 0, b), np.array([1.0, 1.0, 1.0, 0.0]))
 
@@ -89,13 +89,31 @@ def test_mismatch_generic_ragged_and_non_acgt(ctx):
     codes[2, 60:] = 0xEE            # padding bytes past the row must never be read
     for k, m in ((17, 1), (20, 2)):
         ref = cpu_ref.mismatch_raw_windows(codes, lens, k, m)
-        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=0), codes, lens,
-                       L.KMG_I32)
+        # (the host path kmg_gram refuses rows shorter than the window, as the reference
+        # does; the device-resident path takes them)
+        raw = _gram_device(ctx, P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=0),
+                           codes, lens, L.KMG_I32)
         assert np.array_equal(raw.astype(np.int64), ref), k
         assert ctx.last_plan()["formulation"] == "generic"
-        Kn = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=1), codes, lens,
-                      L.KMG_F64)
+        Kn = _gram_device(ctx, P.make(L.KMG_MISMATCH, k=k, m=m, window=101, normalize=1),
+                          codes, lens, L.KMG_F64)
         assert np.array_equal(Kn, cpu_ref.normalize(ref.astype(np.float64)), equal_nan=True)
+
+
+def _gram_device(ctx, params, codes, lens, dt):
+    n, ldc = codes.shape
+    out = np.empty((n, n), dtype=L.DTYPES[dt])
+    d_codes, d_lens, d_out = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes), ctx.dmalloc(out.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device(params, d_codes, d_lens, n, ldc, 0, n, dt, d_out, n)
+        ctx.synchronize()
+        ctx.d2h(out, d_out)
+    finally:
+        for x in (d_codes, d_lens, d_out):
+            ctx.dfree(x)
+    return out
 
 
 def test_spectrum_generic_normalised(ctx):

@@ -33,6 +33,8 @@ def test_all_goldens_through_dropin(golden):
         if name == "SP_k6_xtr0_full":
             continue
         e = golden.entry(name)
+        if e["fn"] in ("get_phi_u", "get_phi_km", "gappy_k", "B_k"):
+            continue  # module-level feature maps: tests/test_gpu_features.py
         if e["fn"] in ("get_WD_d", "get_WDShifts_d"):  # one pair, any L
             x, y = golden.seqs(name)
             v = getattr(kernels, e["fn"])(x, y, **e["kwargs"])
@@ -153,22 +155,28 @@ def _form(tune, form):
     """"F" -> KMG_MM_FORM=F; "F:T" also KMG_PL_THREADS=T (pair lines, 512: two workgroups a CU,
     1024: one; unset: by size)"""
     f, _, t = form.partition(":")
-    tune(KMG_MM_FORM=f, KMG_PL_THREADS=t or None)
+    tune(KMG_MM_FORM=f, KMG_PL_THREADS=(t or None) if f == "3" else None,
+         KMG_NB_THREADS=(t or None) if f == "4" else None)
 
 
-@pytest.mark.parametrize("form", ["0", "3:1024", "3:512"])
+@pytest.mark.parametrize("form", ["0", "3:1024", "3:512", "4:1024", "4:512"])
 def test_mismatch_k9_n20000(ctx, tune, form):
     """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows
-    (default formulation and the pair-lines table at both workgroup sizes)."""
+    (default formulation, the pair-lines table and the neighbourhood lists at both workgroup
+    sizes)."""
     _form(tune, form)
     codes, lens = E.synthetic(20000, 101, seed=3)
     K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
                  L.KMG_F64)
     plan = ctx.last_plan()
-    assert plan["formulation"] == "pair_lines"
+    if form.startswith("4"):
+        assert plan["formulation"] == "neighbourhood" and plan["threads"] == int(form[2:])
+        assert plan["triangle"] == (plan["nchunks"] > 1)
+    else:
+        assert plan["formulation"] == "pair_lines"
     if form in ("0", "3:512"):  # 512 threads: 2 chunks of 10000, upper block triangle + mirror
         assert (plan["threads"], plan["nchunks"], plan["chunk"], plan["triangle"]) == (512, 2, 10000, True)
-    else:                       # 1024 threads: chunks of up to ~24000 columns (cost model)
+    elif form == "3:1024":      # 1024 threads: chunks of up to ~24000 columns (cost model)
         assert plan["threads"] == 1024 and plan["triangle"] == (plan["nchunks"] > 1)
     rows = [0, 1, 7777, 10000, 19999]
     for r in rows:
@@ -208,12 +216,12 @@ def test_mismatch_slots_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["2", "3", "3:1024"])
+@pytest.mark.parametrize("form", ["2", "3", "3:1024", "4", "4:512"])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_mismatch_pairs_k_range(ctx, tune, k, form):
-    """Drop-two tables (2: pair table with per-group headers, 3: pair lines) at every
-    compiled k, raw and normalised, over several column chunkings (chunk = columns per
-    group table)."""
+    """Drop-two tables (2: pair table with per-group headers, 3: pair lines) and the
+    neighbourhood lists (4) at every compiled k, raw and normalised, over several column
+    chunkings (chunk = columns per group table / list set)."""
     codes, lens = E.synthetic(500, 101, seed=80 + k)
     ref = cref.mismatch_raw(codes, lens, k, 1)
     _form(tune, form)
@@ -227,7 +235,7 @@ def test_mismatch_pairs_k_range(ctx, tune, k, form):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
     >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
@@ -247,7 +255,7 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     assert np.array_equal(raw, raw.T)
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4"])
 def test_mismatch_stress_repeats(ctx, tune, form):
     _form(tune, form)
     codes, lens = E.synthetic(40, 101, seed=12)
