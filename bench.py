@@ -681,11 +681,33 @@ def gather_roofline(res, world, esz):
             "frac": recv / t / XGMI_IN_PEAK}
 
 
+def mm_nbhd_roofline(n, rows, gram_ms, plan, esz, k=9, P=93):
+    """HBM model of the neighbourhood-list Gram launch (kmg_nbhd.hip): a row window reads
+    its list once per column chunk, E = (1 + 3k + 9k(k-1)/2) x (chunk x P / 4^k) uint16
+    entries (+ the three segments' padding to 8), and the row writes its K row (a square K
+    built by its upper block triangle: (nch + 1) / (2 nch) of both on average)."""
+    nch, ch = max(1, plan["nchunks"]), max(8, plan["chunk"])
+    nb = 1 + 3 * k + 9 * k * (k - 1) // 2
+    f = (nch + 1) / (2.0 * nch) if plan["triangle"] else 1.0
+    per_window = 2.0 * (nb * n * P / 4.0 ** k + 10.5 * nch)  # bytes over all chunks
+    reads = rows * P * per_window * f
+    writes = rows * n * esz * f
+    alg = reads + writes
+    return {"bound": "hbm", "table": "neighbourhood lists (%d chunk(s) of %d columns%s; %d-thread "
+                                     "workgroups)" % (nch, ch, ", upper block triangle"
+                                                      if plan["triangle"] else "", plan["threads"]),
+            "list_bytes_per_window": per_window, "list_bytes_per_launch": reads,
+            "k_bytes_per_launch": writes, "achieved_GBps": alg / (gram_ms / 1e3) / 1e9,
+            "peak_GBps": HBM_PEAK / 1e9, "frac": alg / (gram_ms / 1e3) / HBM_PEAK}
+
+
 def mm_gather_roofline(n, rows, gram_ms, plan, k=9, P=93):
     """Random-line gather model of the MM(9,1) Gram launch (see the secondary line), for the
     chunking the library reports (kmg_last_plan): a row reads every column chunk, or (a
     square K built by its upper block triangle) (nch + 1) / 2 of them on average."""
     import math
+    if plan["formulation"] == "neighbourhood":
+        return mm_nbhd_roofline(n, rows, gram_ms, plan, 8)
     nch, ch = max(1, plan["nchunks"]), max(8, plan["chunk"])
     reads = (nch + 1) / 2.0 if plan["triangle"] else float(nch)
     if plan["formulation"] == "pair_lines":

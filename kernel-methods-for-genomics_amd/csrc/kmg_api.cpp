@@ -1806,7 +1806,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     // that is all-gathered after the slabs and patched into K; a full list redoes the
     // build with 16-bit slabs
     if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS ||
-        path == SM_PL) {
+        path == SM_PL || path == SM_NB) {
       wire = narrow_bits == 8 ? KMG_U8 : KMG_U16;
       check16 = wire == KMG_U8 || path != SM_POSTING;  // spectrum counts <= P^2 < 65536
     } else if (narrow_bits == 8) {

@@ -110,20 +110,40 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
   seg[b] = make_uint2(p0, p0 + p1);
 }
 
+__device__ __forceinline__ void nb_fill_one(int k, int64_t b, const uint32_t *__restrict__ xoff,
+                                            const uint16_t *__restrict__ xent,
+                                            const uint32_t *__restrict__ nboff,
+                                            const uint2 *__restrict__ nbseg,
+                                            uint16_t *__restrict__ table, uint32_t pad_col,
+                                            uint16_t *stage, uint32_t *wsum, uint32_t &pre2);
+
 // one workgroup per (chunk, k-mer): the neighbourhood list into table[nboff[b] * 8 ..]
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
-    int k, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    int k, int64_t nbins, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col) {
   __shared__ __align__(16) uint16_t stage[NB_STAGE];
   __shared__ uint32_t wsum[NB_FILL_THREADS / 64];
   __shared__ uint32_t pre2;
-  const int64_t b = blockIdx.x;
+  // grid-stride over the (chunk, k-mer) bins: 4^12 bins x 256 threads would pass the 32-bit
+  // AQL grid size
+  for (int64_t b = blockIdx.x; b < nbins; b += gridDim.x) {
+    nb_fill_one(k, b, xoff, xent, nboff, nbseg, table, pad_col, stage, wsum, pre2);
+    __syncthreads();  // the next bin reuses stage / wsum / pre2
+  }
+}
+
+__device__ __forceinline__ void nb_fill_one(int k, int64_t b, const uint32_t *__restrict__ xoff,
+                                            const uint16_t *__restrict__ xent,
+                                            const uint32_t *__restrict__ nboff,
+                                            const uint2 *__restrict__ nbseg,
+                                            uint16_t *__restrict__ table, uint32_t pad_col,
+                                            uint16_t *stage, uint32_t *wsum, uint32_t &pre2) {
   const uint32_t nkeys = 1u << (2 * k);
   const uint32_t u = (uint32_t)b & (nkeys - 1u);
   const uint32_t *off = xoff + (b - u);
   const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
-  if (tot == 0) return;  // block-uniform
+  if (tot == 0) return;  // block-uniform (the caller's barrier follows)
   const uint2 sg = nbseg[b];
   const int nbn = nb_neighbours(k);
   const int per = (nbn + NB_FILL_THREADS - 1) / NB_FILL_THREADS;  // <= 3 (k <= 12)
@@ -329,8 +349,9 @@ hipError_t launch_nb_build(const IndexGeom &g, const uint32_t *xoff, const uint1
   hipError_t e = launch_scan(hist, nboff, cursor, nbins, partials, s);
   if (e != hipSuccess) return e;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
-  hipLaunchKernelGGL(nb_fill_kernel, dim3((unsigned)nbins), dim3(NB_FILL_THREADS), 0, s, g.k, xoff,
-                     xent, nboff, nbseg, table, pad_col);
+  const int64_t fill_blocks = std::min<int64_t>(nbins, (int64_t)1 << 22);
+  hipLaunchKernelGGL(nb_fill_kernel, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, s, g.k,
+                     nbins, xoff, xent, nboff, nbseg, table, pad_col);
   return hipGetLastError();
 }
 
