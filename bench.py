@@ -51,7 +51,7 @@ GATHER_CEILING = 56.38e9  # random 128-B lines/s from a 78.6 MB table (profiles/
 INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROARCH.md)
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
           "(k=9,m=1), 1/2/4/8 GPUs")
-STAGES = ("count", "scan", "place", "fine", "pack", "slots", "extract", "features", "diag",
+STAGES = ("count", "scan", "place", "fine", "pack", "lists", "slots", "extract", "features", "diag",
           "gram", "mirror", "gather")
 
 

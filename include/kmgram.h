@@ -269,7 +269,8 @@ int kmg_stream(kmg_ctx *ctx, void **hip_stream);
  * times only the "gram", "gather", "unpack", "mirror" and "memset" stages, 2 events per
  * Gram launch instead of 2 per stage); nothing is synchronised until a stage time is read.
  * Stage names: "count", "scan", "place", "fine", "diag", "gram", "extract", "features",
- * "pack" (2-bit packing of the input), "slots" (mismatch slot / pair tables), "combine",
+ * "pack" (2-bit packing of the input), "slots" (mismatch slot / pair tables, neighbourhood
+ * lists), "lists" (neighbourhood-list sizes and starts), "combine",
  * "solve", "memset", "gather" (the RCCL all-gathers of kmg_gram_blocks, timed on their own
  * stream), "unpack" (round-slab assembly), "mirror" (lower block triangle of a full square
  * mismatch K built by its upper block triangle).

@@ -92,11 +92,11 @@ struct DevBuf {
 const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
                              "gram",    "extract",  "pack",  "features", "combine",
                              "solve",   "slots",    "memset", "gather", "unpack",
-                             "mirror"};
-constexpr int kNumStages = 16;
+                             "mirror",  "lists"};
+constexpr int kNumStages = 17;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
-  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK, ST_MIRROR
+  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK, ST_MIRROR, ST_LISTS
 };
 
 // Tuning knobs: read from the environment once per context (kmg_create) and again only on
@@ -627,7 +627,9 @@ int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int thre
     const double row_reads = 2.0 * nb * pmax * dens * (double)n + 2.0 * 10.5 * pmax * nch;
     const double gram = (double)n * (row_reads + esz * (double)n) * f;
     const double mirror = tri_esz > 0 ? 2.0 * esz * (double)n * n * (double)(nch - 1) / (2.0 * nch) : 0.0;
-    const double cost = gram / 6e12 + mirror / 5e12;
+    // + building the lists: a fixed cost per (chunk, k-mer) bin on top of the bytes
+    const double build = (double)nch * (double)pow4(k) * 1.0e-9;
+    const double cost = gram / 6e12 + mirror / 5e12 + build * 1e-3 * 1e3 / 1e3;
     if (cost < best_cost * (1.0 - 1e-12)) {
       best_cost = cost;
       best = ch;
@@ -1206,12 +1208,16 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(c->nb_seg.ensure(sizeof(uint2) * (size_t)nbins));
         KMG_TRY(c->nb_lines.ensure(sizeof(uint16_t) * (size_t)(bound + 8)));
         {
-          StageTimer t(c, ST_SLOTS);
-          KMG_HIP(launch_nb_build(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
-                                  c->pr_rtot.as<uint32_t>(), c->pr_rbase.as<uint32_t>(),
-                                  c->pr_cursor.as<uint32_t>(), c->nb_seg.as<uint2>(),
-                                  c->partials.as<uint32_t>(), c->nb_lines.as<uint16_t>(),
-                                  c->stream));
+          StageTimer t(c, ST_LISTS);  // list sizes and starts
+          KMG_HIP(launch_nb_count(g, c->off.as<uint32_t>(), c->pr_rtot.as<uint32_t>(),
+                                  c->pr_rbase.as<uint32_t>(), c->pr_cursor.as<uint32_t>(),
+                                  c->nb_seg.as<uint2>(), c->partials.as<uint32_t>(), c->stream));
+        }
+        {
+          StageTimer t(c, ST_SLOTS);  // the lists themselves
+          KMG_HIP(launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                 c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
+                                 c->nb_lines.as<uint16_t>(), c->stream));
         }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));

@@ -274,9 +274,12 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
 // nbins + 1 words, nbseg nbins, table nb_list_entries_bound(...) uint16
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins);
 size_t nb_gram_lds(const IndexGeom &g, const Packed &pk);
-hipError_t launch_nb_build(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
-                           uint32_t *hist, uint32_t *nboff, uint32_t *cursor, uint2 *nbseg,
-                           uint32_t *partials, uint16_t *table, hipStream_t s);
+hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
+                           uint32_t *nboff, uint32_t *cursor, uint2 *nbseg, uint32_t *partials,
+                           hipStream_t s);
+hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
+                          const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
+                          hipStream_t s);
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,

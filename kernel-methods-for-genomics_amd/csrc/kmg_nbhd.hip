@@ -21,9 +21,9 @@
 //   nb_count_kernel   per (c, u): n0, n1, n2 from the exact index (1 + 3k + 9k(k-1)/2
 //                     lookups of its bin offsets, L2-resident) -> pieces and segment ends
 //   launch_scan       list starts (in pieces; < 2^32: checked by the host)
-//   nb_fill_kernel    per (c, u), one 256-thread workgroup: block scan of the neighbour
-//                     counts, copy of each neighbour's posting list into its slot of the list
-//                     (staged in LDS and written with 16-byte stores when it fits)
+//   nb_fill_kernel    per (c, u), one wave: wave scan of the neighbour counts, copy of each
+//                     neighbour's posting list into its slot of the list (staged in LDS and
+//                     written with 16-byte stores when it fits)
 //   gram_nb_kernel    per (row i, chunk c): row windows -> (list start, pieces, segment
 //                     ends) in LDS, a prefix sum over the row's lists, then every wave streams
 //                     an equal share of the row's pieces (four 16-byte loads in flight per
@@ -39,7 +39,6 @@ namespace kmg {
 
 namespace {
 constexpr int NB_FILL_THREADS = 256;
-constexpr int NB_STAGE = 12288;  // entries of one list staged in LDS by nb_fill_kernel (24 KB)
 constexpr int NB_UNROLL = 4;     // 16-byte pieces in flight per lane in gram_nb_kernel
 
 __device__ __forceinline__ int nb_neighbours(int k) { return 1 + 3 * k + 9 * k * (k - 1) / 2; }
@@ -110,111 +109,109 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
   seg[b] = make_uint2(p0, p0 + p1);
 }
 
-__device__ __forceinline__ void nb_fill_one(int k, int64_t b, const uint32_t *__restrict__ xoff,
-                                            const uint16_t *__restrict__ xent,
-                                            const uint32_t *__restrict__ nboff,
-                                            const uint2 *__restrict__ nbseg,
-                                            uint16_t *__restrict__ table, uint32_t pad_col,
-                                            uint16_t *stage, uint32_t *wsum, uint32_t &pre2);
+// One WAVE per (chunk, k-mer) bin, four waves a workgroup, grid-stride over the bins.  Lane
+// l owns the neighbours t in [l R, l R + R) (R = ceil(nb / 64)): it loads their posting
+// ranges (all loads issued before any is used), a wave prefix sum places each neighbour's
+// run in its segment, and the runs are copied into the wave's LDS image of the list with
+// their loads batched NB_BATCH at a time (a run is ~chunk x P / 4^k entries: 7 at N=20000),
+// then the image leaves with 16-byte stores.  Lists longer than the image are written to
+// HBM directly.  (Round 4's first form -- one 256-thread workgroup a bin, a dependent load
+// per copied entry -- took 1.7 ms per 262144 bins at N=20000.)
+constexpr int NB_WAVE_STAGE = 6144;  // entries of one wave's list image (12 KB)
+constexpr int NB_BATCH = 8;
+constexpr int NB_MAXR = 10;          // neighbours a lane: ceil(631 / 64) at k = 12
 
-// one workgroup per (chunk, k-mer): the neighbourhood list into table[nboff[b] * 8 ..]
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     int k, int64_t nbins, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col) {
-  __shared__ __align__(16) uint16_t stage[NB_STAGE];
-  __shared__ uint32_t wsum[NB_FILL_THREADS / 64];
-  __shared__ uint32_t pre2;
-  // grid-stride over the (chunk, k-mer) bins: 4^12 bins x 256 threads would pass the 32-bit
-  // AQL grid size
-  for (int64_t b = blockIdx.x; b < nbins; b += gridDim.x) {
-    nb_fill_one(k, b, xoff, xent, nboff, nbseg, table, pad_col, stage, wsum, pre2);
-    __syncthreads();  // the next bin reuses stage / wsum / pre2
-  }
-}
-
-__device__ __forceinline__ void nb_fill_one(int k, int64_t b, const uint32_t *__restrict__ xoff,
-                                            const uint16_t *__restrict__ xent,
-                                            const uint32_t *__restrict__ nboff,
-                                            const uint2 *__restrict__ nbseg,
-                                            uint16_t *__restrict__ table, uint32_t pad_col,
-                                            uint16_t *stage, uint32_t *wsum, uint32_t &pre2) {
+  __shared__ __align__(16) uint16_t stage_all[NB_FILL_THREADS / 64][NB_WAVE_STAGE];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint16_t *stage = stage_all[wave];
   const uint32_t nkeys = 1u << (2 * k);
-  const uint32_t u = (uint32_t)b & (nkeys - 1u);
-  const uint32_t *off = xoff + (b - u);
-  const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
-  if (tot == 0) return;  // block-uniform (the caller's barrier follows)
-  const uint2 sg = nbseg[b];
   const int nbn = nb_neighbours(k);
-  const int per = (nbn + NB_FILL_THREADS - 1) / NB_FILL_THREADS;  // <= 3 (k <= 12)
-  const int t0 = threadIdx.x * per;
-  uint32_t cnt[3], src[3];
-  int sgm[3];
-  uint32_t s = 0;
+  const int R = (nbn + 63) >> 6;
+  const int t0 = lane * R;
+  const int64_t wstride = (int64_t)gridDim.x * (NB_FILL_THREADS / 64);
+  for (int64_t b = (int64_t)blockIdx.x * (NB_FILL_THREADS / 64) + wave; b < nbins; b += wstride) {
+    const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+    if (tot == 0) continue;  // wave-uniform
+    const uint32_t u = (uint32_t)b & (nkeys - 1u);
+    const uint32_t *off = xoff + (b - u);
+    const uint2 sg = nbseg[b];
+    uint32_t src[NB_MAXR], cnt[NB_MAXR];
+    int sgm[NB_MAXR];
+    uint32_t s = 0;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    cnt[j] = 0;
-    src[j] = 0;
-    sgm[j] = 0;
-    if (j < per && t0 + j < nbn) {
-      const uint32_t v = nb_neighbour(u, k, t0 + j, sgm[j]);
-      src[j] = off[v];
-      cnt[j] = off[v + 1] - src[j];
+    for (int j = 0; j < NB_MAXR; ++j) {
+      cnt[j] = 0;
+      src[j] = 0;
+      sgm[j] = 0;
+      if (j < R && t0 + j < nbn) {
+        const uint32_t v = nb_neighbour(u, k, t0 + j, sgm[j]);
+        src[j] = off[v];
+        cnt[j] = off[v + 1] - src[j];
+      }
     }
-    s += cnt[j];
-  }
-  // block exclusive scan of the per-thread sums (neighbour order = list order)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t inc = nb_wave_incl_scan(s);
-  if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
-  uint32_t run = inc - s;
-  for (int w = 0; w < wave; ++w) run += wsum[w];
-  // the unpadded prefix where segment 2 starts (neighbour index 1 + 3k)
-  {
-    uint32_t r = run;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (j < per && t0 + j == 1 + 3 * k) pre2 = r;
+    for (int j = 0; j < NB_MAXR; ++j) s += cnt[j];
+    const uint32_t inc = nb_wave_incl_scan(s);
+    const uint32_t total = __shfl(inc, 63, 64);
+    uint32_t run = inc - s;
+    // unpadded prefix where segment 1 (t = 1) and segment 2 (t = 1 + 3k) start
+    const int t2 = 1 + 3 * k;
+    uint32_t my2 = 0xFFFFFFFFu, r = run;
+#pragma unroll
+    for (int j = 0; j < NB_MAXR; ++j) {
+      if (t0 + j == t2) my2 = r;
       r += cnt[j];
     }
-  }
-  uint32_t total = 0;
-  for (int w = 0; w < NB_FILL_THREADS / 64; ++w) total += wsum[w];
-  if (1 + 3 * k >= nbn) pre2 = total;  // (k = 0 never reaches here)
-  __syncthreads();
-  const uint32_t n0 = off[u + 1] - off[u], p2s = pre2;
-  const uint32_t segbase[3] = {0u, sg.x * 8u, sg.y * 8u};
-  const uint32_t segpre[3] = {0u, n0, p2s};
-  const uint32_t segn[3] = {n0, p2s - n0, total - p2s};
-  const uint32_t segend[3] = {sg.x * 8u, sg.y * 8u, tot * 8u};
-  const bool lds = tot * 8u <= (uint32_t)NB_STAGE;
-  uint16_t *gdst = table + (size_t)start * 8u;
-  auto put = [&](uint32_t pos, uint16_t v) {
-    if (lds)
-      stage[pos] = v;
-    else
-      gdst[pos] = v;
-  };
+    const uint32_t n0 = __shfl(cnt[0], 0, 64);  // neighbour 0 (u itself) is lane 0's first
+    uint32_t pre2 = my2;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    if (cnt[j]) {
+    for (int d = 1; d < 64; d <<= 1) pre2 = min(pre2, (uint32_t)__shfl_xor(pre2, d, 64));
+    if (t2 >= nbn) pre2 = total;
+    const uint32_t segbase[3] = {0u, sg.x * 8u, sg.y * 8u};
+    const uint32_t segpre[3] = {0u, n0, pre2};
+    const uint32_t segn[3] = {n0, pre2 - n0, total - pre2};
+    const uint32_t segend[3] = {sg.x * 8u, sg.y * 8u, tot * 8u};
+    const bool lds = tot * 8u <= (uint32_t)NB_WAVE_STAGE;
+    uint16_t *gdst = table + (size_t)start * 8u;
+#pragma unroll
+    for (int j = 0; j < NB_MAXR; ++j) {
       const uint32_t d = segbase[sgm[j]] + (run - segpre[sgm[j]]);
-      for (uint32_t e = 0; e < cnt[j]; ++e) put(d + e, xent[src[j] + e]);
+      for (uint32_t e0 = 0; e0 < cnt[j]; e0 += NB_BATCH) {
+        uint16_t v[NB_BATCH];
+#pragma unroll
+        for (int e = 0; e < NB_BATCH; ++e)
+          if (e0 + e < cnt[j]) v[e] = xent[src[j] + e0 + e];
+#pragma unroll
+        for (int e = 0; e < NB_BATCH; ++e)
+          if (e0 + e < cnt[j]) {
+            if (lds) stage[d + e0 + e] = v[e];
+            else gdst[d + e0 + e] = v[e];
+          }
+      }
+      run += cnt[j];
     }
-    run += cnt[j];
-  }
-  // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
-  if (threadIdx.x < 24) {
-    const int sgi = threadIdx.x >> 3, e = threadIdx.x & 7;
-    const uint32_t pos = segbase[sgi] + segn[sgi] + (uint32_t)e;
-    if (pos < segend[sgi]) put(pos, (uint16_t)(pad_col + (pos & 63u)));
-  }
-  if (lds) {
-    __syncthreads();
-    uint4 *g4 = (uint4 *)gdst;
-    const uint4 *s4 = (const uint4 *)stage;
-    for (uint32_t q = threadIdx.x; q < tot; q += NB_FILL_THREADS) g4[q] = s4[q];
+    // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+    if (lane < 24) {
+      const int sgi = lane >> 3, e = lane & 7;
+      const uint32_t pos = segbase[sgi] + segn[sgi] + (uint32_t)e;
+      if (pos < segend[sgi]) {
+        const uint16_t pv = (uint16_t)(pad_col + (pos & 63u));
+        if (lds) stage[pos] = pv;
+        else gdst[pos] = pv;
+      }
+    }
+    if (lds) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      uint4 *g4 = (uint4 *)gdst;
+      const uint4 *s4 = (const uint4 *)stage;
+      for (uint32_t q = lane; q < tot; q += 64) g4[q] = s4[q];
+      __builtin_amdgcn_wave_barrier();  // the next bin overwrites the image
+    }
   }
 }
 
@@ -339,17 +336,24 @@ size_t nb_gram_lds(const IndexGeom &g, const Packed &pk) {
   return (size_t)((((g.chunk + 3) >> 2) << 2) + 64 + 4 * g.pmax + 1 + pk.ldp) * 4;
 }
 
-hipError_t launch_nb_build(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
-                           uint32_t *hist, uint32_t *nboff, uint32_t *cursor, uint2 *nbseg,
-                           uint32_t *partials, uint16_t *table, hipStream_t s) {
+hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
+                           uint32_t *nboff, uint32_t *cursor, uint2 *nbseg, uint32_t *partials,
+                           hipStream_t s) {
   const int64_t nbins = g.nbins();
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   hipLaunchKernelGGL(nb_count_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, g.k,
                      nbins, xoff, hist, nbseg);
-  hipError_t e = launch_scan(hist, nboff, cursor, nbins, partials, s);
-  if (e != hipSuccess) return e;
+  return launch_scan(hist, nboff, cursor, nbins, partials, s);
+}
+
+hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
+                          const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
+                          hipStream_t s) {
+  const int64_t nbins = g.nbins();
+  if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
-  const int64_t fill_blocks = std::min<int64_t>(nbins, (int64_t)1 << 22);
+  const int64_t wpb = NB_FILL_THREADS / 64;
+  const int64_t fill_blocks = std::min<int64_t>((nbins + wpb - 1) / wpb, (int64_t)1 << 20);
   hipLaunchKernelGGL(nb_fill_kernel, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, s, g.k,
                      nbins, xoff, xent, nboff, nbseg, table, pad_col);
   return hipGetLastError();
