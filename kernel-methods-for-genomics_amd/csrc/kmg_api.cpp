@@ -629,7 +629,7 @@ int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int thre
     const double mirror = tri_esz > 0 ? 2.0 * esz * (double)n * n * (double)(nch - 1) / (2.0 * nch) : 0.0;
     // + building the lists: a fixed cost per (chunk, k-mer) bin on top of the bytes
     const double build = (double)nch * (double)pow4(k) * 1.0e-9;
-    const double cost = gram / 6e12 + mirror / 5e12 + build * 1e-3 * 1e3 / 1e3;
+    const double cost = gram / 6e12 + mirror / 5e12 + build;
     if (cost < best_cost * (1.0 - 1e-12)) {
       best_cost = cost;
       best = ch;
