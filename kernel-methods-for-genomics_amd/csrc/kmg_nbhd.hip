@@ -109,29 +109,39 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
   seg[b] = make_uint2(p0, p0 + p1);
 }
 
-// One WAVE per (chunk, k-mer) bin, four waves a workgroup, grid-stride over the bins.  Lane
-// l owns the neighbours t in [l R, l R + R) (R = ceil(nb / 64)): it loads their posting
-// ranges (all loads issued before any is used), a wave prefix sum places each neighbour's
-// run in its segment, and the runs are copied into the wave's LDS image of the list with
-// their loads batched NB_BATCH at a time (a run is ~chunk x P / 4^k entries: 7 at N=20000),
-// then the image leaves with 16-byte stores.  Lists longer than the image are written to
-// HBM directly.  (Round 4's first form -- one 256-thread workgroup a bin, a dependent load
-// per copied entry -- took 1.7 ms per 262144 bins at N=20000.)
-constexpr int NB_WAVE_STAGE = 6144;  // entries of one wave's list image (12 KB)
+// One WAVE per (chunk, k-mer) bin, four waves a workgroup, grid-stride over the bins.
+//  1. lane l owns the neighbours t in [l R, l R + R) (R = ceil(nb / 64)): their posting
+//     ranges (all loads issued before any is used), a wave prefix sum gives each run's start
+//     in the unpadded concatenation; starts and sources go to the wave's LDS tables;
+//  2. the list is copied ENTRY-parallel in windows of NB_WIN entries: the owners mark the
+//     run of every entry of the window in an LDS map (run id per entry), then lane l copies
+//     entries e = l, l + 64, ... of the window -- NB_BATCH loads in flight, and 64
+//     consecutive entries of a segment are 128 contiguous bytes of the list (coalesced
+//     2-byte stores).
+// A run is ~chunk x P / 4^k entries (7 at N=20000, k=9): copying it lane-per-run took one
+// dependent load per entry (round 4's first two forms: 1.7-2.2 ms per 262144 bins at
+// N=20000).
+constexpr int NB_WIN = 2048;   // entries of the run-id map per wave
 constexpr int NB_BATCH = 8;
-constexpr int NB_MAXR = 10;          // neighbours a lane: ceil(631 / 64) at k = 12
+constexpr int NB_MAXR = 10;    // neighbours a lane: ceil(631 / 64) at k = 12
+constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12)
 
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     int k, int64_t nbins, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col) {
-  __shared__ __align__(16) uint16_t stage_all[NB_FILL_THREADS / 64][NB_WAVE_STAGE];
+  __shared__ uint16_t runmap_all[NB_FILL_THREADS / 64][NB_WIN];
+  __shared__ uint32_t npre_all[NB_FILL_THREADS / 64][NB_MAXN];
+  __shared__ uint32_t nsrc_all[NB_FILL_THREADS / 64][NB_MAXN];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint16_t *stage = stage_all[wave];
+  uint16_t *runmap = runmap_all[wave];
+  uint32_t *npre = npre_all[wave];
+  uint32_t *nsrc = nsrc_all[wave];
   const uint32_t nkeys = 1u << (2 * k);
   const int nbn = nb_neighbours(k);
   const int R = (nbn + 63) >> 6;
   const int t0 = lane * R;
+  const int t2 = 1 + 3 * k;  // first Hamming-2 neighbour
   const int64_t wstride = (int64_t)gridDim.x * (NB_FILL_THREADS / 64);
   for (int64_t b = (int64_t)blockIdx.x * (NB_FILL_THREADS / 64) + wave; b < nbins; b += wstride) {
     const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
@@ -140,78 +150,82 @@ __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     const uint32_t *off = xoff + (b - u);
     const uint2 sg = nbseg[b];
     uint32_t src[NB_MAXR], cnt[NB_MAXR];
-    int sgm[NB_MAXR];
-    uint32_t s = 0;
 #pragma unroll
     for (int j = 0; j < NB_MAXR; ++j) {
       cnt[j] = 0;
       src[j] = 0;
-      sgm[j] = 0;
       if (j < R && t0 + j < nbn) {
-        const uint32_t v = nb_neighbour(u, k, t0 + j, sgm[j]);
+        int sgm;
+        const uint32_t v = nb_neighbour(u, k, t0 + j, sgm);
         src[j] = off[v];
         cnt[j] = off[v + 1] - src[j];
       }
     }
+    uint32_t s = 0;
 #pragma unroll
     for (int j = 0; j < NB_MAXR; ++j) s += cnt[j];
     const uint32_t inc = nb_wave_incl_scan(s);
     const uint32_t total = __shfl(inc, 63, 64);
-    uint32_t run = inc - s;
-    // unpadded prefix where segment 1 (t = 1) and segment 2 (t = 1 + 3k) start
-    const int t2 = 1 + 3 * k;
-    uint32_t my2 = 0xFFFFFFFFu, r = run;
+    uint32_t pre[NB_MAXR];
+    {
+      uint32_t r = inc - s;
 #pragma unroll
-    for (int j = 0; j < NB_MAXR; ++j) {
-      if (t0 + j == t2) my2 = r;
-      r += cnt[j];
+      for (int j = 0; j < NB_MAXR; ++j) {
+        pre[j] = r;
+        if (j < R && t0 + j < nbn) {
+          npre[t0 + j] = r;
+          nsrc[t0 + j] = src[j];
+        }
+        r += cnt[j];
+      }
     }
-    const uint32_t n0 = __shfl(cnt[0], 0, 64);  // neighbour 0 (u itself) is lane 0's first
-    uint32_t pre2 = my2;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) pre2 = min(pre2, (uint32_t)__shfl_xor(pre2, d, 64));
-    if (t2 >= nbn) pre2 = total;
+    if (lane == 0) npre[nbn] = total;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint32_t n0 = npre[1];
+    const uint32_t pre2 = t2 < nbn ? npre[t2] : total;
     const uint32_t segbase[3] = {0u, sg.x * 8u, sg.y * 8u};
     const uint32_t segpre[3] = {0u, n0, pre2};
-    const uint32_t segn[3] = {n0, pre2 - n0, total - pre2};
-    const uint32_t segend[3] = {sg.x * 8u, sg.y * 8u, tot * 8u};
-    const bool lds = tot * 8u <= (uint32_t)NB_WAVE_STAGE;
-    uint16_t *gdst = table + (size_t)start * 8u;
+    uint16_t *dst = table + (size_t)start * 8u;
+    for (uint32_t w0 = 0; w0 < total; w0 += NB_WIN) {
+      const uint32_t w1 = min(total, w0 + (uint32_t)NB_WIN);
+      // run id of every entry of the window, written by the run's owner
 #pragma unroll
-    for (int j = 0; j < NB_MAXR; ++j) {
-      const uint32_t d = segbase[sgm[j]] + (run - segpre[sgm[j]]);
-      for (uint32_t e0 = 0; e0 < cnt[j]; e0 += NB_BATCH) {
-        uint16_t v[NB_BATCH];
-#pragma unroll
-        for (int e = 0; e < NB_BATCH; ++e)
-          if (e0 + e < cnt[j]) v[e] = xent[src[j] + e0 + e];
-#pragma unroll
-        for (int e = 0; e < NB_BATCH; ++e)
-          if (e0 + e < cnt[j]) {
-            if (lds) stage[d + e0 + e] = v[e];
-            else gdst[d + e0 + e] = v[e];
-          }
+      for (int j = 0; j < NB_MAXR; ++j) {
+        const uint32_t a = max(pre[j], w0), z = min(pre[j] + cnt[j], w1);
+        for (uint32_t e = a; e < z; ++e) runmap[e - w0] = (uint16_t)(t0 + j);
       }
-      run += cnt[j];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      for (uint32_t e0 = w0 + lane; e0 < w1; e0 += 64 * NB_BATCH) {
+        uint16_t v[NB_BATCH];
+        uint32_t pos[NB_BATCH];
+#pragma unroll
+        for (int q = 0; q < NB_BATCH; ++q) {
+          const uint32_t e = e0 + 64u * q;
+          pos[q] = 0xFFFFFFFFu;
+          if (e < w1) {
+            const int t = runmap[e - w0];
+            const int sgi = t == 0 ? 0 : (t < t2 ? 1 : 2);
+            v[q] = xent[nsrc[t] + (e - npre[t])];
+            pos[q] = segbase[sgi] + (e - segpre[sgi]);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NB_BATCH; ++q)
+          if (pos[q] != 0xFFFFFFFFu) dst[pos[q]] = v[q];
+      }
+      __builtin_amdgcn_wave_barrier();  // the next window overwrites the map
     }
     // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
     if (lane < 24) {
       const int sgi = lane >> 3, e = lane & 7;
-      const uint32_t pos = segbase[sgi] + segn[sgi] + (uint32_t)e;
-      if (pos < segend[sgi]) {
-        const uint16_t pv = (uint16_t)(pad_col + (pos & 63u));
-        if (lds) stage[pos] = pv;
-        else gdst[pos] = pv;
-      }
+      const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+      const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+      const uint32_t pos = segbase[sgi] + segn + (uint32_t)e;
+      if (pos < segend) dst[pos] = (uint16_t)(pad_col + (pos & 63u));
     }
-    if (lds) {
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      uint4 *g4 = (uint4 *)gdst;
-      const uint4 *s4 = (const uint4 *)stage;
-      for (uint32_t q = lane; q < tot; q += 64) g4[q] = s4[q];
-      __builtin_amdgcn_wave_barrier();  // the next bin overwrites the image
-    }
+    __builtin_amdgcn_wave_barrier();  // the next bin overwrites the tables
   }
 }
 
