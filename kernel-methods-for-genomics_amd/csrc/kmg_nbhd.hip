@@ -113,28 +113,27 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
 //  1. lane l owns the neighbours t in [l R, l R + R) (R = ceil(nb / 64)): their posting
 //     ranges (all loads issued before any is used), a wave prefix sum gives each run's start
 //     in the unpadded concatenation; starts and sources go to the wave's LDS tables;
-//  2. the list is copied ENTRY-parallel in windows of NB_WIN entries: the owners mark the
-//     run of every entry of the window in an LDS map (run id per entry), then lane l copies
-//     entries e = l, l + 64, ... of the window -- NB_BATCH loads in flight, and 64
-//     consecutive entries of a segment are 128 contiguous bytes of the list (coalesced
-//     2-byte stores).
-// A run is ~chunk x P / 4^k entries (7 at N=20000, k=9): copying it lane-per-run took one
-// dependent load per entry (round 4's first two forms: 1.7-2.2 ms per 262144 bins at
-// N=20000).
-constexpr int NB_WIN = 2048;   // entries of the run-id map per wave
-constexpr int NB_BATCH = 8;
-constexpr int NB_MAXR = 10;    // neighbours a lane: ceil(631 / 64) at k = 12
-constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12)
+//  2. the runs are copied by groups of LG lanes, one run a group (LG ~ the mean run length:
+//     chunk x P / 4^k occurrences of a k-mer, 7 at N=20000 and k = 9), 64 / LG runs a step
+//     and NB_STEPS steps' loads in flight; the runs of a step are consecutive in the list, so
+//     a wave's 2-byte stores land on ~128 contiguous bytes.
+// (Round 4's first forms -- a workgroup per bin with one dependent load per copied entry,
+// and an entry-parallel copy through an LDS run map, ~60 VALU per entry -- took 1.7-3.0 ms
+// per 262144 bins at N=20000.)
+constexpr int NB_MAXR = 10;    // neighbours a lane in step 1: ceil(631 / 64) at k = 12
+constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12, + the end)
+constexpr int NB_STEPS = 8;
 
+template <int LG>
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     int k, int64_t nbins, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col) {
-  __shared__ uint16_t runmap_all[NB_FILL_THREADS / 64][NB_WIN];
+  constexpr int G = 64 / LG;  // runs a step
   __shared__ uint32_t npre_all[NB_FILL_THREADS / 64][NB_MAXN];
   __shared__ uint32_t nsrc_all[NB_FILL_THREADS / 64][NB_MAXN];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint16_t *runmap = runmap_all[wave];
+  const int grp = lane / LG, gl = lane % LG;
   uint32_t *npre = npre_all[wave];
   uint32_t *nsrc = nsrc_all[wave];
   const uint32_t nkeys = 1u << (2 * k);
@@ -166,12 +165,10 @@ __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     for (int j = 0; j < NB_MAXR; ++j) s += cnt[j];
     const uint32_t inc = nb_wave_incl_scan(s);
     const uint32_t total = __shfl(inc, 63, 64);
-    uint32_t pre[NB_MAXR];
     {
       uint32_t r = inc - s;
 #pragma unroll
       for (int j = 0; j < NB_MAXR; ++j) {
-        pre[j] = r;
         if (j < R && t0 + j < nbn) {
           npre[t0 + j] = r;
           nsrc[t0 + j] = src[j];
@@ -184,45 +181,42 @@ __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const uint32_t n0 = npre[1];
     const uint32_t pre2 = t2 < nbn ? npre[t2] : total;
-    const uint32_t segbase[3] = {0u, sg.x * 8u, sg.y * 8u};
-    const uint32_t segpre[3] = {0u, n0, pre2};
     uint16_t *dst = table + (size_t)start * 8u;
-    for (uint32_t w0 = 0; w0 < total; w0 += NB_WIN) {
-      const uint32_t w1 = min(total, w0 + (uint32_t)NB_WIN);
-      // run id of every entry of the window, written by the run's owner
+    // (segment base - unpadded segment start) per segment
+    const uint32_t dlt0 = 0u, dlt1 = sg.x * 8u - n0, dlt2 = sg.y * 8u - pre2;
+    for (int t00 = 0; t00 < nbn; t00 += G * NB_STEPS) {
+      uint32_t sa[NB_STEPS], pa[NB_STEPS], ca[NB_STEPS];
 #pragma unroll
-      for (int j = 0; j < NB_MAXR; ++j) {
-        const uint32_t a = max(pre[j], w0), z = min(pre[j] + cnt[j], w1);
-        for (uint32_t e = a; e < z; ++e) runmap[e - w0] = (uint16_t)(t0 + j);
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      for (uint32_t e0 = w0 + lane; e0 < w1; e0 += 64 * NB_BATCH) {
-        uint16_t v[NB_BATCH];
-        uint32_t pos[NB_BATCH];
-#pragma unroll
-        for (int q = 0; q < NB_BATCH; ++q) {
-          const uint32_t e = e0 + 64u * q;
-          pos[q] = 0xFFFFFFFFu;
-          if (e < w1) {
-            const int t = runmap[e - w0];
-            const int sgi = t == 0 ? 0 : (t < t2 ? 1 : 2);
-            v[q] = xent[nsrc[t] + (e - npre[t])];
-            pos[q] = segbase[sgi] + (e - segpre[sgi]);
-          }
+      for (int q = 0; q < NB_STEPS; ++q) {
+        const int t = t00 + q * G + grp;
+        ca[q] = 0;
+        if (t < nbn) {
+          const uint32_t p0 = npre[t];
+          ca[q] = npre[t + 1] - p0;
+          sa[q] = nsrc[t];
+          pa[q] = p0 + (t == 0 ? dlt0 : t < t2 ? dlt1 : dlt2);
         }
-#pragma unroll
-        for (int q = 0; q < NB_BATCH; ++q)
-          if (pos[q] != 0xFFFFFFFFu) dst[pos[q]] = v[q];
       }
-      __builtin_amdgcn_wave_barrier();  // the next window overwrites the map
+      // first LG entries of every run of the steps: loads first, then the stores
+      uint16_t v[NB_STEPS];
+#pragma unroll
+      for (int q = 0; q < NB_STEPS; ++q)
+        if ((uint32_t)gl < ca[q]) v[q] = xent[sa[q] + gl];
+#pragma unroll
+      for (int q = 0; q < NB_STEPS; ++q)
+        if ((uint32_t)gl < ca[q]) dst[pa[q] + gl] = v[q];
+      // runs longer than LG (rare at the chosen LG)
+#pragma unroll
+      for (int q = 0; q < NB_STEPS; ++q)
+        for (uint32_t e = LG + gl; e < ca[q]; e += LG) dst[pa[q] + e] = xent[sa[q] + e];
     }
     // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
     if (lane < 24) {
       const int sgi = lane >> 3, e = lane & 7;
+      const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
       const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
       const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
-      const uint32_t pos = segbase[sgi] + segn + (uint32_t)e;
+      const uint32_t pos = segb + segn + (uint32_t)e;
       if (pos < segend) dst[pos] = (uint16_t)(pad_col + (pos & 63u));
     }
     __builtin_amdgcn_wave_barrier();  // the next bin overwrites the tables
@@ -367,9 +361,20 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
   const int64_t wpb = NB_FILL_THREADS / 64;
-  const int64_t fill_blocks = std::min<int64_t>((nbins + wpb - 1) / wpb, (int64_t)1 << 20);
-  hipLaunchKernelGGL(nb_fill_kernel, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, s, g.k,
-                     nbins, xoff, xent, nboff, nbseg, table, pad_col);
+  // waves in flight: 32 a CU x 256 CUs, each walking bins in key order (neighbouring
+  // k-mers share most of their neighbours' posting lines in L2)
+  const int64_t fill_blocks = std::min<int64_t>((nbins + wpb - 1) / wpb, 8 * 256);
+  // lanes a run: the mean occurrences of a k-mer in a chunk, to a power of two in [4, 32]
+  const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;
+  const int lg = mean <= 4.0 ? 4 : mean <= 8.0 ? 8 : mean <= 16.0 ? 16 : 32;
+#define KMG_NBF(LG_)                                                                             \
+  hipLaunchKernelGGL(nb_fill_kernel<LG_>, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, \
+                     s, g.k, nbins, xoff, xent, nboff, nbseg, table, pad_col)
+  if (lg == 4) KMG_NBF(4);
+  else if (lg == 8) KMG_NBF(8);
+  else if (lg == 16) KMG_NBF(16);
+  else KMG_NBF(32);
+#undef KMG_NBF
   return hipGetLastError();
 }
 

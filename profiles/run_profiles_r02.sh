@@ -17,6 +17,7 @@ case_of() {
     mm1_n20000) echo '[{"kind":"mm","k":9,"n":20000,"steps":5,"check":false,"KMG_MM_FORM":"1"}]' ;;
     mm3_n20000) echo '[{"kind":"mm","k":9,"n":20000,"steps":5,"check":false,"KMG_MM_FORM":"3"}]' ;;
     wd_n9000)  echo '[{"kind":"wd","d":5,"n":9000,"steps":10,"check":false}]' ;;
+    nb_n20000) echo '[{"kind":"mm","k":9,"n":20000,"steps":5,"check":false,"KMG_MM_FORM":"4","KMG_MM_CHUNK":"20000","KMG_MM_TRI":"0"}]' ;;
     config5_full) echo '[{"kind":"mm","k":9,"n":200000,"norm":0,"seed":5,"steps":2,"check":false}]' ;;
     config5_slab) echo '[{"kind":"mm","k":9,"n":200000,"rows":25000,"norm":1,"seed":5,"steps":3,"check":false}]' ;;
   esac
@@ -24,7 +25,7 @@ case_of() {
 sets_of() {
   case $1 in
     dense_sp5) echo "FETCH_SIZE|WRITE_SIZE|SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES|GRBM_GUI_ACTIVE GRBM_COUNT" ;;
-    mm*|config5*) echo "FETCH_SIZE|WRITE_SIZE|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES|SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY|TCC_HIT_sum TCC_MISS_sum" ;;
+    mm*|config5*|nb*) echo "FETCH_SIZE|WRITE_SIZE|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES|SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY|TCC_HIT_sum TCC_MISS_sum" ;;
     *)         echo "FETCH_SIZE|WRITE_SIZE|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES|TCC_HIT_sum TCC_MISS_sum" ;;
   esac
 }
