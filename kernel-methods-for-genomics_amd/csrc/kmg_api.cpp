@@ -109,6 +109,7 @@ struct Tuning {
                             // (kmg_nbhd.hip)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
+  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 / 3 grouped S = 1 / 2
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
                             // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
@@ -166,6 +167,7 @@ void read_tuning(Tuning &t) {
   t.pl_threads = env_or("KMG_PL_THREADS", d.pl_threads);
   if (t.pl_threads != 512 && t.pl_threads != 1024) t.pl_threads = 0;
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
+  t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -1217,7 +1219,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           StageTimer t(c, ST_SLOTS);  // the lists themselves
           KMG_HIP(launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                  c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
-                                 c->nb_lines.as<uint16_t>(), c->stream));
+                                 c->nb_lines.as<uint16_t>(), c->stream, c->tune.nb_fill));
         }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));

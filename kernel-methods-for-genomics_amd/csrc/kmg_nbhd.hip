@@ -223,6 +223,193 @@ __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
   }
 }
 
+// ------------------------------------------------------------------ grouped list fill
+// The lists of the 4^S k-mers u = (prefix P, suffix s_u) that share their first k - S letters
+// are built together by one workgroup.  Every Hamming <= 2 neighbour of such a u is
+// (prefix w, suffix s) with ham(w, P) + ham(s, s_u) <= 2, and the 4^S bins of one prefix w
+// are ADJACENT in the exact index (key order): the workgroup loads the m_S = 1 + 3(k-S) +
+// 9 C(k-S, 2) ranges [w 4^S, (w + 1) 4^S) of bins into LDS once (k = 9, S = 2: 211 ranges of
+// ~113 entries at N=20000), then every wave assembles lists from LDS: 352 runs a list in
+// segment order, a wave prefix sum placing each run, lane-per-run copies LDS -> HBM.  Per
+// list that is ~13 ranges' line requests instead of 352 runs' (the per-list fill above
+// gathered each run from L2 / the Infinity Cache: ~2.5 ms at N=20000).  A group whose ranges
+// overflow the LDS image (repetitive data) copies straight from the index (flat pointer).
+template <int S>
+__device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmask, int &h) {
+  // run j of a list, segment order: (prefix range r, suffix xor dmask, Hamming class h)
+  const int kp = k - S;
+  if (j == 0) {
+    r = 0; dmask = 0; h = 0;
+    return;
+  }
+  j -= 1;
+  if (j < 3 * S) {  // suffix Hamming 1, prefix 0
+    const int ps = j / 3, d = j - 3 * ps + 1;
+    r = 0; dmask = (uint32_t)d << (2 * (S - 1 - ps)); h = 1;
+    return;
+  }
+  j -= 3 * S;
+  if (j < 3 * kp) {  // prefix Hamming 1, suffix 0
+    r = 1 + j; dmask = 0; h = 1;
+    return;
+  }
+  j -= 3 * kp;
+  h = 2;
+  const int ns2 = 9 * S * (S - 1) / 2;
+  if (j < ns2) {  // suffix Hamming 2 (S = 2), prefix 0
+    r = 0; dmask = ((uint32_t)(j / 3 + 1) << 2) | (uint32_t)(j - 3 * (j / 3) + 1);
+    return;
+  }
+  j -= ns2;
+  if (j < 3 * kp * 3 * S) {  // prefix Hamming 1 x suffix Hamming 1
+    const int rp = j / (3 * S), js = j - rp * 3 * S;
+    const int ps = js / 3, d = js - 3 * ps + 1;
+    r = 1 + rp; dmask = (uint32_t)d << (2 * (S - 1 - ps));
+    return;
+  }
+  j -= 3 * kp * 3 * S;
+  r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
+}
+
+template <int S, int NT>
+__global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
+    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
+    uint32_t pad_col, int cap) {
+  constexpr int SW = 1 << (2 * S);
+  constexpr int NW = NT / 64;
+  extern __shared__ __align__(16) uint32_t fsm[];
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  uint32_t *roff = fsm;                      // [mr][SW + 1] absolute index offsets
+  uint32_t *rbase = roff + mr * (SW + 1);    // [mr + 1] LDS position of each range
+  uint32_t *wtot = rbase + mr + 1;           // [NW] scan scratch
+  uint16_t *ent = (uint16_t *)(wtot + NW);   // [cap] the ranges' entries
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t npref = 1u << (2 * kp);
+  const int nbn = nb_neighbours(k);
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
+    // ---- 1. the ranges' bin offsets and sizes; their LDS positions (block scan): thread t
+    // owns the ranges [t RPT, t RPT + RPT)
+    const int rpt = (mr + NT - 1) / NT;
+    uint32_t myn = 0;
+    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
+      uint32_t w = P;
+      if (r > 0) {
+        int t = r - 1;
+        if (t < 3 * kp) {
+          const int p = t / 3;
+          w ^= (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
+        } else {
+          t -= 3 * kp;
+          const int pi = t / 9, rr = t - 9 * pi;
+          int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
+          while (q * (q - 1) / 2 > pi) --q;
+          while ((q + 1) * q / 2 <= pi) ++q;
+          const int p = pi - q * (q - 1) / 2;
+          w ^= ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
+               ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
+        }
+      }
+      const uint32_t *o = xoff + cbase + (int64_t)w * SW;
+#pragma unroll
+      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
+      myn += o[SW] - o[0];
+    }
+    {
+      const uint32_t inc = nb_wave_incl_scan(myn);
+      if (lane == 63) wtot[wave] = inc;
+      __syncthreads();
+      uint32_t base = 0, total = 0;
+      for (int w2 = 0; w2 < NW; ++w2) {
+        base += w2 < wave ? wtot[w2] : 0u;
+        total += wtot[w2];
+      }
+      uint32_t run = base + inc - myn;
+      for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
+        rbase[r] = run;
+        run += roff[r * (SW + 1) + SW] - roff[r * (SW + 1)];
+      }
+      if (threadIdx.x == 0) rbase[mr] = total;
+      __syncthreads();
+    }
+    const uint32_t etot = rbase[mr];
+    const bool staged = etot <= (uint32_t)cap;
+    // ---- 2. the ranges into LDS, one wave a range, all of a range's loads in flight
+    if (staged) {
+      for (int r = wave; r < mr; r += NW) {
+        const uint32_t a = roff[r * (SW + 1)], n = roff[r * (SW + 1) + SW] - a, d = rbase[r];
+        for (uint32_t j0 = 0; j0 < n; j0 += 256) {
+          uint16_t v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t j = j0 + 64u * q + lane;
+            if (j < n) v[q] = xent[a + j];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t j = j0 + 64u * q + lane;
+            if (j < n) ent[d + j] = v[q];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 3. the 4^S lists, one wave a list
+    const int t2 = 1 + 3 * k;
+    for (int su = wave; su < SW; su += NW) {
+      const int64_t b = cbase + (int64_t)P * SW + su;
+      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+      if (tot == 0) continue;  // wave-uniform
+      const uint2 sg = nbseg[b];
+      uint16_t *dst = table + (size_t)start * 8u;
+      uint32_t carry = 0, n0 = 0, pre2 = 0;
+      for (int j0 = 0; j0 < nbn; j0 += 64) {
+        const int j = j0 + lane;
+        uint32_t cnt = 0, srcp = 0;
+        int h = 2;
+        if (j < nbn) {
+          int r;
+          uint32_t dm;
+          nb_run_desc<S>(j, k, r, dm, h);
+          const int sidx = su ^ (int)dm;
+          const uint32_t *ro = roff + r * (SW + 1);
+          const uint32_t a0 = ro[sidx];
+          cnt = ro[sidx + 1] - a0;
+          srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
+        }
+        const uint32_t inc = nb_wave_incl_scan(cnt);
+        const uint32_t pos = carry + inc - cnt;
+        if (j0 == 0) {
+          n0 = __shfl(cnt, 0, 64);
+          pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
+        }
+        carry += __shfl(inc, 63, 64);
+        const uint32_t segd = h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2;
+        uint16_t *o = dst + segd + pos;
+        if (staged) {
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = ent[srcp + e];
+        } else {
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = xent[srcp + e];
+        }
+      }
+      const uint32_t total = carry;
+      // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+      if (lane < 24) {
+        const int sgi = lane >> 3, e = lane & 7;
+        const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
+        const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+        const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+        const uint32_t pp = segb + segn + (uint32_t)e;
+        if (pp < segend) dst[pp] = (uint16_t)(pad_col + (pp & 63u));
+      }
+    }
+    __syncthreads();  // the next group overwrites the LDS image
+  }
+}
+
 // One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
 // triangle for a full square K).
 template <int K>
@@ -356,16 +543,39 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
-                          hipStream_t s) {
+                          hipStream_t s, int form) {
   const int64_t nbins = g.nbins();
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
+  const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;  // occurrences of a k-mer
+  if (form != 1 && g.k >= 4) {
+    // grouped fill: S = 2 (16 lists a workgroup of 1024 threads) while the expected LDS
+    // image stays <= 48 KB, else S = 1 (4 lists, 256 threads); the image is sized at 2x the
+    // expectation (larger groups copy straight from the index)
+    auto ranges = [&](int S) { const int kp = g.k - S; return 1 + 3 * kp + 9 * kp * (kp - 1) / 2; };
+    const double e2 = ranges(2) * 16.0 * mean, e1 = ranges(1) * 4.0 * mean;
+    const int S = (form == 3 || (form == 0 && e2 <= 24576.0)) ? 2 : 1;
+    const int SW = 1 << (2 * S), mr = ranges(S);
+    const int nt = S == 2 ? 1024 : 512;
+    const double e = S == 2 ? e2 : e1;
+    int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
+    cap = (cap + 7) & ~7;
+    const size_t lds = sizeof(uint32_t) * ((size_t)mr * (SW + 1) + mr + 1 + nt / 64) + 2 * (size_t)cap;
+    const int64_t ngroups = nbins / SW;
+    const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
+    if (S == 2)
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 1024>), dim3((unsigned)blocks), dim3(1024), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+    else
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 512>), dim3((unsigned)blocks), dim3(512), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+    return hipGetLastError();
+  }
   const int64_t wpb = NB_FILL_THREADS / 64;
   // waves in flight: 32 a CU x 256 CUs, each walking bins in key order (neighbouring
   // k-mers share most of their neighbours' posting lines in L2)
   const int64_t fill_blocks = std::min<int64_t>((nbins + wpb - 1) / wpb, 8 * 256);
   // lanes a run: the mean occurrences of a k-mer in a chunk, to a power of two in [4, 32]
-  const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;
   const int lg = mean <= 4.0 ? 4 : mean <= 8.0 ? 8 : mean <= 16.0 ? 16 : 32;
 #define KMG_NBF(LG_)                                                                             \
   hipLaunchKernelGGL(nb_fill_kernel<LG_>, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, \
