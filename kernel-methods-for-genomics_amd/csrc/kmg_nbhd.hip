@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
 constexpr int NB_MAXR = 10;    // neighbours a lane in step 1: ceil(631 / 64) at k = 12
 constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12, + the end)
 constexpr int NB_STEPS = 8;
+constexpr int NB_CSTEP = 4;    // grouped fill: copy steps with loads in flight
 
 template <int LG>
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
@@ -271,23 +272,25 @@ __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmas
   r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
 }
 
-template <int S, int NT>
+template <int S, int NT, int LG>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col, int cap) {
   constexpr int SW = 1 << (2 * S);
   constexpr int NW = NT / 64;
+  constexpr int G = 64 / LG;  // runs a copy step
   extern __shared__ __align__(16) uint32_t fsm[];
   const int kp = k - S;
   const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  const int nbn = nb_neighbours(k);
   uint32_t *roff = fsm;                      // [mr][SW + 1] absolute index offsets
   uint32_t *rbase = roff + mr * (SW + 1);    // [mr + 1] LDS position of each range
   uint32_t *wtot = rbase + mr + 1;           // [NW] scan scratch
   uint16_t *ent = (uint16_t *)(wtot + NW);   // [cap] the ranges' entries
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane / LG, gl = lane % LG;
   const uint32_t npref = 1u << (2 * kp);
-  const int nbn = nb_neighbours(k);
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
     const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
@@ -357,7 +360,10 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       }
     }
     __syncthreads();
-    // ---- 3. the 4^S lists, one wave a list
+    // ---- 3. the 4^S lists, one wave a list, 64 runs at a time (segment order): lane j
+    // places run j (wave prefix sum), then groups of LG lanes copy the chunk's runs, one run
+    // a group and G runs a step (the run's list position, source and count fetched from its
+    // lane by shuffles), NB_CSTEP steps' loads in flight
     const int t2 = 1 + 3 * k;
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
@@ -387,12 +393,32 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
           pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
         }
         carry += __shfl(inc, 63, 64);
-        const uint32_t segd = h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2;
-        uint16_t *o = dst + segd + pos;
-        if (staged) {
-          for (uint32_t e = 0; e < cnt; ++e) o[e] = ent[srcp + e];
-        } else {
-          for (uint32_t e = 0; e < cnt; ++e) o[e] = xent[srcp + e];
+        const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+        uint32_t mx = cnt;  // the chunk's longest run (copy steps of LG entries)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+        for (int st0 = 0; st0 < LG; st0 += NB_CSTEP) {
+          uint32_t cd[NB_CSTEP], cs[NB_CSTEP], cc[NB_CSTEP];
+#pragma unroll
+          for (int q = 0; q < NB_CSTEP; ++q) {
+            const int jl = (st0 + q) * G + grp;
+            cd[q] = __shfl(dpos, jl, 64);
+            cs[q] = __shfl(srcp, jl, 64);
+            cc[q] = __shfl(cnt, jl, 64);
+          }
+          for (uint32_t e0 = 0; e0 < mx; e0 += LG) {
+            uint16_t v[NB_CSTEP];
+#pragma unroll
+            for (int q = 0; q < NB_CSTEP; ++q) {
+              const uint32_t e = e0 + gl;
+              if (e < cc[q]) v[q] = staged ? ent[cs[q] + e] : xent[cs[q] + e];
+            }
+#pragma unroll
+            for (int q = 0; q < NB_CSTEP; ++q) {
+              const uint32_t e = e0 + gl;
+              if (e < cc[q]) dst[cd[q] + e] = v[q];
+            }
+          }
         }
       }
       const uint32_t total = carry;
@@ -563,12 +589,18 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     const size_t lds = sizeof(uint32_t) * ((size_t)mr * (SW + 1) + mr + 1 + nt / 64) + 2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
-    if (S == 2)
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 1024>), dim3((unsigned)blocks), dim3(1024), lds, s,
-                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
-    else
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 512>), dim3((unsigned)blocks), dim3(512), lds, s,
-                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+    const int lg = mean <= 8.0 ? 8 : 16;
+#define KMG_NBG(S_, NT_, LG_)                                                                   \
+  hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, LG_>), dim3((unsigned)blocks), dim3(NT_), \
+                     lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
+    if (S == 2) {
+      if (lg == 8) KMG_NBG(2, 1024, 8);
+      else KMG_NBG(2, 1024, 16);
+    } else {
+      if (lg == 8) KMG_NBG(1, 512, 8);
+      else KMG_NBG(1, 512, 16);
+    }
+#undef KMG_NBG
     return hipGetLastError();
   }
   const int64_t wpb = NB_FILL_THREADS / 64;
