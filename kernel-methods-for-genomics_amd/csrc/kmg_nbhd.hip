@@ -123,7 +123,6 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
 constexpr int NB_MAXR = 10;    // neighbours a lane in step 1: ceil(631 / 64) at k = 12
 constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12, + the end)
 constexpr int NB_STEPS = 8;
-constexpr int NB_CSTEP = 4;    // grouped fill: copy steps with loads in flight
 
 template <int LG>
 __global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
@@ -272,51 +271,63 @@ __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmas
   r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
 }
 
-template <int S, int NT, int LG>
+template <int S, int NT>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
     uint32_t pad_col, int cap) {
   constexpr int SW = 1 << (2 * S);
   constexpr int NW = NT / 64;
-  constexpr int G = 64 / LG;  // runs a copy step
   extern __shared__ __align__(16) uint32_t fsm[];
   const int kp = k - S;
   const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
   const int nbn = nb_neighbours(k);
-  uint32_t *roff = fsm;                      // [mr][SW + 1] absolute index offsets
+  uint32_t *rt = fsm;                        // [nbn] run j: r | suffix xor << 16 | class << 24
+  uint32_t *pm = rt + nbn;                   // [mr] prefix xor of range r
+  uint32_t *roff = pm + mr;                  // [mr][SW + 1] absolute index offsets
   uint32_t *rbase = roff + mr * (SW + 1);    // [mr + 1] LDS position of each range
   uint32_t *wtot = rbase + mr + 1;           // [NW] scan scratch
   uint16_t *ent = (uint16_t *)(wtot + NW);   // [cap] the ranges' entries
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int grp = lane / LG, gl = lane % LG;
   const uint32_t npref = 1u << (2 * kp);
+  // the run and range tables, once per workgroup (the grid is persistent)
+  for (int j = threadIdx.x; j < nbn; j += NT) {
+    int r, h;
+    uint32_t dm;
+    nb_run_desc<S>(j, k, r, dm, h);
+    rt[j] = (uint32_t)r | (dm << 16) | ((uint32_t)h << 24);
+  }
+  for (int r = threadIdx.x; r < mr; r += NT) {
+    uint32_t w = 0;
+    if (r > 0) {
+      int t = r - 1;
+      if (t < 3 * kp) {
+        const int p = t / 3;
+        w = (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
+      } else {
+        t -= 3 * kp;
+        const int pi = t / 9, rr = t - 9 * pi;
+        int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
+        while (q * (q - 1) / 2 > pi) --q;
+        while ((q + 1) * q / 2 <= pi) ++q;
+        const int p = pi - q * (q - 1) / 2;
+        w = ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
+            ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
+      }
+    }
+    pm[r] = w;
+  }
+  __syncthreads();
+  const int rpt = (mr + NT - 1) / NT;
+  const int t2 = 1 + 3 * k;
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
     const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
     // ---- 1. the ranges' bin offsets and sizes; their LDS positions (block scan): thread t
     // owns the ranges [t RPT, t RPT + RPT)
-    const int rpt = (mr + NT - 1) / NT;
     uint32_t myn = 0;
     for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
-      uint32_t w = P;
-      if (r > 0) {
-        int t = r - 1;
-        if (t < 3 * kp) {
-          const int p = t / 3;
-          w ^= (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
-        } else {
-          t -= 3 * kp;
-          const int pi = t / 9, rr = t - 9 * pi;
-          int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
-          while (q * (q - 1) / 2 > pi) --q;
-          while ((q + 1) * q / 2 <= pi) ++q;
-          const int p = pi - q * (q - 1) / 2;
-          w ^= ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
-               ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
-        }
-      }
-      const uint32_t *o = xoff + cbase + (int64_t)w * SW;
+      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
 #pragma unroll
       for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
       myn += o[SW] - o[0];
@@ -360,11 +371,8 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       }
     }
     __syncthreads();
-    // ---- 3. the 4^S lists, one wave a list, 64 runs at a time (segment order): lane j
-    // places run j (wave prefix sum), then groups of LG lanes copy the chunk's runs, one run
-    // a group and G runs a step (the run's list position, source and count fetched from its
-    // lane by shuffles), NB_CSTEP steps' loads in flight
-    const int t2 = 1 + 3 * k;
+    // ---- 3. the 4^S lists, one wave a list, 64 runs at a time in segment order: lane j
+    // places run j (wave prefix sum) and copies it
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
@@ -374,14 +382,13 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       uint32_t carry = 0, n0 = 0, pre2 = 0;
       for (int j0 = 0; j0 < nbn; j0 += 64) {
         const int j = j0 + lane;
-        uint32_t cnt = 0, srcp = 0;
-        int h = 2;
+        uint32_t cnt = 0, srcp = 0, h = 2;
         if (j < nbn) {
-          int r;
-          uint32_t dm;
-          nb_run_desc<S>(j, k, r, dm, h);
-          const int sidx = su ^ (int)dm;
+          const uint32_t d = rt[j];
+          const uint32_t r = d & 0xFFFFu;
+          h = d >> 24;
           const uint32_t *ro = roff + r * (SW + 1);
+          const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
           const uint32_t a0 = ro[sidx];
           cnt = ro[sidx + 1] - a0;
           srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
@@ -393,32 +400,13 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
           pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
         }
         carry += __shfl(inc, 63, 64);
-        const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        uint32_t mx = cnt;  // the chunk's longest run (copy steps of LG entries)
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-        for (int st0 = 0; st0 < LG; st0 += NB_CSTEP) {
-          uint32_t cd[NB_CSTEP], cs[NB_CSTEP], cc[NB_CSTEP];
-#pragma unroll
-          for (int q = 0; q < NB_CSTEP; ++q) {
-            const int jl = (st0 + q) * G + grp;
-            cd[q] = __shfl(dpos, jl, 64);
-            cs[q] = __shfl(srcp, jl, 64);
-            cc[q] = __shfl(cnt, jl, 64);
-          }
-          for (uint32_t e0 = 0; e0 < mx; e0 += LG) {
-            uint16_t v[NB_CSTEP];
-#pragma unroll
-            for (int q = 0; q < NB_CSTEP; ++q) {
-              const uint32_t e = e0 + gl;
-              if (e < cc[q]) v[q] = staged ? ent[cs[q] + e] : xent[cs[q] + e];
-            }
-#pragma unroll
-            for (int q = 0; q < NB_CSTEP; ++q) {
-              const uint32_t e = e0 + gl;
-              if (e < cc[q]) dst[cd[q] + e] = v[q];
-            }
-          }
+        uint16_t *o = dst + (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+        if (staged) {
+          const uint16_t *src = ent + srcp;
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
+        } else {
+          const uint16_t *src = xent + srcp;
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
         }
       }
       const uint32_t total = carry;
@@ -586,21 +574,17 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     const double e = S == 2 ? e2 : e1;
     int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
     cap = (cap + 7) & ~7;
-    const size_t lds = sizeof(uint32_t) * ((size_t)mr * (SW + 1) + mr + 1 + nt / 64) + 2 * (size_t)cap;
+    const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
+    const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
+                       2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
-    const int lg = mean <= 8.0 ? 8 : 16;
-#define KMG_NBG(S_, NT_, LG_)                                                                   \
-  hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, LG_>), dim3((unsigned)blocks), dim3(NT_), \
-                     lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
-    if (S == 2) {
-      if (lg == 8) KMG_NBG(2, 1024, 8);
-      else KMG_NBG(2, 1024, 16);
-    } else {
-      if (lg == 8) KMG_NBG(1, 512, 8);
-      else KMG_NBG(1, 512, 16);
-    }
-#undef KMG_NBG
+    if (S == 2)
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 1024>), dim3((unsigned)blocks), dim3(1024), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+    else
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 512>), dim3((unsigned)blocks), dim3(512), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
     return hipGetLastError();
   }
   const int64_t wpb = NB_FILL_THREADS / 64;

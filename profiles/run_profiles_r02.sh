@@ -18,6 +18,8 @@ case_of() {
     mm3_n20000) echo '[{"kind":"mm","k":9,"n":20000,"steps":5,"check":false,"KMG_MM_FORM":"3"}]' ;;
     wd_n9000)  echo '[{"kind":"wd","d":5,"n":9000,"steps":10,"check":false}]' ;;
     nb_n20000) echo '[{"kind":"mm","k":9,"n":20000,"steps":5,"check":false,"KMG_MM_FORM":"4","KMG_MM_CHUNK":"20000","KMG_MM_TRI":"0"}]' ;;
+    nbf1) echo '[{"kind":"mm","k":9,"n":20000,"steps":3,"check":false,"KMG_MM_FORM":"4","KMG_MM_CHUNK":"20000","KMG_MM_TRI":"0","KMG_NB_FILL":"1"}]' ;;
+    nbf3) echo '[{"kind":"mm","k":9,"n":20000,"steps":3,"check":false,"KMG_MM_FORM":"4","KMG_MM_CHUNK":"20000","KMG_MM_TRI":"0","KMG_NB_FILL":"3"}]' ;;
     config5_full) echo '[{"kind":"mm","k":9,"n":200000,"norm":0,"seed":5,"steps":2,"check":false}]' ;;
     config5_slab) echo '[{"kind":"mm","k":9,"n":200000,"rows":25000,"norm":1,"seed":5,"steps":3,"check":false}]' ;;
   esac
