@@ -383,6 +383,7 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         wall = time.perf_counter() - t0
         ctx.set_timing(False)
         stages = stage_means(ctx)
+        plan = ctx.last_plan()
         ok = True
         for r in spot_rows:
             row = np.empty(n, dtype=L.DTYPES[out_dtype])
@@ -395,7 +396,7 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         ctx.dfree(d_lens)
     ms = wall / steps * 1e3
     return {"N": n, "rows": r1 - r0, "steps": steps, "ms_per_step": ms,
-            "pairs_per_s": (r1 - r0) * n / (ms / 1e3), "stages_ms": stages,
+            "pairs_per_s": (r1 - r0) * n / (ms / 1e3), "stages_ms": stages, "plan": plan,
             "spot_check_rows": list(spot_rows), "spot_check": ok}
 
 
@@ -771,18 +772,20 @@ def projection(sp, n, extra):
     if c5:
         s5 = c5["stages_ms"]
         t5_index = sum(v for k, v in s5.items() if k in ("count", "scan", "place", "fine", "pack",
-                                                         "slots"))
+                                                         "lists", "slots"))
         n5 = c5["N"]
-        # the one-GPU build computes the upper block triangle (7 chunks: (7 + 1) / 14 of the
-        # full rows) and mirrors the rest: the model wants the full-row Gram time
-        nch = -(-n5 // _chunked(n5, 28572))
+        # the one-GPU build computes the upper block triangle ((nch + 1) / (2 nch) of the full
+        # rows, nch from the plan the library reported) and mirrors the rest: the model wants
+        # the full-row Gram time
+        plan5 = c5.get("plan") or {}
+        ch5 = plan5.get("chunk") or _chunked(n5, 28572)
+        nch = -(-n5 // ch5)
         g_rows = s5["gram"] * (2.0 * nch) / (nch + 1) if s5.get("mirror") else s5["gram"]
         out["config5_mismatch_k9_n200000_raw_int32"] = {
             "one_gpu": {"gram_ms": s5["gram"], "mirror_ms": s5.get("mirror"),
                         "full_rows_gram_ms_model": g_rows},
             **{str(g): v for g, v in scaling_projection(
-                n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1,
-                chunk=_chunked(n5, 28572)).items()}}
+                n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1, chunk=ch5).items()}}
     return out
 
 

@@ -325,6 +325,7 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
     const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 4^S lists empty (uniform)
     // ---- 1. the ranges' bin offsets and sizes; their LDS positions (block scan): thread t
     // owns the ranges [t RPT, t RPT + RPT)
     uint32_t myn = 0;
@@ -548,7 +549,10 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
 }
 
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
-  return (int64_t)(1 + 3 * k + 9 * k * (k - 1) / 2) * occurrences + 21 * nbins;
+  // every occurrence sits in the lists of its 1 + 3k + 9k(k-1)/2 neighbours; a non-empty list
+  // pads each of its three segments by at most 7 entries
+  const int64_t e = (int64_t)(1 + 3 * k + 9 * k * (k - 1) / 2) * occurrences;
+  return e + 21 * std::min(nbins, e);
 }
 
 size_t nb_gram_lds(const IndexGeom &g, const Packed &pk) {

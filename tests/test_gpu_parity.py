@@ -153,10 +153,13 @@ def test_spectrum_long_sequences_unpacked(ctx):
 
 def _form(tune, form):
     """"F" -> KMG_MM_FORM=F; "F:T" also KMG_PL_THREADS=T (pair lines, 512: two workgroups a CU,
-    1024: one; unset: by size)"""
-    f, _, t = form.partition(":")
+    1024: one; unset: by size) or KMG_NB_THREADS=T (neighbourhood lists); "4:T:L" also
+    KMG_NB_FILL=L (the list fill: 1 per list, 2 / 3 grouped by 4 / 16 lists)"""
+    f, _, rest = form.partition(":")
+    t, _, fill = rest.partition(":")
     tune(KMG_MM_FORM=f, KMG_PL_THREADS=(t or None) if f == "3" else None,
-         KMG_NB_THREADS=(t or None) if f == "4" else None)
+         KMG_NB_THREADS=(t or None) if f == "4" else None,
+         KMG_NB_FILL=(fill or None) if f == "4" else None)
 
 
 @pytest.mark.parametrize("form", ["0", "3:1024", "3:512", "4:1024", "4:512"])
@@ -187,6 +190,23 @@ def test_mismatch_k9_n20000(ctx, tune, form):
     raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes[:3000],
                    lens[:3000], L.KMG_I32)
     assert np.array_equal(raw[:16].astype(np.int64), cref.mismatch_raw(codes[:3000], lens[:3000], 9, 1, rows=(0, 16)))
+
+
+@pytest.mark.parametrize("k", [4, 9, 12])
+@pytest.mark.parametrize("fill", ["1", "2", "3"])
+def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
+    """The three neighbourhood-list fills (per list; grouped by the 4 / 16 lists sharing a
+    prefix, ranges staged in LDS) build the same lists: raw K bit-exact over several column
+    chunkings, one of them small enough to overflow the LDS range image (direct copies)."""
+    codes, lens = E.synthetic(600, 101, seed=90 + k)
+    codes[:40] = 0  # poly-A rows: long runs, groups past the LDS image
+    ref = cref.mismatch_raw(codes, lens, k, 1)
+    tune(KMG_MM_FORM=4, KMG_NB_FILL=fill)
+    for chunk in (("96", "20480") if k < 12 else ("20480",)):  # (k = 12: 4^12 bins a chunk)
+        tune(KMG_MM_CHUNK=chunk)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), ref), chunk
 
 
 @pytest.mark.parametrize("k,m", [(2, 1), (5, 1), (7, 1), (12, 1), (5, 0), (5, 2), (4, 3), (13, 1)])
@@ -235,7 +255,7 @@ def test_mismatch_pairs_k_range(ctx, tune, k, form):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4", "4::1", "4::2", "4::3"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
     >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
@@ -255,7 +275,7 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     assert np.array_equal(raw, raw.T)
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4", "4::1", "4::2", "4::3"])
 def test_mismatch_stress_repeats(ctx, tune, form):
     _form(tune, form)
     codes, lens = E.synthetic(40, 101, seed=12)
