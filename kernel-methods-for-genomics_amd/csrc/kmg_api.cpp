@@ -629,8 +629,10 @@ int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int thre
     const double row_reads = 2.0 * nb * pmax * dens * (double)n + 2.0 * 10.5 * pmax * nch;
     const double gram = (double)n * (row_reads + esz * (double)n) * f;
     const double mirror = tri_esz > 0 ? 2.0 * esz * (double)n * n * (double)(nch - 1) / (2.0 * nch) : 0.0;
-    // + building the lists: a fixed cost per (chunk, k-mer) bin on top of the bytes
-    const double build = (double)nch * (double)pow4(k) * 1.0e-9;
+    // + building the lists: ~2 ns per (chunk, k-mer) bin plus the table at ~1 TB/s (grouped
+    // fill, measured: N=20000 one chunk 1.44 ms, N=200000 five chunks ~13 ms)
+    const double build = (double)nch * (double)pow4(k) * 2.0e-9 +
+                         2.0 * nb * (double)n * pmax / 1e12;
     const double cost = gram / 6e12 + mirror / 5e12 + build;
     if (cost < best_cost * (1.0 - 1e-12)) {
       best_cost = cost;
@@ -852,7 +854,10 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   //   k = 8 and 12: the drop-one slot table (k = 8: 6.70 vs 7.78 pair lines, 15.8 pairs).
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
-  const bool use_nb = s1 && k >= 3 && k <= 12 && form == 4;
+  // k = 9 (BASELINE configs[2] and [4]): the neighbourhood lists at every n (N=20000
+  // normalised build 4.03 -> 3.73 ms, N=200000 one-GPU raw K 185.5 -> 134.8 ms against the
+  // pair lines / slot table; profiles/r04_nb_*)
+  const bool use_nb = s1 && k >= 3 && k <= 12 && (form == 4 || (form == 0 && k == 9));
   const bool use_pl =
       s1 && !use_nb && k >= 3 && k <= 12 && (form == 3 || (form == 0 && k == 9 && n <= 24000));
   const bool use_pairs = s1 && !use_pl && !use_nb &&

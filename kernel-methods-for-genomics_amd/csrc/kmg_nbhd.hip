@@ -271,7 +271,7 @@ __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmas
   r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
 }
 
-template <int S, int NT, int W>
+template <int S, int NT>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
@@ -287,10 +287,8 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
   uint32_t *roff = pm + mr;                  // [mr][SW + 1] absolute index offsets
   uint32_t *rbase = roff + mr * (SW + 1);    // [mr + 1] LDS position of each range
   uint32_t *wtot = rbase + mr + 1;           // [NW] scan scratch
-  uint16_t *img_all = (uint16_t *)(((uintptr_t)(wtot + NW) + 15) & ~(uintptr_t)15);  // [NW][W]
-  uint16_t *ent = img_all + NW * W;          // [cap] the ranges' entries
+  uint16_t *ent = (uint16_t *)(wtot + NW);   // [cap] the ranges' entries
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint16_t *img = img_all + wave * W;        // this wave's window of its list
   const uint32_t npref = 1u << (2 * kp);
   // the run and range tables, once per workgroup (the grid is persistent)
   for (int j = threadIdx.x; j < nbn; j += NT) {
@@ -374,61 +372,53 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       }
     }
     __syncthreads();
-    // ---- 3. the 4^S lists, one wave a list, assembled in windows of W entries in the wave's
-    // LDS image and written out with 16-byte stores.  Per window the runs are walked 64 at a
-    // time in segment order: lane j places run j (wave prefix sum) and copies its part inside
-    // the window (LDS -> LDS); the segments' dummy tails too.
+    // ---- 3. the 4^S lists, one wave a list, 64 runs at a time in segment order: lane j
+    // places run j (wave prefix sum) and copies it
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
       if (tot == 0) continue;  // wave-uniform
       const uint2 sg = nbseg[b];
-      uint4 *dst4 = (uint4 *)(table + (size_t)start * 8u);
-      for (uint32_t w0 = 0; w0 < tot * 8u; w0 += W) {
-        const uint32_t w1 = min(tot * 8u, w0 + (uint32_t)W);
-        uint32_t carry = 0, n0 = 0, pre2 = 0;
-        for (int j0 = 0; j0 < nbn; j0 += 64) {
-          const int j = j0 + lane;
-          uint32_t cnt = 0, srcp = 0, h = 2;
-          if (j < nbn) {
-            const uint32_t d = rt[j];
-            const uint32_t r = d & 0xFFFFu;
-            h = d >> 24;
-            const uint32_t *ro = roff + r * (SW + 1);
-            const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
-            const uint32_t a0 = ro[sidx];
-            cnt = ro[sidx + 1] - a0;
-            srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
-          }
-          const uint32_t inc = nb_wave_incl_scan(cnt);
-          const uint32_t pos = carry + inc - cnt;
-          if (j0 == 0) {
-            n0 = __shfl(cnt, 0, 64);
-            pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
-          }
-          carry += __shfl(inc, 63, 64);
-          const uint32_t dp = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-          const uint32_t lo = max(dp, w0), hi = min(dp + cnt, w1);
-          if (staged) {
-            for (uint32_t e = lo; e < hi; ++e) img[e - w0] = ent[srcp + (e - dp)];
-          } else {
-            for (uint32_t e = lo; e < hi; ++e) img[e - w0] = xent[srcp + (e - dp)];
-          }
+      uint16_t *dst = table + (size_t)start * 8u;
+      uint32_t carry = 0, n0 = 0, pre2 = 0;
+      for (int j0 = 0; j0 < nbn; j0 += 64) {
+        const int j = j0 + lane;
+        uint32_t cnt = 0, srcp = 0, h = 2;
+        if (j < nbn) {
+          const uint32_t d = rt[j];
+          const uint32_t r = d & 0xFFFFu;
+          h = d >> 24;
+          const uint32_t *ro = roff + r * (SW + 1);
+          const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
+          const uint32_t a0 = ro[sidx];
+          cnt = ro[sidx + 1] - a0;
+          srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
         }
-        const uint32_t total = carry;
-        if (lane < 24) {  // dummy columns after each segment (64 distinct LDS words)
-          const int sgi = lane >> 3, e = lane & 7;
-          const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
-          const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
-          const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
-          const uint32_t pp = segb + segn + (uint32_t)e;
-          if (pp < segend && pp >= w0 && pp < w1) img[pp - w0] = (uint16_t)(pad_col + (pp & 63u));
+        const uint32_t inc = nb_wave_incl_scan(cnt);
+        const uint32_t pos = carry + inc - cnt;
+        if (j0 == 0) {
+          n0 = __shfl(cnt, 0, 64);
+          pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        const uint4 *img4 = (const uint4 *)img;
-        for (uint32_t q = lane; q < (w1 - w0) / 8u; q += 64) dst4[w0 / 8u + q] = img4[q];
-        __builtin_amdgcn_wave_barrier();  // the next window / list overwrites the image
+        carry += __shfl(inc, 63, 64);
+        uint16_t *o = dst + (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+        if (staged) {
+          const uint16_t *src = ent + srcp;
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
+        } else {
+          const uint16_t *src = xent + srcp;
+          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
+        }
+      }
+      const uint32_t total = carry;
+      // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+      if (lane < 24) {
+        const int sgi = lane >> 3, e = lane & 7;
+        const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
+        const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+        const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+        const uint32_t pp = segb + segn + (uint32_t)e;
+        if (pp < segend) dst[pp] = (uint16_t)(pad_col + (pp & 63u));
       }
     }
     __syncthreads();  // the next group overwrites the LDS image
@@ -581,27 +571,27 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     // image stays <= 48 KB, else S = 1 (4 lists, 256 threads); the image is sized at 2x the
     // expectation (larger groups copy straight from the index)
     auto ranges = [&](int S) { const int kp = g.k - S; return 1 + 3 * kp + 9 * kp * (kp - 1) / 2; };
-    const double e2 = ranges(2) * 16.0 * mean, e1 = ranges(1) * 4.0 * mean;
-    const int S = (form == 3 || (form == 0 && e2 <= 24576.0)) ? 2 : 1;
+    const double e2 = ranges(2) * 16.0 * mean, e1 = ranges(1) * 4.0 * mean;  // LDS entries
+    // S = 2 unless forced: it beat S = 1 at both sizes measured, also where the range image
+    // overflows the LDS for part of the groups (N=200000 rank slab: fill 13.2 vs 23.3 ms;
+    // N=20000: 1.44 vs 2.43 ms, profiles/r04_nb_fill.jsonl)
+    const int S = form == 2 ? 1 : 2;
     const int SW = 1 << (2 * S), mr = ranges(S);
-    // S = 2: 512 threads (8 waves, 2 lists each), 8 KB list windows; S = 1: 256 threads
-    const int nt = S == 2 ? 512 : 256, W = S == 2 ? 4096 : 4096;
+    const int nt = S == 2 ? 1024 : 512;
     const double e = S == 2 ? e2 : e1;
+    int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
+    cap = (cap + 7) & ~7;
     const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
-    const size_t fixed = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
-                         16 + 2 * (size_t)(nt / 64) * W;
-    const double room = ((S == 2 ? 160.0 : 80.0) * 1024.0 - (double)fixed) / 2.0;
-    int cap = (int)std::min(1.5 * e + 1024.0, room);
-    cap = std::max(0, cap & ~7);
-    const size_t lds = fixed + 2 * (size_t)cap;
+    const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
+                       2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
     if (S == 2)
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 512, 4096>), dim3((unsigned)blocks), dim3(512), lds,
-                         s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 1024>), dim3((unsigned)blocks), dim3(1024), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
     else
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 256, 4096>), dim3((unsigned)blocks), dim3(256), lds,
-                         s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 512>), dim3((unsigned)blocks), dim3(512), lds, s,
+                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
     return hipGetLastError();
   }
   const int64_t wpb = NB_FILL_THREADS / 64;

@@ -175,9 +175,12 @@ def test_mismatch_k9_n20000(ctx, tune, form):
     if form.startswith("4"):
         assert plan["formulation"] == "neighbourhood" and plan["threads"] == int(form[2:])
         assert plan["triangle"] == (plan["nchunks"] > 1)
+    elif form == "0":           # default at k = 9: the neighbourhood lists, one chunk
+        assert plan["formulation"] == "neighbourhood"
+        assert (plan["threads"], plan["nchunks"], plan["triangle"]) == (1024, 1, False)
     else:
         assert plan["formulation"] == "pair_lines"
-    if form in ("0", "3:512"):  # 512 threads: 2 chunks of 10000, upper block triangle + mirror
+    if form == "3:512":         # 512 threads: 2 chunks of 10000, upper block triangle + mirror
         assert (plan["threads"], plan["nchunks"], plan["chunk"], plan["triangle"]) == (512, 2, 10000, True)
     elif form == "3:1024":      # 1024 threads: chunks of up to ~24000 columns (cost model)
         assert plan["threads"] == 1024 and plan["triangle"] == (plan["nchunks"] > 1)
