@@ -69,7 +69,7 @@ def main():
         kernels[short(k)] = {"fetch_bytes_raw": fk, "fetch_bytes_x2": 2 * fk, "write_bytes": wk,
                              "hbm_bytes_est": 2 * fk + wk, "avg_ns": stats.get(short(k))}
     gram = next((v for k, v in kernels.items()
-                 if any(g in k for g in ("gram_sp_kernel", "gram_pl_kernel", "gram_mm"))), None)
+                 if any(g in k for g in ("gram_sp_kernel", "gram_pl_kernel", "gram_mm", "gram_nb"))), None)
     out = {"tag": tag, "workload": workload, "N": n, "kernels": kernels,
            "hbm_bytes_per_launch": gram["hbm_bytes_est"] if gram else None}
     with open(os.path.join(HERE, f"{tag}_pmc.json"), "w") as f:
