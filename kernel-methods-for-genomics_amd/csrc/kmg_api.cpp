@@ -109,7 +109,8 @@ struct Tuning {
                             // (kmg_nbhd.hip)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
-  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 / 3 grouped S = 1 / 2
+  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 grouped S = 1,
+                            // 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
                             // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)

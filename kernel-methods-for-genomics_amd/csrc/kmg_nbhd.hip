@@ -271,7 +271,34 @@ __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmas
   r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
 }
 
-template <int S, int NT>
+// copy one run of n uint16 entries to o (any alignment): WS = 1 one 2-byte store an entry;
+// WS = 2 dword stores of entry pairs (o aligned to 4 bytes in the middle); WS = 4 also
+// 8-byte stores of aligned quads
+template <int WS, typename Src>
+__device__ __forceinline__ void nb_copy_run(uint16_t *o, const Src *src, uint32_t n) {
+  uint32_t e = 0;
+  if constexpr (WS >= 2) {
+    if (n && (((uintptr_t)o) & 2)) {
+      o[0] = src[0];
+      e = 1;
+    }
+    if constexpr (WS >= 4) {
+      if (e + 1 < n && (((uintptr_t)(o + e)) & 4)) {
+        *(uint32_t *)(o + e) = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
+        e += 2;
+      }
+      for (; e + 3 < n; e += 4) {
+        const uint32_t lo = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
+        const uint32_t hi = (uint32_t)src[e + 2] | ((uint32_t)src[e + 3] << 16);
+        *(uint2 *)(o + e) = make_uint2(lo, hi);
+      }
+    }
+    for (; e + 1 < n; e += 2) *(uint32_t *)(o + e) = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
+  }
+  for (; e < n; ++e) o[e] = src[e];
+}
+
+template <int S, int NT, int WS>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
@@ -402,13 +429,10 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
         }
         carry += __shfl(inc, 63, 64);
         uint16_t *o = dst + (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        if (staged) {
-          const uint16_t *src = ent + srcp;
-          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
-        } else {
-          const uint16_t *src = xent + srcp;
-          for (uint32_t e = 0; e < cnt; ++e) o[e] = src[e];
-        }
+        if (staged)
+          nb_copy_run<WS>(o, ent + srcp, cnt);
+        else
+          nb_copy_run<WS>(o, xent + srcp, cnt);
       }
       const uint32_t total = carry;
       // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
@@ -586,12 +610,19 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
                        2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
-    if (S == 2)
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<2, 1024>), dim3((unsigned)blocks), dim3(1024), lds, s,
-                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
-    else
-      hipLaunchKernelGGL((nb_fill_grouped_kernel<1, 512>), dim3((unsigned)blocks), dim3(512), lds, s,
-                         g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+    // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 5)
+    const int ws = form == 3 ? 1 : form == 4 ? 2 : 4;
+#define KMG_NBG(S_, NT_, WS_)                                                                  \
+  hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, WS_>), dim3((unsigned)blocks), dim3(NT_), \
+                     lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
+    if (S == 2) {
+      if (ws == 1) KMG_NBG(2, 1024, 1);
+      else if (ws == 2) KMG_NBG(2, 1024, 2);
+      else KMG_NBG(2, 1024, 4);
+    } else {
+      KMG_NBG(1, 512, 4);
+    }
+#undef KMG_NBG
     return hipGetLastError();
   }
   const int64_t wpb = NB_FILL_THREADS / 64;
