@@ -109,6 +109,7 @@ struct Tuning {
                             // (kmg_nbhd.hip)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
+  int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
   int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 grouped S = 1,
                             // 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
@@ -169,6 +170,7 @@ void read_tuning(Tuning &t) {
   if (t.pl_threads != 512 && t.pl_threads != 1024) t.pl_threads = 0;
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
+  t.nb_cap = env_or("KMG_NB_CAP", d.nb_cap);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -1225,7 +1227,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           StageTimer t(c, ST_SLOTS);  // the lists themselves
           KMG_HIP(launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                  c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
-                                 c->nb_lines.as<uint16_t>(), c->stream, c->tune.nb_fill));
+                                 c->nb_lines.as<uint16_t>(), c->stream, c->tune.nb_fill,
+                                 c->tune.nb_cap));
         }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));

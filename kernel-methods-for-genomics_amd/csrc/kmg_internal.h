@@ -281,7 +281,7 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 // grouped S = 2 with 2- / 4- / 8-byte stores
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
-                          hipStream_t s, int form = 0);
+                          hipStream_t s, int form = 0, int cap_override = -1);
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,

@@ -585,7 +585,7 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
-                          hipStream_t s, int form) {
+                          hipStream_t s, int form, int cap_override) {
   const int64_t nbins = g.nbins();
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
@@ -605,13 +605,15 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     const double e = S == 2 ? e2 : e1;
     int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
     cap = (cap + 7) & ~7;
+    if (cap_override >= 0) cap = std::min(cap, cap_override & ~7);  // (KMG_NB_CAP, tuning)
     const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
     const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
                        2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
-    // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 5)
-    const int ws = form == 3 ? 1 : form == 4 ? 2 : 4;
+    // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 1: the wider stores measured
+    // equal or slower, N=200000 rank slab fill 9.1 -> 15.1 ms, profiles/r04_nb_fill.jsonl r04n)
+    const int ws = form == 4 ? 2 : form == 5 ? 4 : 1;
 #define KMG_NBG(S_, NT_, WS_)                                                                  \
   hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, WS_>), dim3((unsigned)blocks), dim3(NT_), \
                      lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
