@@ -449,6 +449,157 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
   }
 }
 
+// ------------------------------------------------------------------ range-major fill
+// The grouped fill's copies run range-major: the 16 lists of a group (S = 2) take their runs
+// from the 211 prefix ranges, and the 16 sub-bins of one range are contiguous in the index.
+//  1. the ranges' sub-bin offsets (as the grouped fill);
+//  2. one wave a list places its 352 runs (wave prefix sums in segment order) into an LDS
+//     position table pos[list][run] and writes the segments' dummy tails;
+//  3. one wave a range copies the range's entries 64 at a time (coalesced 2-byte loads),
+//     each entry to every list that takes its sub-bin (1 list for the 189 Hamming-2 prefix
+//     ranges, 7 for the 21 Hamming-1 ones, 16 for the group's own prefix): the sub-bin from
+//     the 17 offsets held in SGPRs, the run from an inverse table inv[range][suffix xor].
+// Per group ~420 load and ~700 store instructions, against ~2900 for lane-per-run copies
+// whose lanes idle past the mean run (7 entries of a 64-run chunk whose longest has ~15).
+__global__ __launch_bounds__(1024) void nb_fill_ranges_kernel(
+    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
+    uint32_t pad_col) {
+  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  extern __shared__ __align__(16) uint32_t fsm[];
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  const int nbn = nb_neighbours(k);
+  uint32_t *rt = fsm;                        // [nbn] run j: r | suffix xor << 16 | class << 24
+  uint32_t *pm = rt + nbn;                   // [mr] prefix xor of range r
+  uint32_t *roff = pm + mr;                  // [mr][17] absolute index offsets
+  uint32_t *pos = roff + mr * (SW + 1);      // [SW][nbn] list position of run j (entries)
+  uint32_t *lst = pos + SW * nbn;            // [SW] list start (pieces)
+  uint16_t *inv = (uint16_t *)(lst + SW);    // [mr][16] run of (range, suffix xor); 0xFFFF none
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t npref = 1u << (2 * kp);
+  for (int j = threadIdx.x; j < mr * SW; j += NT) inv[j] = 0xFFFFu;
+  for (int r = threadIdx.x; r < mr; r += NT) {
+    uint32_t w = 0;
+    if (r > 0) {
+      int t = r - 1;
+      if (t < 3 * kp) {
+        const int p = t / 3;
+        w = (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
+      } else {
+        t -= 3 * kp;
+        const int pi = t / 9, rr = t - 9 * pi;
+        int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
+        while (q * (q - 1) / 2 > pi) --q;
+        while ((q + 1) * q / 2 <= pi) ++q;
+        const int p = pi - q * (q - 1) / 2;
+        w = ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
+            ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
+      }
+    }
+    pm[r] = w;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nbn; j += NT) {
+    int r, h;
+    uint32_t dm;
+    nb_run_desc<S>(j, k, r, dm, h);
+    rt[j] = (uint32_t)r | (dm << 16) | ((uint32_t)h << 24);
+    inv[r * SW + (int)dm] = (uint16_t)j;
+  }
+  __syncthreads();
+  const int t2 = 1 + 3 * k;
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 16 lists empty (uniform)
+    // ---- 1. the ranges' sub-bin offsets
+    for (int r = threadIdx.x; r < mr; r += NT) {
+      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
+#pragma unroll
+      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
+    }
+    __syncthreads();
+    // ---- 2. run positions of the 16 lists, one wave a list
+    {
+      const int su = wave;
+      const int64_t b = cbase + (int64_t)P * SW + su;
+      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+      if (lane == 0) lst[su] = start;
+      if (tot > 0) {  // wave-uniform
+        const uint2 sg = nbseg[b];
+        uint32_t carry = 0, n0 = 0, pre2 = 0;
+        for (int j0 = 0; j0 < nbn; j0 += 64) {
+          const int j = j0 + lane;
+          uint32_t cnt = 0, h = 2;
+          if (j < nbn) {
+            const uint32_t d = rt[j];
+            const uint32_t *ro = roff + (d & 0xFFFFu) * (SW + 1);
+            const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
+            cnt = ro[sidx + 1] - ro[sidx];
+            h = d >> 24;
+          }
+          const uint32_t inc = nb_wave_incl_scan(cnt);
+          const uint32_t p0 = carry + inc - cnt;
+          if (j0 == 0) {
+            n0 = __shfl(cnt, 0, 64);
+            pre2 = __shfl(p0, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
+          }
+          carry += __shfl(inc, 63, 64);
+          if (j < nbn)
+            pos[su * nbn + j] = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + p0;
+        }
+        const uint32_t total = carry;
+        if (lane < 24) {  // dummy columns after each segment (64 distinct LDS words)
+          const int sgi = lane >> 3, e = lane & 7;
+          const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
+          const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+          const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+          const uint32_t pp = segb + segn + (uint32_t)e;
+          if (pp < segend) table[(size_t)start * 8u + pp] = (uint16_t)(pad_col + (pp & 63u));
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 3. range-major copies, one wave a range
+    for (int r = wave; r < mr; r += NW) {
+      const uint32_t myoff = lane <= SW ? roff[r * (SW + 1) + lane] : 0u;
+      uint32_t so[SW + 1];
+#pragma unroll
+      for (int q = 0; q <= SW; ++q) so[q] = __builtin_amdgcn_readlane(myoff, q);
+      const uint32_t base = so[0], n = so[SW] - base;
+      const int hp = r == 0 ? 0 : r <= 3 * kp ? 1 : 2;
+      for (uint32_t e0 = 0; e0 < n; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        if (e >= n) continue;
+        const uint16_t v = xent[base + e];
+        int sb = 0;
+#pragma unroll
+        for (int q = 1; q < SW; ++q) sb += (base + e >= so[q]) ? 1 : 0;
+        const uint32_t t = base + e - so[sb];
+        const uint16_t *iv = inv + r * SW;
+        if (hp == 2) {  // only the list with suffix sb
+          table[(size_t)lst[sb] * 8u + pos[sb * nbn + iv[0]] + t] = v;
+        } else if (hp == 1) {  // the lists within one suffix letter of sb
+#pragma unroll
+          for (int x = 0; x < 7; ++x) {
+            const int dmx = x == 0 ? 0 : x <= 3 ? x : (x - 3) << 2;
+            const int su = sb ^ dmx;
+            table[(size_t)lst[su] * 8u + pos[su * nbn + iv[dmx]] + t] = v;
+          }
+        } else {  // the group's own prefix: every list
+#pragma unroll
+          for (int dmx = 0; dmx < SW; ++dmx) {
+            const int su = sb ^ dmx;
+            table[(size_t)lst[su] * 8u + pos[su * nbn + iv[dmx]] + t] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();  // the next group overwrites the tables
+  }
+}
+
 // One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
 // triangle for a full square K).
 template <int K>
@@ -590,6 +741,20 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
   const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;  // occurrences of a k-mer
+  if ((form == 0 || form == 6) && g.k >= 4) {
+    // range-major grouped fill (S = 2)
+    const int kp = g.k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+    const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
+    const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * 17 + 16 * (size_t)nbn + 16) +
+                       sizeof(uint16_t) * (size_t)mr * 16;
+    if (lds <= 160 * 1024) {
+      const int64_t ngroups = nbins / 16;
+      const int64_t blocks = std::min<int64_t>(ngroups, 256 * 8);
+      hipLaunchKernelGGL(nb_fill_ranges_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
+                         ngroups, xoff, xent, nboff, nbseg, table, pad_col);
+      return hipGetLastError();
+    }
+  }
   if (form != 1 && g.k >= 4) {
     // grouped fill: S = 2 (16 lists a workgroup of 1024 threads) while the expected LDS
     // image stays <= 48 KB, else S = 1 (4 lists, 256 threads); the image is sized at 2x the
