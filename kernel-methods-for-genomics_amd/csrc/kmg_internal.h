@@ -277,8 +277,9 @@ size_t nb_gram_lds(const IndexGeom &g, const Packed &pk);
 hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
                            uint32_t *nboff, uint32_t *cursor, uint2 *nbseg, uint32_t *partials,
                            hipStream_t s);
-// form: 0 auto (grouped, S = 2, widest stores), 1 per-list fill, 2 grouped S = 1, 3 / 4 / 5
-// grouped S = 2 with 2- / 4- / 8-byte stores
+// form: 0 auto (grouped, S = 2, 2-byte stores), 1 per-list fill, 2 grouped S = 1, 3 / 4 / 5
+// grouped S = 2 with 2- / 4- / 8-byte stores, 6 range-major grouped fill; cap_override:
+// entries of the grouped fill's LDS range image (-1 auto = none)
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
                           hipStream_t s, int form = 0, int cap_override = -1);

@@ -741,7 +741,7 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
   if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
   const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;  // occurrences of a k-mer
-  if ((form == 0 || form == 6) && g.k >= 4) {
+  if (form == 6 && g.k >= 4) {
     // range-major grouped fill (S = 2)
     const int kp = g.k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
     const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
@@ -770,7 +770,10 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     const double e = S == 2 ? e2 : e1;
     int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
     cap = (cap + 7) & ~7;
-    if (cap_override >= 0) cap = std::min(cap, cap_override & ~7);  // (KMG_NB_CAP, tuning)
+    // no LDS range image by default: copying the runs straight from the index (L2 /
+    // Infinity Cache) measured faster than staging them (N=20000 fill 1.49 -> 1.27 ms, rank
+    // slab equal; profiles/r04_nb_fill.jsonl r04o); KMG_NB_CAP > 0 stages up to that many
+    cap = cap_override >= 0 ? std::min(cap, cap_override & ~7) : 0;
     const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
     const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
                        2 * (size_t)cap;
