@@ -109,6 +109,7 @@ struct Tuning {
                             // (kmg_nbhd.hip)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
+  int nb_unroll = 4;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8)
   int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
   int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 grouped S = 1,
                             // 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores
@@ -171,6 +172,7 @@ void read_tuning(Tuning &t) {
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_cap = env_or("KMG_NB_CAP", d.nb_cap);
+  t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -1242,7 +1244,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                           c->nb_lines.as<uint4>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, nbt);
+                                          (int)w[2], oq, c->stream, nbt, c->tune.nb_unroll);
         }, true));
         return mirror();
       }

@@ -286,7 +286,7 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads);
+                                    hipStream_t s, int threads, int unroll = 4);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -39,7 +39,6 @@ namespace kmg {
 
 namespace {
 constexpr int NB_FILL_THREADS = 256;
-constexpr int NB_UNROLL = 4;     // 16-byte pieces in flight per lane in gram_nb_kernel
 
 __device__ __forceinline__ int nb_neighbours(int k) { return 1 + 3 * k + 9 * k * (k - 1) / 2; }
 
@@ -602,7 +601,7 @@ __global__ __launch_bounds__(1024) void nb_fill_ranges_kernel(
 
 // One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
 // triangle for a full square K).
-template <int K>
+template <int K, int NB_UNROLL>
 __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
                                                        const uint32_t *__restrict__ nboff,
                                                        const uint2 *__restrict__ nbseg,
@@ -815,7 +814,7 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads) {
+                                    hipStream_t s, int threads, int unroll) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (g.k < 3 || g.k > 12 || g.copies != 1) return hipErrorNotSupported;
@@ -829,8 +828,12 @@ hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const 
   switch (g.k) {
 #define KMG_NB(KK)                                                                              \
   case KK:                                                                                      \
-    hipLaunchKernelGGL((gram_nb_kernel<KK>), grid, dim3(threads), lds, s, g, pk, nboff, nbseg,  \
-                       table, row0, rows, w0, w1, w2, o);                                       \
+    if (unroll == 8)                                                                            \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 8>), grid, dim3(threads), lds, s, g, pk, nboff,    \
+                         nbseg, table, row0, rows, w0, w1, w2, o);                              \
+    else                                                                                        \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 4>), grid, dim3(threads), lds, s, g, pk, nboff,    \
+                         nbseg, table, row0, rows, w0, w1, w2, o);                              \
     break;
     KMG_NB(3) KMG_NB(4) KMG_NB(5) KMG_NB(6) KMG_NB(7) KMG_NB(8) KMG_NB(9) KMG_NB(10) KMG_NB(11)
     KMG_NB(12)
