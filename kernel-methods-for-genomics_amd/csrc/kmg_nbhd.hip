@@ -427,11 +427,45 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
           pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
         }
         carry += __shfl(inc, 63, 64);
-        uint16_t *o = dst + (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        if (staged)
-          nb_copy_run<WS>(o, ent + srcp, cnt);
-        else
-          nb_copy_run<WS>(o, xent + srcp, cnt);
+        const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+        if constexpr (WS == 0) {
+          // entry-parallel: lane e copies entry e0 + e of the chunk's runs (concatenated in
+          // run order); its run found by a 6-step search over the runs' chunk-relative starts
+          // held one a lane, its source and destination fetched from that run's lane; 64
+          // consecutive entries go to (mostly) 128 contiguous bytes of the list
+          const uint32_t exc = inc - cnt, ctot = __shfl(inc, 63, 64);
+          const uint16_t *sbase = staged ? (const uint16_t *)ent : xent;
+          for (uint32_t e0 = 0; e0 < ctot; e0 += 64 * 2) {
+            uint16_t v[2];
+            uint32_t od[2];
+            bool ok[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const uint32_t e = e0 + 64u * q + (uint32_t)lane;
+              ok[q] = e < ctot;
+              int lo = 0;
+#pragma unroll
+              for (int st = 32; st >= 1; st >>= 1) {
+                const uint32_t x = (uint32_t)__shfl(exc, lo + st, 64);
+                if (x <= e) lo += st;
+              }
+              const uint32_t rx = (uint32_t)__shfl(exc, lo, 64);
+              const uint32_t rs = (uint32_t)__shfl(srcp, lo, 64);
+              const uint32_t rd = (uint32_t)__shfl(dpos, lo, 64);
+              od[q] = rd + (e - rx);
+              if (ok[q]) v[q] = sbase[rs + (e - rx)];
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              if (ok[q]) dst[od[q]] = v[q];
+          }
+        } else {
+          uint16_t *o = dst + dpos;
+          if (staged)
+            nb_copy_run<WS>(o, ent + srcp, cnt);
+          else
+            nb_copy_run<WS>(o, xent + srcp, cnt);
+        }
       }
       const uint32_t total = carry;
       // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
@@ -780,12 +814,13 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
     // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 1: the wider stores measured
     // equal or slower, N=200000 rank slab fill 9.1 -> 15.1 ms, profiles/r04_nb_fill.jsonl r04n)
-    const int ws = form == 4 ? 2 : form == 5 ? 4 : 1;
+    const int ws = form == 4 ? 2 : form == 5 ? 4 : form == 7 ? 0 : 1;
 #define KMG_NBG(S_, NT_, WS_)                                                                  \
   hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, WS_>), dim3((unsigned)blocks), dim3(NT_), \
                      lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
     if (S == 2) {
       if (ws == 1) KMG_NBG(2, 1024, 1);
+      else if (ws == 0) KMG_NBG(2, 1024, 0);
       else if (ws == 2) KMG_NBG(2, 1024, 2);
       else KMG_NBG(2, 1024, 4);
     } else {

@@ -196,7 +196,7 @@ def test_mismatch_k9_n20000(ctx, tune, form):
 
 
 @pytest.mark.parametrize("k", [4, 9, 12])
-@pytest.mark.parametrize("fill", ["1", "2", "3", "5", "6"])
+@pytest.mark.parametrize("fill", ["1", "2", "3", "5", "6", "7"])
 def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
     """The three neighbourhood-list fills (per list; grouped by the 4 / 16 lists sharing a
     prefix, ranges staged in LDS) build the same lists: raw K bit-exact over several column
