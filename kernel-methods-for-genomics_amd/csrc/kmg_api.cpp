@@ -111,8 +111,10 @@ struct Tuning {
                             // (0 auto)
   int nb_unroll = 4;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8)
   int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
-  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto, 1 per list, 2 grouped S = 1,
-                            // 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores
+  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (grouped lane-per-run copies, 9
+                            // past 8.5 occurrences a k-mer and chunk), 1 per list, 2 grouped
+                            // S = 1, 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores,
+                            // 6 range-major, 9 / 10 piece-assembled (whole / half groups)
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
                             // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)

@@ -67,6 +67,20 @@ __device__ __forceinline__ uint32_t nb_neighbour(uint32_t u, int k, int t, int &
   return u ^ ((uint32_t)d1 << (2 * (k - 1 - p))) ^ ((uint32_t)d2 << (2 * (k - 1 - q)));
 }
 
+// the same inclusive wave scan on DPP row shifts and row broadcasts (VALU only, no LDS
+// permutes): Hillis-Steele inside each 16-lane row, then lane 15 into row 1 (and 47 into row
+// 3), then lane 31 into rows 2 and 3
+__device__ __forceinline__ uint32_t nb_wave_incl_scan_dpp(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return (uint32_t)x;
+}
+
 __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -297,6 +311,52 @@ __device__ __forceinline__ void nb_copy_run(uint16_t *o, const Src *src, uint32_
   for (; e < n; ++e) o[e] = src[e];
 }
 
+// pieces of a list the piece fill assembles in LDS (longer lists: lane-per-run copies)
+constexpr int NBP_MAXP = 640;
+
+// LDS word where the piece fill's image starts (16-byte aligned), host and device
+__host__ __device__ inline int nb_pieces_img_word(int k, int nt) {
+  const int kp = k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+  const int nbn = 1 + 3 * k + 9 * k * (k - 1) / 2;
+  const int tw = 2 * (nbn + 1) + NBP_MAXP;
+  return (nbn + mr + mr * 17 + mr + 1 + nt / 64 + (nt / 64 * tw + 1) / 2 + 3) & ~3;
+}
+
+// the grouped fills' per-workgroup tables: rt[j] = run j of a list (prefix range | suffix xor
+// << 16 | Hamming class << 24, segment order) and pm[r] = the prefix xor of range r
+template <int S>
+__device__ void nb_group_tables(int k, int nt, uint32_t *rt, uint32_t *pm) {
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+  const int nbn = nb_neighbours(k);
+  for (int j = threadIdx.x; j < nbn; j += nt) {
+    int r, h;
+    uint32_t dm;
+    nb_run_desc<S>(j, k, r, dm, h);
+    rt[j] = (uint32_t)r | (dm << 16) | ((uint32_t)h << 24);
+  }
+  for (int r = threadIdx.x; r < mr; r += nt) {
+    uint32_t w = 0;
+    if (r > 0) {
+      int t = r - 1;
+      if (t < 3 * kp) {
+        const int p = t / 3;
+        w = (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
+      } else {
+        t -= 3 * kp;
+        const int pi = t / 9, rr = t - 9 * pi;
+        int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
+        while (q * (q - 1) / 2 > pi) --q;
+        while ((q + 1) * q / 2 <= pi) ++q;
+        const int p = pi - q * (q - 1) / 2;
+        w = ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
+            ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
+      }
+    }
+    pm[r] = w;
+  }
+}
+
 template <int S, int NT, int WS>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
@@ -317,32 +377,7 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t npref = 1u << (2 * kp);
   // the run and range tables, once per workgroup (the grid is persistent)
-  for (int j = threadIdx.x; j < nbn; j += NT) {
-    int r, h;
-    uint32_t dm;
-    nb_run_desc<S>(j, k, r, dm, h);
-    rt[j] = (uint32_t)r | (dm << 16) | ((uint32_t)h << 24);
-  }
-  for (int r = threadIdx.x; r < mr; r += NT) {
-    uint32_t w = 0;
-    if (r > 0) {
-      int t = r - 1;
-      if (t < 3 * kp) {
-        const int p = t / 3;
-        w = (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
-      } else {
-        t -= 3 * kp;
-        const int pi = t / 9, rr = t - 9 * pi;
-        int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
-        while (q * (q - 1) / 2 > pi) --q;
-        while ((q + 1) * q / 2 <= pi) ++q;
-        const int p = pi - q * (q - 1) / 2;
-        w = ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
-            ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
-      }
-    }
-    pm[r] = w;
-  }
+  nb_group_tables<S>(k, NT, rt, pm);
   __syncthreads();
   const int rpt = (mr + NT - 1) / NT;
   const int t2 = 1 + 3 * k;
@@ -428,38 +463,7 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
         }
         carry += __shfl(inc, 63, 64);
         const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        if constexpr (WS == 0) {
-          // entry-parallel: lane e copies entry e0 + e of the chunk's runs (concatenated in
-          // run order); its run found by a 6-step search over the runs' chunk-relative starts
-          // held one a lane, its source and destination fetched from that run's lane; 64
-          // consecutive entries go to (mostly) 128 contiguous bytes of the list
-          const uint32_t exc = inc - cnt, ctot = __shfl(inc, 63, 64);
-          const uint16_t *sbase = staged ? (const uint16_t *)ent : xent;
-          for (uint32_t e0 = 0; e0 < ctot; e0 += 64 * 2) {
-            uint16_t v[2];
-            uint32_t od[2];
-            bool ok[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const uint32_t e = e0 + 64u * q + (uint32_t)lane;
-              ok[q] = e < ctot;
-              int lo = 0;
-#pragma unroll
-              for (int st = 32; st >= 1; st >>= 1) {
-                const uint32_t x = (uint32_t)__shfl(exc, lo + st, 64);
-                if (x <= e) lo += st;
-              }
-              const uint32_t rx = (uint32_t)__shfl(exc, lo, 64);
-              const uint32_t rs = (uint32_t)__shfl(srcp, lo, 64);
-              const uint32_t rd = (uint32_t)__shfl(dpos, lo, 64);
-              od[q] = rd + (e - rx);
-              if (ok[q]) v[q] = sbase[rs + (e - rx)];
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-              if (ok[q]) dst[od[q]] = v[q];
-          }
-        } else {
+        {
           uint16_t *o = dst + dpos;
           if (staged)
             nb_copy_run<WS>(o, ent + srcp, cnt);
@@ -479,6 +483,212 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       }
     }
     __syncthreads();  // the next group overwrites the LDS image
+  }
+}
+
+// ------------------------------------------------------------------ piece-assembled fill
+// The lane-per-run copies above are bound by the texture-address unit, not by bytes: their
+// 2-byte loads and stores cost ~25 TA cycles a wave instruction whatever the lane count, and
+// a 16-list group issues ~2800 of them (PMC, profiles/r04t_pmc_fill.txt: TA busy 67 % of the
+// kernel).  This form moves whole 16-byte pieces through the TA both ways:
+//  1. the group's 211 prefix ranges (S = 2) into an LDS image with 16-byte loads, each range
+//     at its source alignment mod 8 entries (~220 load instructions a group);
+//  2. one wave a list: the 352 runs in segment order -> a wave prefix sum -> a table of the
+//     non-empty runs (compacted by a ballot): destination end and (image offset - destination
+//     start) as uint16, and for every 16-byte piece of the list the first run that reaches it;
+//  3. lane p assembles list piece p from the image (8 LDS reads, the segment's dummy columns
+//     in its padding) and writes it with one 16-byte store: a wave writes 1 KB of the list
+//     per store instruction (~5 a list instead of ~90).
+// Groups whose image exceeds the LDS, and lists of more than NBP_MAXP pieces, take the
+// lane-per-run copy from the index.
+template <int NL>
+__global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
+    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
+    uint32_t pad_col, int cap) {
+  constexpr int S = 2, SW = 16, NT = NL * 64, NW = NL, NH = SW / NL;
+  extern __shared__ __align__(16) uint32_t fsm[];
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  const int nbn = nb_neighbours(k);
+  const int tw = 2 * (nbn + 1) + NBP_MAXP;           // uint16 table words a wave
+  uint32_t *rt = fsm;                                 // [nbn] runs of a list
+  uint32_t *pm = rt + nbn;                            // [mr] prefix xor of range r
+  uint32_t *roff = pm + mr;                           // [mr][SW + 1] absolute index offsets
+  uint32_t *rbase = roff + mr * (SW + 1);             // [mr + 1] image position of each range
+  uint32_t *wtot = rbase + mr + 1;                    // [NW] scan scratch
+  uint16_t *tabs = (uint16_t *)(wtot + NW);           // [NW][tw] re, rsd, pst
+  uint16_t *img = (uint16_t *)(fsm + nb_pieces_img_word(k, NT));  // [cap], 16-byte aligned
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t npref = 1u << (2 * kp);
+  nb_group_tables<S>(k, NT, rt, pm);
+  __syncthreads();
+  const int rpt = (mr + NT - 1) / NT;
+  const int t2 = 1 + 3 * k;
+  const int nfull = 1 + 3 * kp;  // ranges whose every sub-bin a half group takes
+  const uint64_t ltmask = (1ull << lane) - 1ull;
+  uint16_t *re = tabs + wave * tw;   // [nbn + 1] destination end of non-empty run idx
+  uint16_t *rsd = re + nbn + 1;      // [nbn + 1] image offset - destination start
+  uint16_t *pst = rsd + nbn + 1;     // [NBP_MAXP] first run reaching piece p
+  for (int64_t bi = blockIdx.x; bi < ngroups * NH; bi += gridDim.x) {
+    const int64_t gi = bi / NH;
+    const int hh = (int)(bi - gi * NH);  // which NL of the group's 16 lists (suffixes)
+    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    const int64_t cbase = (gi - P) * SW;
+    if (nboff[gi * SW + hh * NL + NL] == nboff[gi * SW + hh * NL]) continue;  // uniform
+    // sub-bins [slo, shi) of range r the block's lists take: all 16 of the own prefix and the
+    // Hamming-1 prefixes (suffix Hamming <= 1 reaches every first letter), only the block's
+    // own suffixes [hh NL, hh NL + NL) of the Hamming-2 prefixes
+    auto slo = [&](int r) { return r < nfull ? 0 : hh * NL; };
+    auto shi = [&](int r) { return r < nfull ? SW : hh * NL + NL; };
+    // ---- 1. ranges: offsets, image positions (n + 14 words each: 8-aligned + source phase)
+    uint32_t myn = 0;
+    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
+      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
+#pragma unroll
+      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
+      myn += o[shi(r)] - o[slo(r)] + 14u;
+    }
+    {
+      const uint32_t inc = nb_wave_incl_scan_dpp(myn);
+      if (lane == 63) wtot[wave] = inc;
+      __syncthreads();
+      uint32_t base = 0, total = 0;
+      for (int w2 = 0; w2 < NW; ++w2) {
+        base += w2 < wave ? wtot[w2] : 0u;
+        total += wtot[w2];
+      }
+      uint32_t run = base + inc - myn;
+      for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
+        const uint32_t a = roff[r * (SW + 1) + slo(r)];
+        rbase[r] = ((run + 7u) & ~7u) + (a & 7u);
+        run += roff[r * (SW + 1) + shi(r)] - a + 14u;
+      }
+      if (threadIdx.x == 0) rbase[mr] = total;
+      __syncthreads();
+    }
+    const bool staged = rbase[mr] <= (uint32_t)cap;
+    // ---- 2. the image: whole 16-byte pieces of each range, one wave a range
+    if (staged) {
+      for (int r = wave; r < mr; r += NW) {
+        const uint32_t a = roff[r * (SW + 1) + slo(r)], n = roff[r * (SW + 1) + shi(r)] - a;
+        if (n == 0) continue;
+        const uint32_t fp = a >> 3, lp = (a + n + 7u) >> 3;
+        uint16_t *d0 = img + (rbase[r] - (a & 7u));
+        for (uint32_t pc = fp + (uint32_t)lane; pc < lp; pc += 64u)
+          *(uint4 *)(d0 + 8u * (pc - fp)) = ((const uint4 *)xent)[pc];
+      }
+    }
+    __syncthreads();
+    // ---- 3. the block's NL lists, one wave a list
+    for (int su = hh * NL + wave; su < hh * NL + NL; su += NW) {
+      const int64_t b = cbase + (int64_t)P * SW + su;
+      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+      if (tot == 0) continue;  // wave-uniform
+      const uint2 sg = nbseg[b];
+      uint16_t *dst = table + (size_t)start * 8u;
+      const bool pieces = staged && tot <= (uint32_t)NBP_MAXP;  // wave-uniform
+      uint32_t carry = 0, n0 = 0, pre2 = 0, nzc = 0;
+      for (int j0 = 0; j0 < nbn; j0 += 64) {
+        const int j = j0 + lane;
+        uint32_t cnt = 0, a0 = 0, si = 0, h = 2;
+        if (j < nbn) {
+          const uint32_t d = rt[j];
+          const uint32_t r = d & 0xFFFFu;
+          h = d >> 24;
+          const uint32_t *ro = roff + r * (SW + 1);
+          const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
+          a0 = ro[sidx];
+          cnt = ro[sidx + 1] - a0;
+          si = rbase[r] + (a0 - ro[slo((int)r)]);
+        }
+        const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
+        const uint32_t pos = carry + inc - cnt;
+        if (j0 == 0) {
+          n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
+          pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);  // (t2 < 64 for k <= 21)
+        }
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+        if (pieces) {
+          const uint64_t bal = __ballot(cnt != 0u);
+          const uint32_t idx = nzc + (uint32_t)__popcll(bal & ltmask);
+          if (cnt) {
+            re[idx] = (uint16_t)(dpos + cnt);
+            rsd[idx] = (uint16_t)(si - dpos);
+          }
+          nzc += (uint32_t)__popcll(bal);
+        } else {
+          nb_copy_run<1>(dst + dpos, xent + a0, cnt);
+        }
+      }
+      const uint32_t total = carry;
+      if (pieces) {
+        if (lane == 0) {
+          re[nzc] = (uint16_t)(tot * 8u);  // sentinel: past every entry
+          rsd[nzc] = 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (uint32_t idx = (uint32_t)lane; idx <= nzc; idx += 64u) {
+          const uint32_t lo = idx ? re[idx - 1] : 0u, hi = re[idx];
+          for (uint32_t p = (lo + 7u) >> 3; p < ((hi + 7u) >> 3); ++p) pst[p] = (uint16_t)idx;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // dummy columns: [n0, sx), [e1, sy), [e2, tot * 8)
+        const uint32_t sx = sg.x * 8u, sy = sg.y * 8u;
+        const uint32_t e1 = sx + (pre2 - n0), e2 = sy + (total - pre2);
+        for (uint32_t p = (uint32_t)lane; p < tot; p += 64u) {
+          const uint32_t d0 = 8u * p;
+          uint32_t jr = pst[p];
+          uint32_t rej = re[jr], sdj = rsd[jr];
+          uint32_t w[4];
+          if ((d0 + 8u > n0 && d0 < sx) || (d0 + 8u > e1 && d0 < sy) || d0 + 8u > e2) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const uint32_t d = d0 + (uint32_t)q;
+              if (d >= rej) {
+                ++jr;
+                rej = re[jr];
+                sdj = rsd[jr];
+              }
+              uint32_t v;
+              if ((d >= n0 && d < sx) || (d >= e1 && d < sy) || d >= e2)
+                v = (pad_col + (d & 63u)) & 0xFFFFu;
+              else
+                v = img[(sdj + d) & 0xFFFFu];
+              if (q & 1) w[q >> 1] |= v << 16;
+              else w[q >> 1] = v;
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const uint32_t d = d0 + (uint32_t)q;
+              if (d >= rej) {  // runs are non-empty and contiguous here: one step
+                ++jr;
+                rej = re[jr];
+                sdj = rsd[jr];
+              }
+              const uint32_t v = img[(sdj + d) & 0xFFFFu];
+              if (q & 1) w[q >> 1] |= v << 16;
+              else w[q >> 1] = v;
+            }
+          }
+          *(uint4 *)(dst + d0) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        __builtin_amdgcn_wave_barrier();  // the next list overwrites the tables
+      } else if (lane < 24) {
+        // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+        const int sgi = lane >> 3, e = lane & 7;
+        const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
+        const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+        const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+        const uint32_t pp = segb + segn + (uint32_t)e;
+        if (pp < segend) dst[pp] = (uint16_t)(pad_col + (pp & 63u));
+      }
+    }
+    __syncthreads();  // the next group overwrites the image
   }
 }
 
@@ -788,6 +998,35 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
       return hipGetLastError();
     }
   }
+  // auto: the piece-assembled fill where a list's runs are long enough for its fixed cost per
+  // group (~7 us of range offsets + image loads) to pay: N=200000 rank slab (7 chunks of
+  // 28572 columns, 10.1 occurrences a k-mer and chunk) fill 9.1 -> 7.0 ms; at N=20000 (7.1)
+  // the lane-per-run copies stay ahead, 1.25 vs 1.30 ms (profiles/r04_nb_fill.jsonl r04z)
+  if (form == 0 && mean >= 8.5) form = 9;
+  if ((form == 9 || form == 10) && g.k >= 4 && (((uintptr_t)xent) & 15u) == 0) {
+    // piece-assembled grouped fill (S = 2): 16 lists a 1024-thread workgroup (form 9) or 8
+    // lists a 512-thread one (form 10: half the LDS image, two workgroups a CU, measured
+    // slower: each half group reloads the 211 ranges' offsets); the LDS left after the
+    // tables is the image
+    const int nl = form == 9 ? 16 : 8, nt = nl * 64;
+    const int bpc = form == 9 ? 1 : 2;  // workgroups a CU the LDS is split for
+    const size_t fixed = 4 * (size_t)nb_pieces_img_word(g.k, nt);
+    const size_t avail = (size_t)160 * 1024 / bpc;
+    int cap = fixed < avail ? (int)std::min<size_t>((avail - fixed) / 2, 65528) & ~7 : 0;
+    if (cap_override >= 0) cap = std::min(cap, cap_override & ~7);
+    if (cap >= 1024) {
+      const size_t lds = fixed + 2 * (size_t)cap;
+      const int64_t ngroups = nbins / 16;
+      const int64_t blocks = std::min<int64_t>(ngroups * (16 / nl), 256 * bpc);
+      if (nl == 16)
+        hipLaunchKernelGGL(nb_fill_pieces_kernel<16>, dim3((unsigned)blocks), dim3(nt), lds, s, g.k,
+                           ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+      else
+        hipLaunchKernelGGL(nb_fill_pieces_kernel<8>, dim3((unsigned)blocks), dim3(nt), lds, s, g.k,
+                           ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
+      return hipGetLastError();
+    }
+  }
   if (form != 1 && g.k >= 4) {
     // grouped fill: S = 2 (16 lists a workgroup of 1024 threads) while the expected LDS
     // image stays <= 48 KB, else S = 1 (4 lists, 256 threads); the image is sized at 2x the
@@ -808,19 +1047,18 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     // slab equal; profiles/r04_nb_fill.jsonl r04o); KMG_NB_CAP > 0 stages up to that many
     cap = cap_override >= 0 ? std::min(cap, cap_override & ~7) : 0;
     const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
+    const int ws = form == 4 ? 2 : form == 5 ? 4 : 1;
     const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
                        2 * (size_t)cap;
     const int64_t ngroups = nbins / SW;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
     // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 1: the wider stores measured
     // equal or slower, N=200000 rank slab fill 9.1 -> 15.1 ms, profiles/r04_nb_fill.jsonl r04n)
-    const int ws = form == 4 ? 2 : form == 5 ? 4 : form == 7 ? 0 : 1;
 #define KMG_NBG(S_, NT_, WS_)                                                                  \
   hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, WS_>), dim3((unsigned)blocks), dim3(NT_), \
                      lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
     if (S == 2) {
       if (ws == 1) KMG_NBG(2, 1024, 1);
-      else if (ws == 0) KMG_NBG(2, 1024, 0);
       else if (ws == 2) KMG_NBG(2, 1024, 2);
       else KMG_NBG(2, 1024, 4);
     } else {

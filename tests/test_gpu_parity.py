@@ -196,7 +196,7 @@ def test_mismatch_k9_n20000(ctx, tune, form):
 
 
 @pytest.mark.parametrize("k", [4, 9, 12])
-@pytest.mark.parametrize("fill", ["1", "2", "3", "5", "6", "7"])
+@pytest.mark.parametrize("fill", ["1", "2", "3", "5", "6", "9", "10"])
 def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
     """The three neighbourhood-list fills (per list; grouped by the 4 / 16 lists sharing a
     prefix, ranges staged in LDS) build the same lists: raw K bit-exact over several column
@@ -208,6 +208,22 @@ def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
     for chunk in (("96", "20480") if k < 12 else ("20480",)):  # (k = 12: 4^12 bins a chunk)
         tune(KMG_MM_CHUNK=chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                       L.KMG_I32)
+        assert np.array_equal(raw.astype(np.int64), ref), chunk
+
+
+@pytest.mark.parametrize("cap", ["-1", "4096"])
+def test_mismatch_nb_piece_fill_fallbacks(ctx, tune, cap):
+    """The piece-assembled fill's two fallbacks: lists longer than its piece table (80 poly-A
+    rows: the A^9 list holds 7440 entries, 930 pieces) and groups whose range image overflows
+    the LDS (cap 4096: the poly-A groups) take the lane-per-run copies; raw K bit-exact."""
+    codes, lens = E.synthetic(600, 101, seed=97)
+    codes[:80] = 0
+    ref = cref.mismatch_raw(codes, lens, 9, 1)
+    tune(KMG_MM_FORM=4, KMG_NB_FILL="9", KMG_NB_CAP=cap)
+    for chunk in ("96", "20480"):
+        tune(KMG_MM_CHUNK=chunk)
+        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
                        L.KMG_I32)
         assert np.array_equal(raw.astype(np.int64), ref), chunk
 
