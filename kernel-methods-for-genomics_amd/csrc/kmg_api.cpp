@@ -110,6 +110,7 @@ struct Tuning {
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
   int nb_unroll = 4;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8)
+  int nb_acc16 = 0;         // KMG_NB_ACC16: NB Gram with 16-bit LDS counters (K_ii K_jj bound)
   int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
   int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (grouped lane-per-run copies, 9
                             // past 8.5 occurrences a k-mer and chunk), 1 per list, 2 grouped
@@ -175,6 +176,7 @@ void read_tuning(Tuning &t) {
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_cap = env_or("KMG_NB_CAP", d.nb_cap);
   t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
+  t.nb_acc16 = env_or("KMG_NB_ACC16", d.nb_acc16);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -209,6 +211,7 @@ struct kmg_ctx {
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   DevBuf pr_big;                  // pair lines: blocks with groups past the small image
   DevBuf nb_seg, nb_lines;        // neighbourhood lists: segment ends, the lists
+  DevBuf nb_dmax;                 // per column chunk, the largest raw K_jj (16-bit counters)
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -617,9 +620,10 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
 // reads (nch + 1) / (2 nch) of them and writes as much of its K row, and the mirror moves
 // 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
 // mirror; the largest chunk is the int32 LDS accumulator beside the row tables.
-int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads) {
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool a16) {
   const int64_t lds_words = (threads == 512 ? 80 : 160) * 1024 / 4;
-  int64_t max_chunk = (lds_words - 64 - 4 * (int64_t)pmax - 1 - ldp - 8) & ~7LL;
+  // (16-bit counters: two columns a word)
+  int64_t max_chunk = ((lds_words - 64 - 4 * (int64_t)pmax - 1 - ldp - 8) * (a16 ? 2 : 1)) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
   if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
   if (max_chunk < 8) return 8;
@@ -1207,7 +1211,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
         const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
-        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt));
+        const bool a16 = c->tune.nb_acc16 != 0;
+        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, a16));
         o.tri = tri_esz > 0 && g.nchunks > 1;
         note_plan(nbt);
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
@@ -1234,7 +1239,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                  c->nb_lines.as<uint16_t>(), c->stream, c->tune.nb_fill,
                                  c->tune.nb_cap));
         }
-        if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
+        if (p->normalize || dt == KMG_U8 || a16) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));
           KMG_TRY(diag_hamming(c, g, pkd));
           if (p->normalize) {
@@ -1243,10 +1248,17 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             o.dsq = c->dsq.as<double>();
           }
         }
+        if (a16) {
+          KMG_TRY(c->nb_dmax.ensure(sizeof(double) * (size_t)g.nchunks));
+          KMG_HIP(launch_chunk_dmax(c->diagv.as<double>(), n, g.chunk, g.nchunks,
+                                    c->nb_dmax.as<double>(), c->stream));
+        }
         KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                           c->nb_lines.as<uint4>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, nbt, c->tune.nb_unroll);
+                                          (int)w[2], oq, c->stream, nbt, c->tune.nb_unroll,
+                                          a16 ? c->diagv.as<double>() : nullptr,
+                                          a16 ? c->nb_dmax.as<double>() : nullptr);
         }, true));
         return mirror();
       }

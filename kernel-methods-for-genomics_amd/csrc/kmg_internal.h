@@ -273,7 +273,9 @@ hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, cons
 // Hamming distance 0 | 1 | 2 (uint16 columns, 3 segments padded to 8); hist / nboff / cursor
 // nbins + 1 words, nbseg nbins, table nb_list_entries_bound(...) uint16
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins);
-size_t nb_gram_lds(const IndexGeom &g, const Packed &pk);
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk, bool a16);
+hipError_t launch_chunk_dmax(const double *kdiag, int64_t n, int chunk, int nchunks, double *dmax,
+                             hipStream_t s);
 hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
                            uint32_t *nboff, uint32_t *cursor, uint2 *nbseg, uint32_t *partials,
                            hipStream_t s);
@@ -286,7 +288,8 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads, int unroll = 4);
+                                    hipStream_t s, int threads, int unroll = 4,
+                                    const double *kdiag = nullptr, const double *kdmax = nullptr);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);

@@ -845,13 +845,20 @@ __global__ __launch_bounds__(1024) void nb_fill_ranges_kernel(
 
 // One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
 // triangle for a full square K).
-template <int K, int NB_UNROLL>
+// A16: 16-bit column counters, two a dword (the LDS of a chunk halves: two workgroups a CU
+// at N=200000's 28572-column chunks instead of one).  Exact while no count reaches 2^16:
+// K is a Gram matrix (K_ij = <phi(x_i), phi(x_j)>), so K_ij^2 <= K_ii K_jj, and a (row,
+// chunk) whose K_ii x max_{j in chunk} K_jj < 2^32 cannot overflow; any other takes two
+// passes over its list with 32-bit counters for half the chunk's columns each.
+template <int K, int NB_UNROLL, bool A16>
 __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
                                                        const uint32_t *__restrict__ nboff,
                                                        const uint2 *__restrict__ nbseg,
                                                        const uint4 *__restrict__ table,
                                                        int64_t row0, int64_t rows, int w0, int w1,
-                                                       int w2, OutSpec o) {
+                                                       int w2, OutSpec o,
+                                                       const double *__restrict__ kdiag,
+                                                       const double *__restrict__ kdmax) {
   extern __shared__ __align__(16) uint32_t smem[];
   int c;
   int64_t il;
@@ -861,16 +868,14 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int accw = ((g.chunk + 3) >> 2) << 2;
+  const int accn = A16 ? (((accw >> 1) + 32 + 3) & ~3) : accw + 64;  // counter words (+ dummies)
   const int P = g.pmax;
-  int32_t *acc = (int32_t *)smem;     // [accw] + 64 dummy words (list padding)
-  uint32_t *wst = smem + accw + 64;   // [P] list start of window a (pieces)
+  uint32_t *wst = smem + accn;        // [P] list start of window a (pieces)
   uint32_t *wcum = wst + P;           // [P + 1] pieces of windows < a
   uint32_t *ws0 = wcum + P + 1;       // [P] end of segment 0 (pieces, list-relative)
   uint32_t *ws1 = ws0 + P;            // [P] end of segment 1
   uint32_t *srec = ws1 + P;           // packed row record
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  uint4 *acc4 = (uint4 *)acc;
-  for (int w = threadIdx.x; w < (accw >> 2) + 16; w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
   stage_record(pk, i, srec);
   __syncthreads();
   const uint32_t cbase = (uint32_t)c << (2 * K);
@@ -902,58 +907,116 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
     }
     if (lane == 0) wcum[0] = 0;
   }
-  __syncthreads();
-  // this wave's share of the row's pieces; lane l takes pieces qb + l, qb + l + 64, ...
-  const uint32_t T = wcum[P];
-  const uint32_t qb = (uint32_t)(((uint64_t)T * wave) / nw), qe = (uint32_t)(((uint64_t)T * (wave + 1)) / nw);
-  uint32_t q = qb + lane;
-  int a = 0;  // window of piece q: the last a with wcum[a] <= q
-  {
-    int lo = 0, hi = P - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (wcum[mid] <= q) lo = mid;
-      else hi = mid - 1;
-    }
-    a = lo;
-  }
-  uint32_t abeg = wcum[a], aend = wcum[a + 1], ast = wst[a], as0 = ws0[a], as1 = ws1[a];
-  for (; q < qe; q += 64 * NB_UNROLL) {
-    uint4 v[NB_UNROLL];
-    int wt[NB_UNROLL];
-#pragma unroll
-    for (int t = 0; t < NB_UNROLL; ++t) {
-      const uint32_t qq = q + 64u * t;
-      wt[t] = 0;
-      if (qq < qe) {
-        while (qq >= aend) {
-          ++a;
-          abeg = aend;
-          aend = wcum[a + 1];
-          ast = wst[a];
-          as0 = ws0[a];
-          as1 = ws1[a];
-        }
-        const uint32_t rel = qq - abeg;
-        v[t] = table[(uint64_t)ast + rel];
-        wt[t] = rel < as0 ? w0 : rel < as1 ? w1 : w2;
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < NB_UNROLL; ++t) {
-      if (wt[t]) {
-        const uint32_t x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          atomicAdd(&acc[x[h] & 0xFFFFu], wt[t]);
-          atomicAdd(&acc[x[h] >> 16], wt[t]);
-        }
-      }
-    }
-  }
-  __syncthreads();
+  // 16-bit counters for this (row, chunk), or two 32-bit passes over column halves
+  const bool c16 = A16 && kdiag[i] * kdmax[c] < 4294967296.0;
+  const int npass = (!A16 || c16) ? 1 : 2;
+  const uint32_t half = (uint32_t)((((cw + 1) >> 1) + 7) & ~7);  // pass 1's first column
   const bool norm = o.normalize && o.diagv[0] != 1.0;
-  emit_row<true>(o, il, i, col0, cw, (const int32_t *)acc, norm);
+  for (int pass = 0; pass < npass; ++pass) {
+    // pass columns [plo, plo + pcw) (relative to col0); 32-bit counters at acc[x - plo]
+    const uint32_t plo = npass == 1 ? 0u : pass * half;
+    const uint32_t pcw = npass == 1 ? (uint32_t)cw : pass ? (uint32_t)cw - half : half;
+    {
+      uint4 *acc4 = (uint4 *)smem;
+      for (int w = threadIdx.x; w < (accn >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    // this wave's share of the row's pieces; lane l takes pieces qb + l, qb + l + 64, ...
+    const uint32_t T = wcum[P];
+    const uint32_t qb = (uint32_t)(((uint64_t)T * wave) / nw), qe = (uint32_t)(((uint64_t)T * (wave + 1)) / nw);
+    uint32_t q = qb + lane;
+    int a = 0;  // window of piece q: the last a with wcum[a] <= q
+    {
+      int lo = 0, hi = P - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (wcum[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      a = lo;
+    }
+    uint32_t abeg = wcum[a], aend = wcum[a + 1], ast = wst[a], as0 = ws0[a], as1 = ws1[a];
+    for (; q < qe; q += 64 * NB_UNROLL) {
+      uint4 v[NB_UNROLL];
+      int wt[NB_UNROLL];
+#pragma unroll
+      for (int t = 0; t < NB_UNROLL; ++t) {
+        const uint32_t qq = q + 64u * t;
+        wt[t] = 0;
+        if (qq < qe) {
+          while (qq >= aend) {
+            ++a;
+            abeg = aend;
+            aend = wcum[a + 1];
+            ast = wst[a];
+            as0 = ws0[a];
+            as1 = ws1[a];
+          }
+          const uint32_t rel = qq - abeg;
+          v[t] = table[(uint64_t)ast + rel];
+          wt[t] = rel < as0 ? w0 : rel < as1 ? w1 : w2;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NB_UNROLL; ++t) {
+        if (wt[t]) {
+          const uint32_t x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+          if (!A16) {
+            int32_t *acc = (int32_t *)smem;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              atomicAdd(&acc[x[h] & 0xFFFFu], wt[t]);
+              atomicAdd(&acc[x[h] >> 16], wt[t]);
+            }
+          } else if (c16) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const uint32_t xl = x[h] & 0xFFFFu, xh = x[h] >> 16;
+              atomicAdd(&smem[xl >> 1], (uint32_t)wt[t] << ((xl & 1u) << 4));
+              atomicAdd(&smem[xh >> 1], (uint32_t)wt[t] << ((xh & 1u) << 4));
+            }
+          } else {  // 32-bit counters of this pass's columns (dummies >= accw never land)
+            int32_t *acc = (int32_t *)smem;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const uint32_t xl = (x[h] & 0xFFFFu) - plo, xh = (x[h] >> 16) - plo;
+              if (xl < pcw) atomicAdd(&acc[xl], wt[t]);
+              if (xh < pcw) atomicAdd(&acc[xh], wt[t]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (c16)
+      emit_row<true, true>(o, il, i, col0, cw, (const int32_t *)smem, norm);
+    else
+      emit_row<true>(o, il, i, col0 + plo, (int)pcw, (const int32_t *)smem, norm);
+    if (pass + 1 < npass) __syncthreads();
+  }
+}
+
+// per column chunk, the largest raw diagonal K_jj of its columns (the 16-bit counters' bound)
+__global__ __launch_bounds__(256) void chunk_dmax_kernel(const double *__restrict__ kdiag, int64_t n,
+                                                         int chunk, double *__restrict__ dmax) {
+  __shared__ double red[256];
+  const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = min(n, c0 + chunk);
+  double m = 0.0;
+  for (int64_t j = c0 + threadIdx.x; j < c1; j += 256) m = fmax(m, kdiag[j]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dmax[blockIdx.x] = red[0];
+}
+
+hipError_t launch_chunk_dmax(const double *kdiag, int64_t n, int chunk, int nchunks, double *dmax,
+                             hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(chunk_dmax_kernel, dim3((unsigned)nchunks), dim3(256), 0, s, kdiag, n, chunk, dmax);
+  return hipGetLastError();
 }
 
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
@@ -963,8 +1026,9 @@ int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
   return e + 21 * std::min(nbins, e);
 }
 
-size_t nb_gram_lds(const IndexGeom &g, const Packed &pk) {
-  return (size_t)((((g.chunk + 3) >> 2) << 2) + 64 + 4 * g.pmax + 1 + pk.ldp) * 4;
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk, bool a16) {
+  const int accw = ((g.chunk + 3) >> 2) << 2;
+  return (size_t)((a16 ? (((accw >> 1) + 32 + 3) & ~3) : accw + 64) + 4 * g.pmax + 1 + pk.ldp) * 4;
 }
 
 hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
@@ -1087,26 +1151,31 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint4 *table, int64_t row0,
                                     int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads, int unroll) {
+                                    hipStream_t s, int threads, int unroll, const double *kdiag,
+                                    const double *kdmax) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (g.k < 3 || g.k > 12 || g.copies != 1) return hipErrorNotSupported;
   if (threads != 512 && threads != 1024) return hipErrorInvalidValue;
+  const bool a16 = kdiag != nullptr && kdmax != nullptr;
   const int64_t nblk = rowacc_blocks(g, o, row0, rows);
   if (nblk * threads >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   if (g.chunk + 64 + 63 >= 65536) return hipErrorInvalidValue;      // uint16 columns + dummies
-  const size_t lds = nb_gram_lds(g, pk);
+  const size_t lds = nb_gram_lds(g, pk, a16);
   if (lds > (threads == 512 ? 80 : 160) * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk);
   switch (g.k) {
 #define KMG_NB(KK)                                                                              \
   case KK:                                                                                      \
-    if (unroll == 8)                                                                            \
-      hipLaunchKernelGGL((gram_nb_kernel<KK, 8>), grid, dim3(threads), lds, s, g, pk, nboff,    \
-                         nbseg, table, row0, rows, w0, w1, w2, o);                              \
+    if (a16)                                                                                    \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 4, true>), grid, dim3(threads), lds, s, g, pk,     \
+                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
+    else if (unroll == 8)                                                                       \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 8, false>), grid, dim3(threads), lds, s, g, pk,    \
+                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
     else                                                                                        \
-      hipLaunchKernelGGL((gram_nb_kernel<KK, 4>), grid, dim3(threads), lds, s, g, pk, nboff,    \
-                         nbseg, table, row0, rows, w0, w1, w2, o);                              \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 4, false>), grid, dim3(threads), lds, s, g, pk,    \
+                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
     break;
     KMG_NB(3) KMG_NB(4) KMG_NB(5) KMG_NB(6) KMG_NB(7) KMG_NB(8) KMG_NB(9) KMG_NB(10) KMG_NB(11)
     KMG_NB(12)

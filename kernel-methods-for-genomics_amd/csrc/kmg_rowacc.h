@@ -114,9 +114,11 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
 // (int32 / float32: 4 columns a lane, float64: 2).  Two 16-byte stores 32 bytes apart per
 // lane (emit4's float64 form) leave half-written lines behind every store instruction,
 // which cost the spectrum kernel 2.2x as non-temporal stores (profiles/r02t_sp_store.jsonl).
-template <bool NT>
+// A16: the counters are packed 16-bit (column q at halfword q of the accumulator)
+template <bool NT, bool A16 = false>
 __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i, int64_t col0,
                                          int cw, const int32_t *acc, bool norm) {
+  const uint16_t *a16 = (const uint16_t *)acc;
   // columns below o.col_lo are not written; col_lo - col0 is a multiple of 8 (host check)
   const int qs = (int)max((int64_t)0, o.col_lo - col0);
   if (o.dtype == KMG_U8) {
@@ -130,7 +132,7 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
       uint32_t v[16];
 #pragma unroll
       for (int h = 0; h < 16; ++h) {
-        const uint32_t x = q + h < cw ? (uint32_t)acc[q + h] : 0u;
+        const uint32_t x = q + h < cw ? (A16 ? (uint32_t)a16[q + h] : (uint32_t)acc[q + h]) : 0u;
         const bool dg = col0 + q + h == i;
         v[h] = (dg || q + h >= cw) ? 0u : u8_slab_entry(o, i, col0 + q + h, x, big);
       }
@@ -158,12 +160,18 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
     for (int q = qs + threadIdx.x * 8; q < cw; q += blockDim.x * 8) {
       uint32_t v[8];
       if (q + 8 <= cw) {
-        const uint4 a = *(const uint4 *)&acc[q], b = *(const uint4 *)&acc[q + 4];
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if constexpr (A16) {
+          const uint4 a = *(const uint4 *)&a16[q];
+          v[0] = a.x & 0xFFFFu; v[1] = a.x >> 16; v[2] = a.y & 0xFFFFu; v[3] = a.y >> 16;
+          v[4] = a.z & 0xFFFFu; v[5] = a.z >> 16; v[6] = a.w & 0xFFFFu; v[7] = a.w >> 16;
+        } else {
+          const uint4 a = *(const uint4 *)&acc[q], b = *(const uint4 *)&acc[q + 4];
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
       } else {
 #pragma unroll
-        for (int h = 0; h < 8; ++h) v[h] = q + h < cw ? (uint32_t)acc[q + h] : 0u;
+        for (int h = 0; h < 8; ++h) v[h] = q + h < cw ? (A16 ? (uint32_t)a16[q + h] : (uint32_t)acc[q + h]) : 0u;
       }
 #pragma unroll
       for (int h = 0; h < 8; ++h) {
@@ -193,7 +201,13 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
     const bool al = (((uintptr_t)prow) & 15) == 0;
     const double di = norm ? o.dsq[i] : 1.0;
     for (int q = qs + threadIdx.x * 2; q < cw; q += blockDim.x * 2) {
-      const int2 w = *(const int2 *)&acc[q];
+      int2 w;
+      if constexpr (A16) {
+        const uint32_t pr = *(const uint32_t *)&a16[q];
+        w = make_int2((int)(pr & 0xFFFFu), (int)(pr >> 16));
+      } else {
+        w = *(const int2 *)&acc[q];
+      }
       const int64_t c0 = col0 + q;
       const bool two = q + 1 < cw;
       double r0 = (double)w.x, r1 = two ? (double)w.y : 0.0;
@@ -214,7 +228,13 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
     }
   } else {
     for (int q = qs + threadIdx.x * 4; q < cw; q += blockDim.x * 4) {
-      const int4 w = *(const int4 *)&acc[q];
+      int4 w;
+      if constexpr (A16) {
+        const uint2 pr = *(const uint2 *)&a16[q];
+        w = make_int4((int)(pr.x & 0xFFFFu), (int)(pr.x >> 16), (int)(pr.y & 0xFFFFu), (int)(pr.y >> 16));
+      } else {
+        w = *(const int4 *)&acc[q];
+      }
       if (o.dtype == KMG_F32)
         emit4<KMG_F32, NT>(o, il, i, col0 + q, min(4, cw - q), w.x, w.y, w.z, w.w, norm);
       else

@@ -212,6 +212,22 @@ def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
         assert np.array_equal(raw.astype(np.int64), ref), chunk
 
 
+@pytest.mark.parametrize("chunk", ["96", "20480"])
+def test_mismatch_nb_acc16(ctx, tune, chunk):
+    """16-bit LDS counters in the neighbourhood-list Gram (KMG_NB_ACC16): exact by the
+    Gram-matrix bound K_ij^2 <= K_ii K_jj.  20 poly-A rows (K_ii = 93 * 93 * 28) exceed it
+    against each other and take two 32-bit passes over column halves; the random rows, also
+    in chunks holding a poly-A column, stay 16-bit.  Raw and normalised K bit-exact."""
+    codes, lens = E.synthetic(600, 101, seed=98)
+    codes[:20] = 0
+    tune(KMG_MM_FORM=4, KMG_NB_ACC16=1, KMG_MM_CHUNK=chunk)
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
+    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1))
+    assert raw[0, 0] == 93 * 93 * 28
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.mismatch_rows(codes, lens, 9, 1))
+
+
 @pytest.mark.parametrize("cap", ["-1", "4096"])
 def test_mismatch_nb_piece_fill_fallbacks(ctx, tune, cap):
     """The piece-assembled fill's two fallbacks: lists longer than its piece table (80 poly-A
