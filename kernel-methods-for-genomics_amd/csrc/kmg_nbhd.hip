@@ -395,7 +395,7 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
       myn += o[SW] - o[0];
     }
     {
-      const uint32_t inc = nb_wave_incl_scan(myn);
+      const uint32_t inc = nb_wave_incl_scan_dpp(myn);
       if (lane == 63) wtot[wave] = inc;
       __syncthreads();
       uint32_t base = 0, total = 0;
@@ -455,13 +455,13 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
           cnt = ro[sidx + 1] - a0;
           srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
         }
-        const uint32_t inc = nb_wave_incl_scan(cnt);
+        const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
         const uint32_t pos = carry + inc - cnt;
         if (j0 == 0) {
-          n0 = __shfl(cnt, 0, 64);
-          pre2 = __shfl(pos, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
+          n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
+          pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);  // (t2 < 64 for k <= 21)
         }
-        carry += __shfl(inc, 63, 64);
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
         {
           uint16_t *o = dst + dpos;
