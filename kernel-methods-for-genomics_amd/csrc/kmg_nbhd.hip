@@ -357,6 +357,33 @@ __device__ void nb_group_tables(int k, int nt, uint32_t *rt, uint32_t *pm) {
   }
 }
 
+// a group's range offsets into LDS (roff[r][q] = bin offset q of prefix range r), one word a
+// lane: consecutive lanes read a range's SW + 1 consecutive offsets (a few lines a wave
+// instruction instead of one line a lane), NLD loads in flight a thread before their stores
+template <int SW, int NT>
+__device__ __forceinline__ void nb_load_range_offsets(const uint32_t *__restrict__ xoff,
+                                                      int64_t cbase, uint32_t P,
+                                                      const uint32_t *pm, int mr, uint32_t *roff) {
+  constexpr int NLD = 4;
+  const int tot = mr * (SW + 1);
+  for (int w0 = threadIdx.x; w0 < tot; w0 += NLD * NT) {
+    uint32_t v[NLD];
+#pragma unroll
+    for (int t = 0; t < NLD; ++t) {
+      const int w = w0 + t * NT;
+      if (w < tot) {
+        const int r = w / (SW + 1), q = w - r * (SW + 1);
+        v[t] = xoff[cbase + (int64_t)(P ^ pm[r]) * SW + q];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NLD; ++t) {
+      const int w = w0 + t * NT;
+      if (w < tot) roff[w] = v[t];
+    }
+  }
+}
+
 template <int S, int NT, int WS>
 __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
@@ -387,13 +414,11 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
     if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 4^S lists empty (uniform)
     // ---- 1. the ranges' bin offsets and sizes; their LDS positions (block scan): thread t
     // owns the ranges [t RPT, t RPT + RPT)
+    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
+    __syncthreads();
     uint32_t myn = 0;
-    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
-      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
-#pragma unroll
-      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
-      myn += o[SW] - o[0];
-    }
+    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r)
+      myn += roff[r * (SW + 1) + SW] - roff[r * (SW + 1)];
     {
       const uint32_t inc = nb_wave_incl_scan_dpp(myn);
       if (lane == 63) wtot[wave] = inc;
@@ -542,13 +567,11 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
     auto slo = [&](int r) { return r < nfull ? 0 : hh * NL; };
     auto shi = [&](int r) { return r < nfull ? SW : hh * NL + NL; };
     // ---- 1. ranges: offsets, image positions (n + 14 words each: 8-aligned + source phase)
+    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
+    __syncthreads();
     uint32_t myn = 0;
-    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
-      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
-#pragma unroll
-      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
-      myn += o[shi(r)] - o[slo(r)] + 14u;
-    }
+    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r)
+      myn += roff[r * (SW + 1) + shi(r)] - roff[r * (SW + 1) + slo(r)] + 14u;
     {
       const uint32_t inc = nb_wave_incl_scan_dpp(myn);
       if (lane == 63) wtot[wave] = inc;
