@@ -212,6 +212,21 @@ def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
         assert np.array_equal(raw.astype(np.int64), ref), chunk
 
 
+def test_mismatch_triangle_mirror_ragged_chunks(ctx, tune):
+    """A full square K built by its upper block triangle + mirror_chunks_kernel with chunk
+    edges that are no multiple of its 64 x 64 tiles (328 columns, 4 chunks): raw int32 and
+    normalised float64 bit-exact.  (A 128 x 128 tile and loads issued before the LDS
+    stores measured equal at config 5, 27.2 vs 27.3 ms: the mirror runs at the HBM copy
+    rate, ~5.3 TB/s for 144 GB read + written.)"""
+    codes, lens = E.synthetic(1000, 101, seed=99)
+    tune(KMG_MM_FORM=4, KMG_MM_CHUNK="328")
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
+    assert ctx.last_plan()["triangle"]
+    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1))
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.mismatch_rows(codes, lens, 9, 1))
+
+
 @pytest.mark.parametrize("chunk", ["96", "20480"])
 def test_mismatch_nb_acc16(ctx, tune, chunk):
     """16-bit LDS counters in the neighbourhood-list Gram (KMG_NB_ACC16): exact by the
