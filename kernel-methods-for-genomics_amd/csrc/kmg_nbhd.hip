@@ -666,8 +666,22 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
           const uint32_t d0 = 8u * p;
           uint32_t jr = pst[p];
           uint32_t rej = re[jr], sdj = rsd[jr];
+          // the next two runs (past the sentinel these read other table words, never used:
+          // the sentinel's end lies past every entry)
+          const uint32_t re1 = re[jr + 1], sd1 = rsd[jr + 1], re2 = re[jr + 2], sd2 = rsd[jr + 2];
           uint32_t w[4];
-          if ((d0 + 8u > n0 && d0 < sx) || (d0 + 8u > e1 && d0 < sy) || d0 + 8u > e2) {
+          const bool padp = (d0 + 8u > n0 && d0 < sx) || (d0 + 8u > e1 && d0 < sy) || d0 + 8u > e2;
+          if (!padp && (re1 >= d0 + 8u || re2 >= d0 + 8u)) {
+            // at most three runs reach the piece: branch-free selects
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const uint32_t d = d0 + (uint32_t)q;
+              const uint32_t sd = d < rej ? sdj : d < re1 ? sd1 : sd2;
+              const uint32_t v = img[(sd + d) & 0xFFFFu];
+              if (q & 1) w[q >> 1] |= v << 16;
+              else w[q >> 1] = v;
+            }
+          } else if (padp) {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
               const uint32_t d = d0 + (uint32_t)q;
