@@ -21,10 +21,15 @@
 //   nb_count_kernel   per (c, u): n0, n1, n2 from the exact index (1 + 3k + 9k(k-1)/2
 //                     lookups of its bin offsets, L2-resident) -> pieces and segment ends
 //   launch_scan       list starts (in pieces; < 2^32: checked by the host)
-//   nb_fill_kernel    per (c, u), one wave: wave scan of the neighbour counts, copy of each
-//                     neighbour's posting list into its slot of the list (staged in LDS and
-//                     written with 16-byte stores when it fits)
-//   gram_nb_kernel    per (row i, chunk c): row windows -> (list start, pieces, segment
+//   list fills        (launch_nb_fill picks one)
+//     nb_fill_grouped_kernel  default: one workgroup per 16 k-mers sharing a (k-2)-letter
+//                     prefix, the 211 prefix ranges' sub-bin offsets in LDS; one wave a list:
+//                     DPP prefix sum of its 352 runs, lane-per-run copies from the index
+//     nb_fill_pieces_kernel   past 8.5 occurrences a k-mer and chunk: the ranges as an LDS
+//                     image (16-byte loads), each list assembled 16 bytes a lane from it
+//     nb_fill_kernel, nb_fill_ranges_kernel   the per-list and range-major forms (measured
+//                     slower; KMG_NB_FILL 1 / 6)
+//   gram_nb_kernel   per (row i, chunk c): row windows -> (list start, pieces, segment
 //                     ends) in LDS, a prefix sum over the row's lists, then every wave streams
 //                     an equal share of the row's pieces (four 16-byte loads in flight per
 //                     lane), adding the segment's weight for each of the 8 columns of a piece
