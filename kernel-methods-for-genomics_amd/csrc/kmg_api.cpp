@@ -109,7 +109,9 @@ struct Tuning {
                             // (kmg_nbhd.hip)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
-  int nb_unroll = 4;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8)
+  int nb_unroll = 0;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8;
+                            // 0 auto: 8, or 4 for an upper-block-triangle build -- interleaved
+                            // A/B, profiles/r04x2_nb_unroll_ab.jsonl)
   int nb_acc16 = 0;         // KMG_NB_ACC16: NB Gram with 16-bit LDS counters (K_ii K_jj bound)
   int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
   int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (grouped lane-per-run copies, 9
@@ -1256,7 +1258,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                           c->nb_lines.as<uint4>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, nbt, c->tune.nb_unroll,
+                                          (int)w[2], oq, c->stream, nbt,
+                                          c->tune.nb_unroll ? c->tune.nb_unroll : (o.tri ? 4 : 8),
                                           a16 ? c->diagv.as<double>() : nullptr,
                                           a16 ? c->nb_dmax.as<double>() : nullptr);
         }, true));
