@@ -957,7 +957,9 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
   for (int pass = 0; pass < npass; ++pass) {
     // pass columns [plo, plo + pcw) (relative to col0); 32-bit counters at acc[x - plo]
     const uint32_t plo = npass == 1 ? 0u : pass * half;
-    const uint32_t pcw = npass == 1 ? (uint32_t)cw : pass ? (uint32_t)cw - half : half;
+    // (a chunk's last columns can be fewer than half: pass 0 takes them all, pass 1 none)
+    const uint32_t ucw = (uint32_t)cw;
+    const uint32_t pcw = npass == 1 ? ucw : pass ? (ucw > half ? ucw - half : 0u) : min(half, ucw);
     {
       uint4 *acc4 = (uint4 *)smem;
       for (int w = threadIdx.x; w < (accn >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);

@@ -236,6 +236,10 @@ def test_mismatch_nb_acc16(ctx, tune, chunk):
     codes, lens = E.synthetic(600, 101, seed=98)
     codes[:20] = 0
     tune(KMG_MM_FORM=4, KMG_NB_ACC16=1, KMG_MM_CHUNK=chunk)
+    # a chunk narrower than the two-pass half width (5 columns: pass 0 takes them all)
+    raw5 = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes[17:22],
+                    lens[17:22], L.KMG_I32)  # rows 17..19 poly-A: two passes
+    assert np.array_equal(raw5.astype(np.int64), cref.mismatch_raw(codes[17:22], lens[17:22], 9, 1))
     raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
     assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1))
     assert raw[0, 0] == 93 * 93 * 28
