@@ -853,7 +853,7 @@ def main():
     if not args.no_mismatch:
         mm = run_build(ctx, dist, "mismatch_k9_m1",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64,
-                       args.mm_n, 3, max(3, args.steps // 4), 1, check_mismatch,
+                       args.mm_n, 3, max(10, args.steps), 2, check_mismatch,
                        gather=None if (rccl or dist.world == 1) else 0)
     c5 = None
     if rccl and not args.no_extra:
