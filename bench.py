@@ -51,7 +51,7 @@ GATHER_CEILING = 56.38e9  # random 128-B lines/s from a 78.6 MB table (profiles/
 INT8_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense bf16, MI355X_MICROARCH.md)
 METRIC = ("Gram pairs/sec (N×N) + full-K build time, spectrum k=8 and mismatch "
           "(k=9,m=1), 1/2/4/8 GPUs")
-STAGES = ("count", "scan", "place", "fine", "pack", "lists", "slots", "extract", "features", "diag",
+STAGES = ("count", "scan", "place", "fine", "pack", "lists", "nbfill", "slots", "extract", "features", "diag",
           "gram", "mirror", "gather")
 
 
@@ -580,6 +580,11 @@ def downstream(ctx):
     K += n * 1e-3 * np.eye(n)
     d = np.sqrt(np.diag(K))
     K = K / d[:, None] / d[None, :]
+    # K / d_i / d_j rounds differently at (i, j) and (j, i) (about a third of the entries
+    # differ by an ulp), which would send KRR / KLR to the per-column LU of an asymmetric K;
+    # every Gram kmg_gram returns is bitwise symmetric, so the bench's K is made so too
+    Ka = K
+    K = (K + K.T) / 2.0
     nbytes = K.nbytes
     dK = [ctx.dmalloc(nbytes) for _ in range(p)]
     for x in dK:
@@ -618,7 +623,22 @@ def downstream(ctx):
             out[f"krr_solve_n{m_}"] = {
                 "ms": ms, "alg_flops": fl, "achieved_TFLOPs": fl / (ms / 1e3) / 1e12,
                 "fp64_frac": fl / (ms / 1e3) / FP64_PEAK, "source": "KRR.py:33",
+                "factorisation": ctx.last_factorisation(),
                 "note": "symmetry check + Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I"}
+        # the same solve on the ulp-asymmetric K / d_i / d_j: LU (rocSOLVER dgetrf, launch-bound
+        # per column), what any user-normalised K not symmetrised costs
+        ctx.h2d(dK[1], Ka)
+        m_ = 2000
+        L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[1], n, m_, d_y, 0.1, d_a))
+        ctx.synchronize()
+        ctx.timing_reset()
+        for _ in range(reps):
+            L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[1], n, m_, d_y, 0.1, d_a))
+        tot, cnt = ctx.stage_stats("solve")
+        out["krr_solve_asymmetric_K_n2000"] = {
+            "ms": tot / cnt, "factorisation": ctx.last_factorisation(), "source": "KRR.py:33",
+            "note": "K != K^T by ulps: symmetry check + LU (dgetrf / dgetrs)"}
+        ctx.h2d(dK[1], K)
         it = ctypes.c_int32(0)
         m_ = 2000
         ctx.timing_reset()
@@ -627,6 +647,7 @@ def downstream(ctx):
         tot, cnt = ctx.stage_stats("solve")
         out["klr_fit_n2000"] = {"ms": tot, "iterations": it.value,
                                 "ms_per_iteration": tot / max(1, it.value),
+                                "factorisation": ctx.last_factorisation(),
                                 "source": "KLR.py:57-75",
                                 "note": "IRLS: dgemv + HIP IRLS kernel + Cholesky per step"}
         for m_ in (2000, n):
@@ -684,19 +705,25 @@ def gather_roofline(res, world, esz):
 
 def mm_nbhd_roofline(n, rows, gram_ms, plan, esz, k=9, P=93):
     """HBM model of the neighbourhood-list Gram launch (kmg_nbhd.hip): a row window reads
-    its list once per column chunk, E = (1 + 3k + 9k(k-1)/2) x (chunk x P / 4^k) uint16
-    entries (+ the three segments' padding to 8), and the row writes its K row (a square K
-    built by its upper block triangle: (nch + 1) / (2 nch) of both on average)."""
+    its list once per column chunk, (1 + 3k) x (chunk x P / 4^k) uint16 entries in segments
+    0 / 1 and 9k(k-1)/2 x (chunk x P / 4^k) in segment 2 -- packed, 16 B a 15 entries (the
+    0.5 % of 15-entry runs that spill, measured on this data, ~1.078 B an entry), or 2 B --
+    plus the segments' padding to 8, and the row writes its K row (a square K built by its
+    upper block triangle: (nch + 1) / (2 nch) of both on average)."""
     nch, ch = max(1, plan["nchunks"]), max(8, plan["chunk"])
-    nb = 1 + 3 * k + 9 * k * (k - 1) // 2
+    n01, n2 = 1 + 3 * k, 9 * k * (k - 1) // 2
+    b2 = 1.078 if plan.get("packed") else 2.0
     f = (nch + 1) / (2.0 * nch) if plan["triangle"] else 1.0
-    per_window = 2.0 * (nb * n * P / 4.0 ** k + 10.5 * nch)  # bytes over all chunks
+    occ = n * P / 4.0 ** k  # occurrences of a k-mer over all chunks
+    per_window = (2.0 * n01 + b2 * n2) * occ + 2.0 * 10.5 * nch  # bytes over all chunks
     reads = rows * P * per_window * f
     writes = rows * n * esz * f
     alg = reads + writes
-    return {"bound": "hbm", "table": "neighbourhood lists (%d chunk(s) of %d columns%s; %d-thread "
-                                     "workgroups)" % (nch, ch, ", upper block triangle"
-                                                      if plan["triangle"] else "", plan["threads"]),
+    return {"bound": "hbm", "table": "neighbourhood lists (%s segment 2; %d chunk(s) of %d "
+                                     "columns%s; %d-thread workgroups)"
+                                     % ("packed" if plan.get("packed") else "16-bit", nch, ch,
+                                        ", upper block triangle" if plan["triangle"] else "",
+                                        plan["threads"]),
             "list_bytes_per_window": per_window, "list_bytes_per_launch": reads,
             "k_bytes_per_launch": writes, "achieved_GBps": alg / (gram_ms / 1e3) / 1e9,
             "peak_GBps": HBM_PEAK / 1e9, "frac": alg / (gram_ms / 1e3) / HBM_PEAK}
@@ -706,28 +733,13 @@ def mm_gather_roofline(n, rows, gram_ms, plan, k=9, P=93):
     """Random-line gather model of the MM(9,1) Gram launch (see the secondary line), for the
     chunking the library reports (kmg_last_plan): a row reads every column chunk, or (a
     square K built by its upper block triangle) (nch + 1) / 2 of them on average."""
-    import math
     if plan["formulation"] == "neighbourhood":
         return mm_nbhd_roofline(n, rows, gram_ms, plan, 8)
-    nch, ch = max(1, plan["nchunks"]), max(8, plan["chunk"])
+    nch = max(1, plan["nchunks"])
     reads = (nch + 1) / 2.0 if plan["triangle"] else float(nch)
-    if plan["formulation"] == "pair_lines":
-        mean = 16.0 * ch * P / 4.0 ** k
-        eu = ec = 0.0
-        pr = math.exp(-mean)
-        for x in range(0, 4000):
-            if x > 0:
-                pr *= mean / x
-                eu += pr * math.ceil(x / 64.0)
-                ec += pr * math.ceil((8.0 + x) / 64.0)
-        per_chunk = 27 * eu + 9 * ec
-        form = ("pair lines (27 uniform + 9 correction groups a window and chunk; %d chunk(s) "
-                "of %d columns%s; %d-thread workgroups)"
-                % (nch, ch, ", upper block triangle" if plan["triangle"] else "", plan["threads"]))
-    else:
-        per_chunk = 117.0
-        form = ("slot table (117 one-line lists a window and chunk, %d chunks%s)"
-                % (nch, ", upper block triangle" if plan["triangle"] else ""))
+    per_chunk = 117.0
+    form = ("slot table (117 one-line lists a window and chunk, %d chunks%s)"
+            % (nch, ", upper block triangle" if plan["triangle"] else ""))
     per_window = per_chunk * reads
     lines = rows * P * per_window
     rate = lines / (gram_ms / 1e3)
@@ -772,7 +784,7 @@ def projection(sp, n, extra):
     if c5:
         s5 = c5["stages_ms"]
         t5_index = sum(v for k, v in s5.items() if k in ("count", "scan", "place", "fine", "pack",
-                                                         "lists", "slots"))
+                                                         "lists", "nbfill", "slots"))
         n5 = c5["N"]
         # the one-GPU build computes the upper block triangle ((nch + 1) / (2 nch) of the full
         # rows, nch from the plan the library reported) and mirrors the rest: the model wants
@@ -786,6 +798,57 @@ def projection(sp, n, extra):
                         "full_rows_gram_ms_model": g_rows},
             **{str(g): v for g, v in scaling_projection(
                 n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1, chunk=ch5).items()}}
+    return out
+
+
+_STAGE_KEYS = ("count", "place", "fine", "pack", "lists", "nbfill", "slots", "diag", "gram",
+               "mirror")
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def _compact_record(rec):
+    """The few keys of a build record the stdout tail must carry."""
+    out = {}
+    for k in ("workload", "N", "ms_per_step", "value", "pairs_per_s", "spot_check"):
+        if k in rec:
+            out[k] = _r(rec[k]) if k != "workload" else rec[k][:60]
+    st = rec.get("stages_ms") or {}
+    out["stages_ms"] = {k: _r(st[k]) for k in _STAGE_KEYS if k in st}
+    pl = rec.get("plan") or {}
+    if pl:
+        out["plan"] = {k: pl.get(k) for k in ("formulation", "nchunks", "chunk", "triangle")}
+    for k in ("hbm_frac_of_gram_and_mirror", "gram_hbm_frac"):
+        if k in rec:
+            out[k] = _r(rec[k])
+    if isinstance(rec.get("cpu_baseline"), dict):
+        out["cpu_baseline"] = {k: _r(rec["cpu_baseline"].get(k)) for k in ("value", "cores")}
+    return out
+
+
+def _compact_configs(extra):
+    out = {}
+    for k, v in extra.items():
+        if k.startswith("config") and isinstance(v, dict):
+            out[k] = _compact_record(v)
+    if isinstance(extra.get("run_py_kernels_n9000"), dict):
+        out["run_py_kernels_n9000_total_ms"] = _r(extra["run_py_kernels_n9000"].get("total_ms"))
+    return out
+
+
+def _projection_summary(proj):
+    """G = 8 speedup models per line of projection() (the full tables: bench_details.json)."""
+    out = {}
+    h = proj.get("headline_strong_collective_free", {}).get("8")
+    if h:
+        out["headline_collective_free"] = _r(h["speedup_model"], 3)
+    for k, v in proj.items():
+        if k.startswith("config") and isinstance(v, dict) and "8" in v:
+            g8 = v["8"]
+            out[k.split("_")[0]] = {"every_gpu": _r(g8.get("every_gpu_speedup"), 3),
+                                   "collective_free": _r(g8.get("collective_free_speedup"), 3)}
     return out
 
 
@@ -960,11 +1023,25 @@ def main():
             "note": "reference kernels.py cost model (BASELINE.md), survey container 8-core Xeon"}
         if mm:
             line["secondary"]["cpu_baseline"] = cpu["mismatch_k9_m1"]
-    if extra:
-        line["configs"] = extra
+    # The full records (every config's stages, run.py's kernels, the downstream solvers, the
+    # G > 1 projection, the secondary's gather model) go to bench_details.json; the JSON line
+    # keeps compact forms and ends with the configs 2 / 5 and configs[2] (secondary) numbers,
+    # so the driver's 2000-character stdout tail holds them.
+    details = {"configs": extra, "secondary": line.get("secondary")}
     if dist.world == 1:
-        line["projection"] = projection(sp, n, extra)
+        details["projection"] = projection(sp, n, extra)
+        line["projection_g8"] = _projection_summary(details["projection"])
+    if extra:
+        line["configs"] = _compact_configs(extra)
+    if "secondary" in line:
+        line["secondary"] = _compact_record(line.pop("secondary"))
+    line["details_file"] = "bench_details.json"
     if dist.rank == 0:
+        try:
+            with open(os.path.join(ROOT, "bench_details.json"), "w") as f:
+                json.dump(details, f, indent=1, default=str)
+        except OSError as e:
+            line["details_file"] = "unwritable: %r" % (e,)
         print(json.dumps(line), file=json_out, flush=True)
     dist.close()
 

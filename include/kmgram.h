@@ -157,6 +157,26 @@ int kmg_features(kmg_ctx *ctx, const kmg_params *p, const uint8_t *codes, const 
                  int64_t n, int64_t ldc, const uint32_t *cols, int64_t ncols, double *out,
                  int64_t ld_out);
 
+/*
+ * kmg_features over SYMBOL columns: column j is cols[16 j .. 16 j + k), k symbol codes in the
+ * code space of `codes` (any uint8 but the padding code 255), so every symbol compares by
+ * identity: get_phi_u(x, k, betas) with betas holding letters outside A/C/G/T (string
+ * equality, kernels.py:23-24: the beta 'GTN' counts the windows 'GTN'), get_phi_km(x, k, m,
+ * betas) with format()ed values outside 1..4 in x or in the betas (integer comparison,
+ * kernels.py:174).  KMG_SPECTRUM or KMG_MISMATCH only.  flags KMG_FEATURES_BCAST (mismatch):
+ * rows shorter than the window take numpy's broadcasting of their short k-mers -- a 1-symbol
+ * window compares that symbol against every letter of the beta, an empty one (k = 1) counts
+ * with 0 mismatches -- and a row whose short windows would not broadcast is KMG_EINVAL (the
+ * reference raises).  Note: the Gram paths (kmg_gram, KMG_MISMATCH) give a window holding a
+ * non-ACGT symbol weight 0, where get_phi_km counts the symbol as one mismatch; the reference's
+ * get_mismatch_K never meets such a window (format() raises on letters outside A/C/G/T,
+ * kernels.py:193), so that Gram case has no reference counterpart (parity unpinned).
+ */
+#define KMG_FEATURES_BCAST 1
+int kmg_features_sym(kmg_ctx *ctx, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                     int64_t n, int64_t ldc, const uint8_t *cols, int64_t ncols, int32_t flags,
+                     double *out, int64_t ld_out);
+
 /* normalize_K (kernels.py:398-415) in place on a host float64 matrix, including the
  * "K[0,0]==1 -> unchanged" rule (returns 1 in *skipped then). */
 int kmg_normalize(kmg_ctx *ctx, double *K, int64_t n, int64_t ld, int32_t *skipped);
@@ -288,8 +308,20 @@ int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *
  * choosing),
  * plan[1] columns per chunk, plan[2] column chunks, plan[3] 1 when a full square K was built
  * by its upper block triangle and mirrored, plan[4] Gram workgroup threads (0 where the
- * formulation has no column chunks).  No reference counterpart (diagnostics). */
-int kmg_last_plan(kmg_ctx *ctx, int32_t plan[5]);
+ * formulation has no column chunks), plan[5] neighbourhood lists only: 1 when their Hamming-2
+ * segments were sorted and packed (1 B + 1/15 of 2 B an entry), 0 when they stayed 16-bit.
+ * No reference counterpart (diagnostics). */
+int kmg_last_plan(kmg_ctx *ctx, int32_t plan[6]);
+
+/* The factorisation of the last KRR / KLR solve on ctx (diagnostics, no reference
+ * counterpart; the reference inverts with numpy's LU, KRR.py:33, KLR.py:55-56):
+ * KMG_FACTOR_CHOLESKY for a bitwise-symmetric positive-definite system (every Gram kmg_gram
+ * returns), KMG_FACTOR_LU_ASYMMETRIC when K != K^T bitwise, KMG_FACTOR_LU_INDEFINITE when
+ * Cholesky failed; 0 before any solve. */
+#define KMG_FACTOR_CHOLESKY 1
+#define KMG_FACTOR_LU_ASYMMETRIC 2
+#define KMG_FACTOR_LU_INDEFINITE 3
+int kmg_last_factorisation(kmg_ctx *ctx, int32_t *kind);
 
 /* RCCL (one rank per process / GPU).  id is an opaque 128-byte ncclUniqueId. */
 int kmg_comm_unique_id(uint8_t id[128]);

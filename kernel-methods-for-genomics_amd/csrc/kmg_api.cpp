@@ -88,15 +88,17 @@ struct DevBuf {
 };
 
 // "pack" = 2-bit packing of the input, "slots" = slot layout of the mismatch index,
-// "gather" = the RCCL row all-gather (kmg_allgather_rows)
+// "lists" = neighbourhood-list sizes and starts, "nbfill" = the neighbourhood lists
+// themselves, "gather" = the RCCL row all-gather (kmg_allgather_rows)
 const char *kStageNames[] = {"count",   "scan",     "place", "fine",    "diag",
                              "gram",    "extract",  "pack",  "features", "combine",
                              "solve",   "slots",    "memset", "gather", "unpack",
-                             "mirror",  "lists"};
-constexpr int kNumStages = 17;
+                             "mirror",  "lists",    "nbfill"};
+constexpr int kNumStages = 18;
 enum {
   ST_COUNT, ST_SCAN, ST_PLACE, ST_FINE, ST_DIAG, ST_GRAM, ST_EXTRACT, ST_PACK, ST_FEATURES,
-  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK, ST_MIRROR, ST_LISTS
+  ST_COMBINE, ST_SOLVE, ST_SLOTS, ST_MEMSET, ST_GATHER, ST_UNPACK, ST_MIRROR, ST_LISTS,
+  ST_NBFILL
 };
 
 // Tuning knobs: read from the environment once per context (kmg_create) and again only on
@@ -105,26 +107,23 @@ struct Tuning {
   int sp_chunk = 24576;     // KMG_SP_CHUNK: columns per chunk, spectrum index
   int mm_chunk = 20480;     // KMG_MM_CHUNK: columns per chunk, mismatch index (upper bound)
   int mm_form = 0;          // KMG_MM_FORM: 0 auto, 1 drop-one slot table, 2 drop-two pair table,
-                            // 3 drop-two pair lines (kmg_pairs.hip), 4 neighbourhood lists
-                            // (kmg_nbhd.hip)
+                            // 4 neighbourhood lists (kmg_nbhd.hip); (3, round 3's pair lines,
+                            // was removed in round 5: measured slower than the lists at k = 9)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
   int nb_unroll = 0;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8;
                             // 0 auto: 8, or 4 for an upper-block-triangle build -- interleaved
                             // A/B, profiles/r04x2_nb_unroll_ab.jsonl)
-  int nb_acc16 = 0;         // KMG_NB_ACC16: NB Gram with 16-bit LDS counters (K_ii K_jj bound)
-  int nb_cap = -1;          // KMG_NB_CAP: entries of the grouped fill's LDS range image (-1 auto)
-  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (grouped lane-per-run copies, 9
-                            // past 8.5 occurrences a k-mer and chunk), 1 per list, 2 grouped
-                            // S = 1, 3 / 4 / 5 grouped S = 2 with 2- / 4- / 8-byte stores,
-                            // 6 range-major, 9 / 10 piece-assembled (whole / half groups)
+  int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (sorted + packed segment 2 where a
+                            // list is read >= nb_pack_reads times and nb_sorted_cap allows;
+                            // else staged 16-bit lists), 1 sorted, 2 grouped lane-per-run,
+                            // 3 piece-assembled, 4 staged (launch_nb_fill)
+  int nb_pack_reads = 16;   // KMG_NB_PACK_READS: reads a list must get for the packed segment 2
+                            // (its sort costs ~1 ms more at N=20000, k=9; each read of the
+                            // list saves ~0.9 of its 16-bit segment-2 bytes)
   int mm_tri = 1;           // KMG_MM_TRI: full square mismatch K by its upper block triangle
                             // (column chunks at or right of the row's own) + mirror, 0 off
   int esc_cap = 0;          // KMG_ESC_CAP: escape-list entries of uint8 round slabs (0: by size)
-  int pl_dbg = 0;           // KMG_PL_DBG: diagnostics only (wrong results): 1 no correction
-                            // weights, 2 no bank rotation
-  int pl_threads = 0;       // KMG_PL_THREADS: pair-lines Gram workgroup, 1024 (one a CU), 512
-                            // (two a CU, chunks <= ~11800 columns) or 0 auto (pl_threads())
   int ss_lpp = 0;           // KMG_SS_LPP: SS grouped sweep, lanes a pair (0 auto, 16, 32)
   int la_lpp = 0;           // KMG_LA_LPP: intended-LA grouped sweep, lanes a pair (0 auto, 16, 32)
   int wd_form = 0;          // KMG_WD_FORM: 0 2-bit packed WD kernel, 1 byte-tile WD kernel
@@ -167,18 +166,14 @@ void read_tuning(Tuning &t) {
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
-  t.pl_dbg = env_or("KMG_PL_DBG", d.pl_dbg);
   t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
   t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.ss_lpp = env_or("KMG_SS_LPP", d.ss_lpp);
-  t.pl_threads = env_or("KMG_PL_THREADS", d.pl_threads);
-  if (t.pl_threads != 512 && t.pl_threads != 1024) t.pl_threads = 0;
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
-  t.nb_cap = env_or("KMG_NB_CAP", d.nb_cap);
+  t.nb_pack_reads = env_or("KMG_NB_PACK_READS", d.nb_pack_reads);
   t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
-  t.nb_acc16 = env_or("KMG_NB_ACC16", d.nb_acc16);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -209,11 +204,10 @@ struct kmg_ctx {
   DevBuf esc, esc_all, esc_cnt;   // uint8 round slabs: escape list, all-gathered lists, counts
   uint32_t esc_cap = 0;           // entries of `esc` in use by the current build (0: none)
   int64_t cur_n = 0;              // columns of the current Gram call
-  int32_t plan[5] = {-1, 0, 0, 0, 0};  // last spectrum / mismatch call (kmg_last_plan)
+  int32_t plan[6] = {-1, 0, 0, 0, 0, 0};  // last spectrum / mismatch call (kmg_last_plan)
+  int32_t last_factor = 0;        // last KRR / KLR solve's factorisation (kmg_last_factorisation)
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
-  DevBuf pr_big;                  // pair lines: blocks with groups past the small image
-  DevBuf nb_seg, nb_lines;        // neighbourhood lists: segment ends, the lists
-  DevBuf nb_dmax;                 // per column chunk, the largest raw K_jj (16-bit counters)
+  DevBuf nb_seg, nb_use, nb_lines;  // neighbourhood lists: segment ends, pieces in use, lists
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -503,78 +497,16 @@ int pair_chunk(int64_t n, int pmax, int k, int cap) {
   return (int)std::max<int64_t>(8, (best + 7) & ~7LL);
 }
 
-// Columns per chunk of the pair-lines table (kmg_pairs.hip): the fewest expected 128-byte
-// lines per row window, nch x (uniform pairs E[ceil(X / 64)] + k correction pairs
-// E[ceil((8 + X) / 64)]), X ~ Poisson(chunk * pmax / 4^(k-2)), over the chunkings whose
-// int32 LDS accumulator fits beside the kernel's wave queues and whose per-chunk table
-// stays Infinity-Cache sized (<= 192 MB: the chunk-major grid reads one chunk's table at a
-// time, and the K rows stream past it).
-// tri_esz > 0 (a full square K by its upper block triangle, OutSpec::tri): a row reads
-// (nch + 1) / 2 chunks on average and the mirror moves 2 tri_esz (nch - 1) / (2 nch) n^2
-// bytes; lines are priced at the measured random-line rate of the Infinity Cache (54 G
-// lines/s), the mirror at 5.5 TB/s.
+// Cost of a chunking, in seconds: a row reads nch x lines_per_window_chunk lines per window,
+// or, for a full square K built by its upper block triangle (tri_esz > 0), (nch + 1) / 2 of
+// them on average while the mirror moves 2 tri_esz (nch - 1) / (2 nch) n^2 bytes; lines are
+// priced at the measured random-line rate of the Infinity Cache (54 G lines/s), the mirror at
+// 5.5 TB/s.
 double tri_cost(int64_t n, int pmax, double lines_per_window_chunk, int64_t nch, int tri_esz) {
   if (tri_esz <= 0) return (double)nch * lines_per_window_chunk;
   const double lines = (double)n * pmax * lines_per_window_chunk * (double)(nch + 1) / 2.0;
   const double mirror = 2.0 * tri_esz * (double)n * n * (double)(nch - 1) / (2.0 * nch);
   return lines / 54e9 + mirror / 5.5e12;
-}
-
-// Workgroup size of the pair-lines Gram kernel.  512 threads (two workgroups a CU: one row's
-// float64 epilogue and LDS adds overlap the other row's line gathers) need chunks of <= ~11800
-// columns: they win where the K is built by its upper block triangle anyway or fits one such
-// chunk; a row range over more columns keeps 1024 (one chunk of up to ~24000 columns).
-// N=20000 normalised square K: Gram 3.97 -> 3.19 ms (2 chunks, triangle), build 4.40 -> 4.09;
-// the same 2 chunks without the triangle 4.21 (profiles/r03t_pl_threads_ab.jsonl).
-int64_t pl_max_chunk(int pmax, int ldp, int threads) {
-  const int64_t lds_words = (threads == 512 ? 80 : 160) * 1024 / 4;  // 512: two workgroups a CU
-  const int64_t m =
-      (lds_words - 66 - pmax - ldp - KMG_PAIRS_MAX - (threads / 64) * KMG_PL_WAVE_WORDS) & ~7LL;
-  return std::min<int64_t>(m, 65536 - 64);
-}
-
-int pl_threads(const Tuning &t, int64_t n, int tri_esz, int pmax, int ldp) {
-  if (t.pl_threads) return t.pl_threads;
-  return (tri_esz > 0 || n <= pl_max_chunk(pmax, ldp, 512)) ? 512 : 1024;
-}
-
-int pl_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads) {
-  const double keys = (double)pow4(k - 2);
-  const int np = k * (k - 1) / 2;
-  int64_t max_chunk = pl_max_chunk(pmax, ldp, threads);
-  if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
-  if (max_chunk < 8) return 8;
-  const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
-  int64_t best = std::min<int64_t>(std::max<int64_t>(n, 8), max_chunk);
-  double best_lines = 1e300;
-  for (int64_t nch = nch0; nch <= nch0 + 64; ++nch) {
-    const int64_t ch = ((n + nch - 1) / nch + 7) & ~7LL;
-    if (ch > max_chunk) continue;
-    const double mean = (double)ch * pmax / keys;
-    double eu = 0.0, ec = 0.0, pr = std::exp(-mean), cdf = 0.0;
-    for (int x = 0; x < 4000 && cdf < 1.0 - 1e-12; ++x) {
-      if (x > 0) pr *= mean / x;
-      cdf += pr;
-      if (x > 0) {
-        eu += pr * std::ceil(x / 64.0);
-        ec += pr * std::ceil((8.0 + x) / 64.0);
-      }
-    }
-    const double per = (np - k) * eu + k * ec;  // lines per window and chunk
-    const double table = per * keys * 128.0;      // bytes of one chunk's table
-    if (table > 192e6 && nch < nch0 + 64) continue;
-    if ((double)nch * (double)pow4(k) > (double)(1 << 28)) continue;  // exact index bins
-    if ((double)np * nch * keys * 16.0 >= 4294967296.0) continue;      // pl_pack work-items
-    // + a quarter line per list for its summary record and decode, which every (window,
-    // pair, chunk) pays however small the group (without it, tiny groups at large k would
-    // make every extra chunk look free)
-    const double cost = tri_cost(n, pmax, per + 0.25 * np, nch, tri_esz);
-    if (cost < best_lines * (1.0 - 1e-12)) {
-      best_lines = cost;
-      best = ch;
-    }
-  }
-  return (int)std::max<int64_t>(8, best);
 }
 
 // Columns per chunk of the drop-one slot table.  A row reads one 128-byte line per
@@ -616,21 +548,28 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
 }
 
 // Columns per chunk of the neighbourhood-list Gram (kmg_nbhd.hip).  A row reads, per chunk,
-// its windows' lists: ~2 B x (1 + 3k + 9k(k-1)/2) x P x chunk x P / 4^k plus three padded
-// segment tails per list, so the chunk count barely changes the bytes a full row reads; it
-// only matters for a square K built by its upper block triangle (tri_esz > 0), where a row
-// reads (nch + 1) / (2 nch) of them and writes as much of its K row, and the mirror moves
+// its windows' lists: (1 + 3k) x 2 B + 9k(k-1)/2 x b2 per occurrence (b2 = 1.08 B for a packed
+// segment 2, 2 B for 16-bit lists) x P x chunk x P / 4^k, plus three padded segment tails
+// per list, so the chunk count barely changes the bytes a full row reads; it only matters
+// for a square K built by its upper block triangle (tri_esz > 0), where a row reads
+// (nch + 1) / (2 nch) of them and writes as much of its K row, and the mirror moves
 // 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
-// mirror; the largest chunk is the int32 LDS accumulator beside the row tables.
-int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool a16) {
-  const int64_t lds_words = (threads == 512 ? 80 : 160) * 1024 / 4;
-  // (16-bit counters: two columns a word)
-  int64_t max_chunk = ((lds_words - 64 - 4 * (int64_t)pmax - 1 - ldp - 8) * (a16 ? 2 : 1)) & ~7LL;
+// mirror.  Largest chunk: the int32 LDS accumulator beside the row tables, and where
+// segment 2 packs, the sorted fill's LDS buffer (nb_sorted_max_chunk: ~24900 at k = 9).
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted) {
+  // two workgroups a CU (their table builds, epilogues and streams overlap; one a CU measured
+  // 22 % slower at N=20000, profiles/r05g_*): the accumulator, 16 dummy columns and the row
+  // table in 80 KB (1024 threads) or 40 KB (512)
+  const int64_t lds_words = (threads == 512 ? 40 : 80) * 1024 / 4;
+  int64_t max_chunk = (lds_words - 16 - 4 * (int64_t)pmax - 2 - ldp) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
+  const int smax = sorted ? nb_sorted_max_chunk(k, pmax) : 0;
+  if (smax >= 8) max_chunk = std::min<int64_t>(max_chunk, smax);
   if (cap > 0) max_chunk = std::min<int64_t>(max_chunk, std::max(8, cap));
   if (max_chunk < 8) return 8;
   const int64_t nch0 = std::max<int64_t>(1, (n + max_chunk - 1) / max_chunk);
-  const int64_t nb = 1 + 3 * k + 9 * (int64_t)k * (k - 1) / 2;
+  const double n01 = 1 + 3 * k, n2 = 4.5 * k * (k - 1);
+  const double b2 = smax >= 8 ? 1.08 : 2.0;
   const double dens = (double)pmax / (double)pow4(k);  // occurrences of a k-mer per column
   const int esz = tri_esz > 0 ? tri_esz : 4;
   int64_t best = std::min<int64_t>(std::max<int64_t>(n, 8), max_chunk);
@@ -639,13 +578,13 @@ int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int thre
     const int64_t ch = ((n + nch - 1) / nch + 7) & ~7LL;
     if (ch > max_chunk) continue;
     const double f = tri_esz > 0 ? (double)(nch + 1) / (2.0 * nch) : 1.0;
-    const double row_reads = 2.0 * nb * pmax * dens * (double)n + 2.0 * 10.5 * pmax * nch;
+    const double row_reads = (2.0 * n01 + b2 * n2) * pmax * dens * (double)n + 2.0 * 10.5 * pmax * nch;
     const double gram = (double)n * (row_reads + esz * (double)n) * f;
     const double mirror = tri_esz > 0 ? 2.0 * esz * (double)n * n * (double)(nch - 1) / (2.0 * nch) : 0.0;
     // + building the lists: ~2 ns per (chunk, k-mer) bin plus the table at ~1 TB/s (grouped
     // fill, measured: N=20000 one chunk 1.44 ms, N=200000 five chunks ~13 ms)
     const double build = (double)nch * (double)pow4(k) * 2.0e-9 +
-                         2.0 * nb * (double)n * pmax / 1e12;
+                         (2.0 * n01 + b2 * n2) * (double)n * pmax / 1e12;
     const double cost = gram / 6e12 + mirror / 5e12 + build;
     if (cost < best_cost * (1.0 - 1e-12)) {
       best_cost = cost;
@@ -853,30 +792,26 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
 // ----------------------------------------------------------------- dispatch
 // Formulation of a spectrum / mismatch call (one decision, used by gram_device and by
 // kmg_gram_blocks' choice of the round-slab format).
+// (kmg_last_plan numbers: SM_PL, round 3's pair lines, was removed in round 5)
 enum SmPath { SM_DENSE, SM_HAMMING, SM_POSTING, SM_SLOTS, SM_PAIRS, SM_PL, SM_NB };
 constexpr int32_t KMG_PLAN_GENERIC = 7;  // kmg_last_plan: the per-pair kernels of k > 16
 SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
   const bool exact = !mm || p->m == 0;  // spectrum-shaped: only ham 0 counts
-  // mismatch m = 1, auto (N=20000 normalised float64 builds, profiles/r03g_mm_forms.jsonl):
-  //   k = 9 up to one pair-lines chunk (n <= 24000): the pair-lines table (3.93 ms against
-  //     the slot table's 4.17: 0.64x the lines, uniform groups); larger n (config 5,
-  //     7 chunks): the slot table (one-GPU raw K 184.6 vs 210.9 ms, both upper-triangle);
-  //   k = 10, 11: the drop-two pair table (k = 10: 4.74 vs 5.98 ms slots);
+  // mismatch m = 1, auto:
+  //   k = 9 (BASELINE configs[2] and [4]): the neighbourhood lists at every n (N=20000
+  //     normalised build 4.03 -> 3.73 ms, N=200000 one-GPU raw K 185.5 -> 134.8 ms against
+  //     round 3's pair lines / slot table; profiles/r04_nb_*)
+  //   k = 10, 11: the drop-two pair table (k = 10: 4.74 vs 5.98 ms slots; round 2);
   //   k = 8 and 12: the drop-one slot table (k = 8: 6.70 vs 7.78 pair lines, 15.8 pairs).
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
-  // k = 9 (BASELINE configs[2] and [4]): the neighbourhood lists at every n (N=20000
-  // normalised build 4.03 -> 3.73 ms, N=200000 one-GPU raw K 185.5 -> 134.8 ms against the
-  // pair lines / slot table; profiles/r04_nb_*)
-  const bool use_nb = s1 && k >= 3 && k <= 12 && (form == 4 || (form == 0 && k == 9));
-  const bool use_pl =
-      s1 && !use_nb && k >= 3 && k <= 12 && (form == 3 || (form == 0 && k == 9 && n <= 24000));
-  const bool use_pairs = s1 && !use_pl && !use_nb &&
+  const bool use_nb = s1 && k >= 4 && k <= 12 && (form == 4 || (form == 0 && k == 9));
+  const bool use_pairs = s1 && !use_nb &&
                          (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
-  const bool use_slots = s1 && !use_pairs && !use_pl && !use_nb && k >= 8 && k <= 12 && form != 2;
-  const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_pl || use_nb;
+  const bool use_slots = s1 && !use_pairs && !use_nb && k >= 8 && k <= 12 && form != 2;
+  const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_nb;
   // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
   // every count <= 127, i.e. <= 127 windows), posting lists for large sparse k,
   // all-pairs Hamming otherwise.  KMG_ALGO: 0 auto, 1 dense, 2 index/hamming.
@@ -887,7 +822,6 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
     return SM_DENSE;  // (algo 1 without dense_ok: gram_device reports it)
   if (!use_index) return SM_HAMMING;
   if (use_pairs) return SM_PAIRS;
-  if (use_pl) return SM_PL;
   if (use_nb) return SM_NB;
   return exact ? SM_POSTING : SM_SLOTS;
 }
@@ -941,7 +875,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                     (long long)ldc, g.window);
       // kmg_last_plan: reset first, so no return below reports the previous call's plan
       c->plan[0] = -1;
-      c->plan[1] = c->plan[2] = c->plan[3] = c->plan[4] = 0;
+      c->plan[1] = c->plan[2] = c->plan[3] = c->plan[4] = c->plan[5] = 0;
       if (k > 16) {
         // k-mers past 32 bits: the generic per-pair kernels (kmg_generic.hip)
         c->plan[0] = KMG_PLAN_GENERIC;
@@ -1014,15 +948,15 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       const SmPath path = sm_path(c->tune, p, g.pmax, n);
-      const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS, use_pl = path == SM_PL;
+      const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
       const bool use_nb = path == SM_NB;
-      const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_pl || use_nb;
+      const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_nb;
       // a full square K (one range over [0, n), every column written) of a mismatch
       // posting-list formulation: built by its upper block triangle, then mirrored
       // (OutSpec::tri; set below once the chunking is known)
       const bool square = ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
                           ranges[0].col_lo == 0 && !after && !narrow && n > 0;
-      const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_pl || use_nb))
+      const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_nb))
                               ? (int)dtype_size(dt) : 0;
       auto mirror = [&]() -> int {
         if (!o.tri) return KMG_OK;
@@ -1145,50 +1079,56 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         }, true));
         return mirror();
       }
-      if (use_pl) {
-        // exact k-mer index over the mismatch window (kernels.py:171), then the pair-lines
-        // table assembled from it (kmg_pairs.hip): uniform pairs first, then the k
-        // correction pairs G(r) = {r-1, r} (r >= 1) and {0, k-1} (outer letter k-1)
+      if (use_nb) {
+        // exact k-mer index over the mismatch window (kernels.py:171), then every (chunk,
+        // k-mer)'s neighbourhood list assembled from it (kmg_nbhd.hip)
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        const int plt = pl_threads(c->tune, n, tri_esz, g.pmax, (int)pkd.ldp);
-        choose_chunks(g, pl_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, plt));
+        const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
+        // the sorted fill (packed segment 2) where each list is read often enough to repay its
+        // sort: reads a list = rows read x windows a row / 4^k (x (nch + 1) / (2 nch) for a
+        // square by its block triangle); else 16-bit lists
+        bool sorted = c->tune.nb_fill == 1;
+        if (c->tune.nb_fill == 0) {
+          int64_t rows_read = 0;
+          for (const RowRange &r : ranges) rows_read += r.row1 - r.row0;
+          const int ch = nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, true);
+          const int64_t nch = (n + ch - 1) / ch;
+          const double f = (tri_esz > 0 && nch > 1) ? (double)(nch + 1) / (2.0 * nch) : 1.0;
+          sorted = (double)rows_read * g.pmax / (double)pow4(k) * f >= (double)c->tune.nb_pack_reads;
+        }
+        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, sorted));
         o.tri = tri_esz > 0 && g.nchunks > 1;
-        note_plan(plt);
+        note_plan(nbt);
+        c->plan[5] = (sorted && nb_sorted_cap(k, g.pmax, g.chunk) > 0) ? 1 : 0;
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
-        PairGeom pg{};
-        pg.k = k;
-        pg.nchunks = g.nchunks;
-        pg.chunk = g.chunk;
-        pg.nkeys2 = (uint32_t)pow4(k - 2);
-        auto is_corr = [k](int pp, int qq) { return qq == pp + 1 || (pp == 0 && qq == k - 1); };
-        for (int pp = 0; pp < k; ++pp)
-          for (int qq = pp + 1; qq < k; ++qq)
-            if (!is_corr(pp, qq)) pg.pq[pg.npairs++] = (uint16_t)(pp | (qq << 8));
-        pg.corr0 = pg.npairs;
-        pg.pq[pg.npairs++] = (uint16_t)(0 | ((k - 1) << 8) | KMG_PL_OUTER_Q);  // r = 0
-        for (int r = 1; r < k; ++r) pg.pq[pg.npairs++] = (uint16_t)((r - 1) | (r << 8));
-        const int64_t nrec = pg.nrec();
-        const int64_t nlines = pl_lines_bound(pg, n * g.pmax);
-        if (nlines * 128 >= 0xFFFFFFF0LL || nlines >= (1LL << 28))
-          return fail(KMG_EUNSUPPORTED, "pair-lines table too large for 32-bit offsets");
-        KMG_TRY(c->pr_summary.ensure(sizeof(uint32_t) * 8 * (size_t)nrec));
-        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
-        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
-        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nrec + 1)));
-        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nrec)));
-        KMG_TRY(c->pr_lines.ensure((size_t)nlines * 128));
-        KMG_TRY(c->pr_big.ensure(sizeof(uint32_t) * (size_t)(pl_pack_blocks(pg) + 1)));
+        const int64_t nbins = g.nbins();
+        const int64_t bound = nb_list_entries_bound(k, n * (int64_t)g.pmax, nbins);
+        if (bound / 8 + nbins >= 0xFFFFFFF0LL)
+          return fail(KMG_EUNSUPPORTED, "neighbourhood lists: more than 2^32 pieces");
+        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
+        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nbins)));
+        KMG_TRY(c->nb_seg.ensure(sizeof(uint2) * (size_t)nbins));
+        KMG_TRY(c->nb_use.ensure(sizeof(uint2) * (size_t)nbins));
+        KMG_TRY(c->nb_lines.ensure(sizeof(uint16_t) * (size_t)(bound + 8)));
         {
-          StageTimer t(c, ST_SLOTS);
-          KMG_HIP(launch_pl_count(pg, c->off.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
-                                  c->pr_rtot.as<uint32_t>(), c->stream));
-          KMG_HIP(launch_scan(c->pr_rtot.as<uint32_t>(), c->pr_rbase.as<uint32_t>(),
-                              c->pr_cursor.as<uint32_t>(), nrec, c->partials.as<uint32_t>(),
-                              c->stream));
-          KMG_HIP(launch_pl_pack(pg, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
-                                 c->pr_rbase.as<uint32_t>(), c->pr_summary.as<uint32_t>(),
-                                 c->pr_lines.as<uint4>(), c->pr_big.as<uint32_t>(), c->stream));
+          StageTimer t(c, ST_LISTS);  // list sizes and starts
+          KMG_HIP(launch_nb_count(g, c->off.as<uint32_t>(), c->pr_rtot.as<uint32_t>(),
+                                  c->pr_rbase.as<uint32_t>(), c->pr_cursor.as<uint32_t>(),
+                                  c->nb_seg.as<uint2>(), c->partials.as<uint32_t>(), c->stream));
+        }
+        {
+          StageTimer t(c, ST_NBFILL);  // the lists themselves
+          const hipError_t e = launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+                                              c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
+                                              c->nb_use.as<uint2>(), c->nb_lines.as<uint16_t>(),
+                                              c->stream,
+                                              c->tune.nb_fill != 0 ? c->tune.nb_fill : sorted ? 0 : 5);
+          if (e == hipErrorInvalidValue && c->tune.nb_fill == 1)
+            return fail(KMG_EUNSUPPORTED, "KMG_NB_FILL=1: no sorted fill at k=%d, chunk %d", k, g.chunk);
+          KMG_HIP(e);
         }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));
@@ -1200,68 +1140,10 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           }
         }
         KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-          return launch_gram_mismatch1_pl(pg, g, pkd, c->pr_summary.as<uint32_t>(),
-                                          c->pr_lines.as<uint4>(), nlines, c->off.as<uint32_t>(),
-                                          c->ent.as<uint16_t>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, 4, c->tune.pl_dbg, plt);
-        }, true));
-        return mirror();
-      }
-      if (use_nb) {
-        // exact k-mer index over the mismatch window (kernels.py:171), then every (chunk,
-        // k-mer)'s neighbourhood list assembled from it (kmg_nbhd.hip)
-        g.copies = 1;
-        g.nkeys = (uint32_t)pow4(k);
-        const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
-        const bool a16 = c->tune.nb_acc16 != 0;
-        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, a16));
-        o.tri = tri_esz > 0 && g.nchunks > 1;
-        note_plan(nbt);
-        KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
-        const int64_t nbins = g.nbins();
-        const int64_t bound = nb_list_entries_bound(k, n * (int64_t)g.pmax, nbins);
-        if (bound / 8 + nbins >= 0xFFFFFFF0LL)
-          return fail(KMG_EUNSUPPORTED, "neighbourhood lists: more than 2^32 pieces");
-        KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
-        KMG_TRY(c->pr_rbase.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
-        KMG_TRY(c->pr_cursor.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
-        KMG_TRY(c->partials.ensure(sizeof(uint32_t) * scan_partials_words(nbins)));
-        KMG_TRY(c->nb_seg.ensure(sizeof(uint2) * (size_t)nbins));
-        KMG_TRY(c->nb_lines.ensure(sizeof(uint16_t) * (size_t)(bound + 8)));
-        {
-          StageTimer t(c, ST_LISTS);  // list sizes and starts
-          KMG_HIP(launch_nb_count(g, c->off.as<uint32_t>(), c->pr_rtot.as<uint32_t>(),
-                                  c->pr_rbase.as<uint32_t>(), c->pr_cursor.as<uint32_t>(),
-                                  c->nb_seg.as<uint2>(), c->partials.as<uint32_t>(), c->stream));
-        }
-        {
-          StageTimer t(c, ST_SLOTS);  // the lists themselves
-          KMG_HIP(launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
-                                 c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
-                                 c->nb_lines.as<uint16_t>(), c->stream, c->tune.nb_fill,
-                                 c->tune.nb_cap));
-        }
-        if (p->normalize || dt == KMG_U8 || a16) {  // (8-bit slabs: the unpack's K_ii)
-          KMG_TRY(upload_wtab(c, w));
-          KMG_TRY(diag_hamming(c, g, pkd));
-          if (p->normalize) {
-            o.normalize = 1;
-            o.diagv = c->diagv.as<double>();
-            o.dsq = c->dsq.as<double>();
-          }
-        }
-        if (a16) {
-          KMG_TRY(c->nb_dmax.ensure(sizeof(double) * (size_t)g.nchunks));
-          KMG_HIP(launch_chunk_dmax(c->diagv.as<double>(), n, g.chunk, g.nchunks,
-                                    c->nb_dmax.as<double>(), c->stream));
-        }
-        KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
-                                          c->nb_lines.as<uint4>(), r0, r1, (int)w[0], (int)w[1],
-                                          (int)w[2], oq, c->stream, nbt,
-                                          c->tune.nb_unroll ? c->tune.nb_unroll : (o.tri ? 4 : 8),
-                                          a16 ? c->diagv.as<double>() : nullptr,
-                                          a16 ? c->nb_dmax.as<double>() : nullptr);
+                                          c->nb_use.as<uint2>(), c->nb_lines.as<uint4>(), r0, r1,
+                                          (int)w[0], (int)w[1], (int)w[2], oq, c->stream, nbt,
+                                          c->tune.nb_unroll ? c->tune.nb_unroll : (o.tri ? 4 : 8));
         }, true));
         return mirror();
       }
@@ -1533,12 +1415,12 @@ int kmg_destroy(kmg_ctx *c) {
   DevBuf *bufs[] = {&c->kmers, &c->partials, &c->tmp, &c->esc, &c->esc_all, &c->esc_cnt,
                     &c->off,   &c->ent,    &c->diagv, &c->dsq,     &c->wtab,     &c->h_codes,
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
-                    &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines, &c->pr_big,
+                    &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
                     &c->gcoef, &c->feat32, &c->k32, &c->ft_cols,
-                    &c->nb_seg, &c->nb_lines};
+                    &c->nb_seg, &c->nb_use, &c->nb_lines};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -1592,9 +1474,11 @@ int kmg_gram(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_
   return KMG_OK;
 }
 
-int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
-                 int64_t n, int64_t ldc, const uint32_t *cols, int64_t ncols, double *out,
-                 int64_t ld_out) {
+// kmg_features (cols: uint32 base-4 codes) and kmg_features_sym (cols: 16 symbol bytes each;
+// flags bit 0: numpy's broadcast of short k-mers, get_phi_km on rows shorter than the window)
+static int features_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                         int64_t n, int64_t ldc, const void *cols, bool sym, int32_t flags,
+                         int64_t ncols, double *out, int64_t ld_out) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   if (!p) return fail(KMG_EINVAL, "params is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1603,6 +1487,7 @@ int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const in
   if (!codes || !lens || !cols || !out) return fail(KMG_EINVAL, "NULL buffer");
   if (ld_out < ncols) return fail(KMG_EINVAL, "ld_out < ncols");
   int k = p->k, m = 0, window = 0, binary = 0;
+  const int bcast = sym && (flags & KMG_FEATURES_BCAST) ? 1 : 0;
   switch (p->kind) {
     case KMG_SPECTRUM: break;  // get_phi_u: windows range(len(x) - k + 1)
     case KMG_MISMATCH:         // get_phi_km: windows range(101 - k + 1)
@@ -1611,6 +1496,7 @@ int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const in
       if (m < 0) return fail(KMG_EINVAL, "m < 0");
       break;
     case KMG_GAPPY:  // gappy_k (k = 1, g = 0): letters of x[0:101]
+      if (sym) return fail(KMG_EUNSUPPORTED, "symbol columns: spectrum or mismatch only");
       if (!(p->k == 1 && p->g == 0)) return fail(KMG_EUNSUPPORTED, "gappy features: k=1, g=0 only");
       window = p->window > 0 ? p->window : 101;
       binary = 1;
@@ -1621,8 +1507,19 @@ int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const in
   if (k < 1 || k > 16) return fail(KMG_EUNSUPPORTED, "features: 1 <= k <= 16 (k = %d)", k);
   for (int64_t i = 0; i < n; ++i) {
     if (lens[i] < 0 || lens[i] > ldc) return fail(KMG_EINVAL, "lens[%lld] outside [0,ldc]", (long long)i);
-    if (p->kind == KMG_MISMATCH && lens[i] < window)
+    if (p->kind == KMG_MISMATCH && lens[i] < window && !bcast)
       return fail(KMG_EINVAL, "mismatch features need sequences of length >= %d", window);
+    if (bcast && p->kind == KMG_MISMATCH && lens[i] < window) {
+      // windows of ln = min(k, len - a) symbols, a < window - k + 1: numpy broadcasts ln = 1
+      // (and ln = 0 against a 1-letter beta); any other short window raises in the reference
+      const int first_short = std::max(0, (int)lens[i] - k + 1);
+      for (int a2 = first_short; a2 < window - k + 1; ++a2) {
+        const int ln = std::max(0, std::min(k, (int)lens[i] - a2));
+        if (ln != k && ln != 1 && !(ln == 0 && k == 1))
+          return fail(KMG_EINVAL, "features: a %d-symbol window of row %lld does not broadcast "
+                      "against a %d-mer", ln, (long long)i, k);
+      }
+    }
     if ((window > 0 ? std::min<int64_t>(window, lens[i]) : lens[i]) - k + 1 > KMG_FEAT_MAXW)
       return fail(KMG_EUNSUPPORTED, "features: more than %d windows per sequence", KMG_FEAT_MAXW);
   }
@@ -1631,19 +1528,24 @@ int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const in
   const int64_t slab = std::max<int64_t>(1, std::min<int64_t>({n, 65535, (1LL << 27) / ncols}));
   KMG_TRY(c->h_codes.ensure((size_t)n * std::max<int64_t>(1, ldc)));
   KMG_TRY(c->h_lens.ensure(sizeof(int32_t) * (size_t)n));
-  KMG_TRY(c->ft_cols.ensure(sizeof(uint32_t) * (size_t)ncols));
+  const size_t csz = sym ? 16 : sizeof(uint32_t);
+  KMG_TRY(c->ft_cols.ensure(csz * (size_t)ncols));
   KMG_TRY(c->h_out.ensure(sizeof(double) * (size_t)slab * ncols));
   KMG_HIP(hipMemcpyAsync(c->h_codes.p, codes, (size_t)n * ldc, hipMemcpyHostToDevice, c->stream));
   KMG_HIP(hipMemcpyAsync(c->h_lens.p, lens, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
-  KMG_HIP(hipMemcpyAsync(c->ft_cols.p, cols, sizeof(uint32_t) * ncols, hipMemcpyHostToDevice,
-                         c->stream));
+  KMG_HIP(hipMemcpyAsync(c->ft_cols.p, cols, csz * ncols, hipMemcpyHostToDevice, c->stream));
   for (int64_t r0 = 0; r0 < n; r0 += slab) {
     const int64_t rows = std::min(slab, n - r0);
     {
       StageTimer t(c, ST_FEATURES);
-      KMG_HIP(launch_features(c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), ldc, r0, rows, k,
-                              m, window, binary, c->ft_cols.as<uint32_t>(), ncols,
-                              c->h_out.as<double>(), ncols, c->stream));
+      if (sym)
+        KMG_HIP(launch_features_sym(c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), ldc, r0, rows,
+                                    k, m, window, bcast, c->ft_cols.as<uint4>(), ncols,
+                                    c->h_out.as<double>(), ncols, c->stream));
+      else
+        KMG_HIP(launch_features(c->h_codes.as<uint8_t>(), c->h_lens.as<int32_t>(), ldc, r0, rows, k,
+                                m, window, binary, c->ft_cols.as<uint32_t>(), ncols,
+                                c->h_out.as<double>(), ncols, c->stream));
     }
     KMG_HIP(hipMemcpy2DAsync(out + (size_t)r0 * ld_out, (size_t)ld_out * sizeof(double), c->h_out.p,
                              (size_t)ncols * sizeof(double), (size_t)ncols * sizeof(double),
@@ -1653,6 +1555,18 @@ int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const in
   }
   KMG_HIP(hipStreamSynchronize(c->stream));
   return KMG_OK;
+}
+
+int kmg_features(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                 int64_t n, int64_t ldc, const uint32_t *cols, int64_t ncols, double *out,
+                 int64_t ld_out) {
+  return features_impl(c, p, codes, lens, n, ldc, cols, false, 0, ncols, out, ld_out);
+}
+
+int kmg_features_sym(kmg_ctx *c, const kmg_params *p, const uint8_t *codes, const int32_t *lens,
+                     int64_t n, int64_t ldc, const uint8_t *cols, int64_t ncols, int32_t flags,
+                     double *out, int64_t ld_out) {
+  return features_impl(c, p, codes, lens, n, ldc, cols, true, flags, ncols, out, ld_out);
 }
 
 int kmg_gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
@@ -1842,7 +1756,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
     // that is all-gathered after the slabs and patched into K; a full list redoes the
     // build with 16-bit slabs
     if ((path == SM_POSTING && pmax <= 255) || path == SM_SLOTS || path == SM_PAIRS ||
-        path == SM_PL || path == SM_NB) {
+        path == SM_NB) {
       wire = narrow_bits == 8 ? KMG_U8 : KMG_U16;
       check16 = wire == KMG_U8 || path != SM_POSTING;  // spectrum counts <= P^2 < 65536
     } else if (narrow_bits == 8) {
@@ -2140,10 +2054,17 @@ int kmg_stage_ms(kmg_ctx *c, const char *stage, double *ms) {
   return KMG_OK;
 }
 
-int kmg_last_plan(kmg_ctx *c, int32_t plan[5]) {
+int kmg_last_factorisation(kmg_ctx *c, int32_t *kind) {
+  if (!c || !kind) return fail(KMG_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *kind = c->last_factor;
+  return KMG_OK;
+}
+
+int kmg_last_plan(kmg_ctx *c, int32_t plan[6]) {
   if (!c || !plan) return fail(KMG_EINVAL, "NULL argument");
   std::lock_guard<std::mutex> lk(c->mu);
-  for (int q = 0; q < 5; ++q) plan[q] = c->plan[q];
+  for (int q = 0; q < 6; ++q) plan[q] = c->plan[q];
   return KMG_OK;
 }
 
@@ -2373,6 +2294,7 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs, bool as
   rocblas_int hinfo = 0;
   KMG_TRY(build());
   if (asym) {
+    c->last_factor = KMG_FACTOR_LU_ASYMMETRIC;
     KMG_BLAS(rocsolver_dgetrf(c->blas, ni, ni, B, ni, ipiv, info));
     KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
     KMG_HIP(hipStreamSynchronize(c->stream));
@@ -2387,9 +2309,11 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs, bool as
   KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
   if (hinfo == 0) {
+    c->last_factor = KMG_FACTOR_CHOLESKY;
     KMG_BLAS(rocsolver_dpotrs(c->blas, fill, ni, 1, B, ni, rhs, ni));
     return KMG_OK;
   }
+  c->last_factor = KMG_FACTOR_LU_INDEFINITE;
   KMG_TRY(build());  // not positive definite: rebuild and use LU, like inv()
   KMG_BLAS(rocsolver_dgetrf(c->blas, ni, ni, B, ni, ipiv, info));
   KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));

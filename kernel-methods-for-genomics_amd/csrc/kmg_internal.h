@@ -120,8 +120,7 @@ struct PairGeom {
   int nchunks;
   int chunk;
   uint32_t nkeys2;                 // 4^(k-2)
-  uint16_t pq[KMG_PAIRS_MAX];      // p | q << 8 (pair lines: | KMG_PL_OUTER_Q, see below)
-  int corr0 = 0;                   // pair lines: first correction pair (kmg_pairs.hip)
+  uint16_t pq[KMG_PAIRS_MAX];      // p | q << 8
   __host__ __device__ int64_t ngroups() const { return (int64_t)npairs * nchunks * nkeys2; }
   __host__ __device__ int64_t nrec() const { return (ngroups() + 31) / 32; }
 };
@@ -156,33 +155,6 @@ inline int64_t pair_lines_bound(const PairGeom &pg, int64_t occurrences) {
   const int64_t entries = (int64_t)pg.npairs * occurrences;
   const int64_t nonempty = pg.ngroups() < entries ? pg.ngroups() : entries;
   return nonempty + nonempty / 8 + 2 * entries / 128 + 64;
-}
-
-// ---------------------------------------------------------------- pair lines (kmg_pairs.hip)
-// Drop-two table, second layout.  Pairs are ordered "uniform" first, then the k
-// correction pairs (index corr0 + r for r = 0..k-1): pair {r-1, r} with outer letter r-1
-// (r >= 1) and pair {0, k-1} with outer letter k-1 (r = 0, flag KMG_PL_OUTER_Q).
-//   uniform group: n uint16 columns, no header, padded to nl = ceil(n / 64) lines with
-//     dummy columns (64 LDS words past the accumulator); every entry weighs w2.
-//   correction group: 16-byte header of sub-bin ends (bytes, sub-bin = z_outer * 4 +
-//     z_inner), then the entries in sub-bin order, nl = ceil((8 + n) / 64) lines.
-// Summary record per 32 groups (8 dwords): w0 base line, w1..w4 4-bit line counts,
-// w5 "wide" bits (group too large for lines: read from the exact index instead).
-#define KMG_PL_OUTER_Q 0x80
-#define KMG_PL_MAXNL 14
-#define KMG_PL_WAVE_WORDS 1024  // LDS words of one wave's line ring (gram_pl_kernel)
-hipError_t launch_pl_count(const PairGeom &pg, const uint32_t *xoff, uint32_t *summary,
-                           uint32_t *rtot, hipStream_t s);
-hipError_t launch_pl_pack(const PairGeom &pg, const uint32_t *xoff, const uint16_t *xent,
-                          const uint32_t *rbase, uint32_t *summary, uint4 *lines, uint32_t *big,
-                          hipStream_t s);
-// pl_pack's list of blocks holding groups of more than 4 lines: 1 + this many words
-inline int64_t pl_pack_blocks(const PairGeom &pg) { return (pg.ngroups() + 15) / 16; }
-// upper bound of the line count of the pair-lines table
-inline int64_t pl_lines_bound(const PairGeom &pg, int64_t occurrences) {
-  const int64_t entries = (int64_t)pg.npairs * occurrences;
-  const int64_t nonempty = pg.ngroups() < entries ? pg.ngroups() : entries;
-  return nonempty + entries / 64 + 65;  // + the dummy line 0
 }
 
 // ---------------------------------------------------------------- Gram kernels
@@ -261,35 +233,31 @@ hipError_t launch_gram_mismatch1_pairs(const PairGeom &pg, const IndexGeom &g, c
                                        int64_t nlines, const uint32_t *xoff, const uint16_t *xent,
                                        int64_t row0, int64_t row1, int w0, int w1, int w2,
                                        const OutSpec &o, hipStream_t s);
-// mismatch (k, 1), 3 <= k <= 12, on the pair-lines table; xoff / xent = exact index
-hipError_t launch_gram_mismatch1_pl(const PairGeom &pg, const IndexGeom &g, const Packed &pk,
-                                    const uint32_t *summary, const uint4 *lines, int64_t nlines,
-                                    const uint32_t *xoff, const uint16_t *xent, int64_t row0,
-                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int depth = 4, int dbg = 0,
-                                    int threads = 1024);
-// mismatch (k, 1), 3 <= k <= 12, through neighbourhood lists (kmg_nbhd.hip): from the exact
+// mismatch (k, 1), 4 <= k <= 12, through neighbourhood lists (kmg_nbhd.hip): from the exact
 // index (xoff / xent over [chunk][4^k]) every (chunk, k-mer)'s list of the column windows at
-// Hamming distance 0 | 1 | 2 (uint16 columns, 3 segments padded to 8); hist / nboff / cursor
-// nbins + 1 words, nbseg nbins, table nb_list_entries_bound(...) uint16
+// Hamming distance 0 | 1 | 2 (3 segments; segment 2 packed where the sorted fill runs);
+// hist / nboff / cursor nbins + 1 words, nbseg / nbuse nbins, table
+// nb_list_entries_bound(...) uint16
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins);
-size_t nb_gram_lds(const IndexGeom &g, const Packed &pk, bool a16);
-hipError_t launch_chunk_dmax(const double *kdiag, int64_t n, int chunk, int nchunks, double *dmax,
-                             hipStream_t s);
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk);
+// entries of segment 2 the sorted fill's per-wave LDS buffer holds at this chunk (0: the
+// lists stay 16-bit: k too sparse to pack, or the buffer below 1.25x the mean segment), and
+// the largest chunk it runs at (0: none)
+int nb_sorted_cap(int k, int pmax, int chunk);
+int nb_sorted_max_chunk(int k, int pmax);
 hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
                            uint32_t *nboff, uint32_t *cursor, uint2 *nbseg, uint32_t *partials,
                            hipStream_t s);
-// form: 0 auto (grouped, S = 2, 2-byte stores), 1 per-list fill, 2 grouped S = 1, 3 / 4 / 5
-// grouped S = 2 with 2- / 4- / 8-byte stores, 6 range-major grouped fill; cap_override:
-// entries of the grouped fill's LDS range image (-1 auto = none)
+// form: 0 auto (sorted where nb_sorted_cap > 0, else 16-bit lists), 1 sorted, 2 grouped,
+// 3 pieces, 4 staged, 5 auto 16-bit (staged where a typical list fits its per-wave LDS
+// buffer, else the piece-assembled fill past 8.5 occurrences a k-mer and chunk, else grouped)
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
-                          const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
-                          hipStream_t s, int form = 0, int cap_override = -1);
+                          const uint32_t *nboff, const uint2 *nbseg, uint2 *nbuse,
+                          uint16_t *table, hipStream_t s, int form = 0);
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
-                                    const uint2 *nbseg, const uint4 *table, int64_t row0,
-                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads, int unroll = 4,
-                                    const double *kdiag = nullptr, const double *kdmax = nullptr);
+                                    const uint2 *nbseg, const uint2 *nbuse, const uint4 *table,
+                                    int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                    const OutSpec &o, hipStream_t s, int threads, int unroll = 8);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
@@ -346,6 +314,9 @@ hipError_t launch_fill(const OutSpec &o, int64_t rows, int64_t cols, double valu
 // per-sequence feature vectors over caller-chosen k-mer columns (kmg_features.hip):
 // out[r][j] for sequences row0 + r, r < rows; window 0 = every window of the row
 #define KMG_FEAT_MAXW 4096
+hipError_t launch_features_sym(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t row0,
+                               int64_t rows, int k, int m, int window, int bcast, const uint4 *cols,
+                               int64_t ncols, double *out, int64_t ld, hipStream_t s);
 hipError_t launch_features(const uint8_t *codes, const int32_t *lens, int64_t ldc, int64_t row0,
                            int64_t rows, int k, int m, int window, int binary,
                            const uint32_t *cols, int64_t ncols, double *out, int64_t ld,

@@ -3,74 +3,56 @@
 // get_mismatch_K (kernels.py:196-217) reduces to the closed form
 //   K(x, y) = sum_{a, b} w[ham(x_a, y_b)],  w = (1 + 3k, 4, 2) for m = 1
 // (kmgram.params.mismatch_weights), i.e. for row i's window k-mer u every column window at
-// Hamming distance <= 2 of u adds w[ham] to its column.  The drop-one slot table and the
-// drop-two pair lines (kmg_gram.hip, kmg_pairs.hip) read those column windows as many
-// short posting groups (117 or 36 random 128-byte lines a window and chunk, 1.6-2x the
-// entries a window needs: a Hamming-1 neighbour sits in k - 1 pair groups, Hamming 0 in all
-// of them).  This formulation materialises, once per build, for every (column chunk c,
-// k-mer u) the NEIGHBOURHOOD LIST of u:
+// Hamming distance <= 2 of u adds w[ham] to its column.  This formulation materialises, once
+// per build, for every (column chunk c, k-mer u) the NEIGHBOURHOOD LIST of u:
 //
 //   [ occurrences of u | of its 3k Hamming-1 neighbours | of its 9 k(k-1)/2 Hamming-2 ]
 //
-// as uint16 columns inside the chunk, each of the three segments padded to whole 16-byte
-// pieces (8 columns) with dummy columns (LDS words past the accumulator).  Every column
-// window then appears exactly once per list, and a row window reads ONE contiguous list
-// (N=200000, k=9: ~25000 entries, 50 KB over all chunks) instead of 117 random lines per
-// chunk: the Gram kernel streams HBM, 16 bytes a lane, 1 KB per wave instruction.
+// as columns inside the chunk, so that a row window reads ONE contiguous list (N=200000,
+// k=9: ~25000 entries over all chunks) and the Gram kernel streams HBM, 16 bytes a lane.
+//
+// List layout (in 16-byte pieces; nboff = list start, nbseg = (end of segment 0, end of
+// segment 1), nbuse = (16-bit pieces, packed pieces), written by the fill):
+//   [0, s0)            segment 0 as uint16 columns, 8 a piece (dummy columns pad the tail)
+//   [s0, s1)           segment 1, the same
+//   [s1, n16)          16-bit part of segment 2: the entries the packing left over
+//   [n16, n16 + np)    PACKED part of segment 2: a piece = one uint16 column c (the minimum
+//                      of its 15 columns) + 14 bytes o_1..o_14, columns c + o_t.  The sorted
+//                      fill counting-sorts the segment by column >> 6 and cuts it into runs of
+//                      15; a run spanning <= 254 columns becomes a packed piece, any other (and
+//                      the last n2 mod 15 entries) go to the 16-bit part.
+// Segment 2 holds ~93 % of a list's entries (k = 9), at ~0.115 entries a column of the chunk:
+// 15 of them span ~122 columns, 0.5 % of the runs exceed 254 (1.078 B an entry against 2).
+// A list whose segment 2 exceeds the fill's LDS sort buffer, or a k too sparse to pack
+// (k >= 10: ~28 columns between entries), keeps the whole segment as 16-bit pieces
+// (n16 = list size, np = 0).
 //
 //   nb_count_kernel   per (c, u): n0, n1, n2 from the exact index (1 + 3k + 9k(k-1)/2
-//                     lookups of its bin offsets, L2-resident) -> pieces and segment ends
+//                     lookups of its bin offsets, L2-resident) -> 16-bit pieces and segment ends
 //   launch_scan       list starts (in pieces; < 2^32: checked by the host)
 //   list fills        (launch_nb_fill picks one)
-//     nb_fill_grouped_kernel  default: one workgroup per 16 k-mers sharing a (k-2)-letter
-//                     prefix, the 211 prefix ranges' sub-bin offsets in LDS; one wave a list:
-//                     DPP prefix sum of its 352 runs, lane-per-run copies from the index
-//     nb_fill_pieces_kernel   past 8.5 occurrences a k-mer and chunk: the ranges as an LDS
-//                     image (16-byte loads), each list assembled 16 bytes a lane from it
-//     nb_fill_kernel, nb_fill_ranges_kernel   the per-list and range-major forms (measured
-//                     slower; KMG_NB_FILL 1 / 6)
+//     nb_fill_sorted_kernel   default where segment 2 packs: one workgroup per 16 k-mers
+//                     sharing a (k-2)-letter prefix, one wave a list: segments 0 / 1 copied
+//                     into the table, segment 2 counting-sorted by column >> 6 in a per-wave
+//                     LDS buffer, then packed 15 entries a lane
+//     nb_fill_grouped_kernel  16-bit lists (k >= 10): the same groups, lane-per-run copies
+//     nb_fill_pieces_kernel   16-bit lists past 8.5 occurrences a k-mer and chunk: the
+//                     ranges as an LDS image (16-byte loads), each list assembled 16 B a lane
 //   gram_nb_kernel   per (row i, chunk c): row windows -> (list start, pieces, segment
-//                     ends) in LDS, a prefix sum over the row's lists, then every wave streams
-//                     an equal share of the row's pieces (four 16-byte loads in flight per
-//                     lane), adding the segment's weight for each of the 8 columns of a piece
-//                     into the LDS accumulator; fused normalize_K epilogue (emit_row).
+//                     ends) in LDS, prefix sums over the row's 16-bit and packed pieces, then
+//                     every wave streams an equal share of each, 16 bytes a lane, adding the
+//                     segment's weight for each column of a piece into the LDS accumulator;
+//                     fused normalize_K epilogue (emit_row).
 //
-// Roofline: the lists are read from HBM once per (row, chunk) -- 2 B per (row window,
-// neighbour occurrence): N=20000 ~466 KB a row against the 160 KB float64 K row; the bound is
-// HBM (table reads + K writes), not the Infinity-Cache line rate of the table formulations.
+// Roofline: the lists are read from HBM once per (row, chunk): N=20000 ~270 KB a row (packed;
+// 466 KB as 16-bit lists) against the 160 KB float64 K row; the bound is HBM (list reads +
+// K writes) beside the LDS adds (one ds_add per entry).
 #include "kmg_rowacc.h"
 
 namespace kmg {
 
 namespace {
-constexpr int NB_FILL_THREADS = 256;
-
 __device__ __forceinline__ int nb_neighbours(int k) { return 1 + 3 * k + 9 * k * (k - 1) / 2; }
-
-// neighbour t of u (t < nb_neighbours(k)) and its segment: t = 0 u itself; then the 3k
-// Hamming-1 k-mers (position p, letter xor d = 1..3); then the Hamming-2 k-mers of the pairs
-// p < q in order (0,1), (0,2), (1,2), (0,3), ... (q-major), 9 letter xors each
-__device__ __forceinline__ uint32_t nb_neighbour(uint32_t u, int k, int t, int &seg) {
-  if (t == 0) {
-    seg = 0;
-    return u;
-  }
-  t -= 1;
-  if (t < 3 * k) {
-    seg = 1;
-    const int p = t / 3, d = t - 3 * p + 1;
-    return u ^ ((uint32_t)d << (2 * (k - 1 - p)));
-  }
-  seg = 2;
-  t -= 3 * k;
-  const int pi = t / 9, r = t - 9 * pi;
-  int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);  // pi = q(q-1)/2 + p
-  while (q * (q - 1) / 2 > pi) --q;
-  while ((q + 1) * q / 2 <= pi) ++q;
-  const int p = pi - q * (q - 1) / 2;
-  const int d1 = r / 3 + 1, d2 = r - 3 * (r / 3) + 1;
-  return u ^ ((uint32_t)d1 << (2 * (k - 1 - p))) ^ ((uint32_t)d2 << (2 * (k - 1 - q)));
-}
 
 // the same inclusive wave scan on DPP row shifts and row broadcasts (VALU only, no LDS
 // permutes): Hillis-Steele inside each 16-lane row, then lane 15 into row 1 (and 47 into row
@@ -86,18 +68,23 @@ __device__ __forceinline__ uint32_t nb_wave_incl_scan_dpp(uint32_t v) {
   return (uint32_t)x;
 }
 
-__device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
-  return v;
+// LDS written by some lanes of the wave, read by others next: compiler and memory order at
+// wave scope (a wave's LDS instructions execute in order)
+__device__ __forceinline__ void nb_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// dummy column of list position pp: NB_DUMMIES LDS words past the accumulator, spread by
+// position (16: the Gram kernel's LDS is counted to the word, two workgroups a CU)
+constexpr int NB_DUMMIES = 16;
+__device__ __forceinline__ uint16_t nb_dummy(uint32_t pad_col, uint32_t pp) {
+  return (uint16_t)(pad_col + (pp & (uint32_t)(NB_DUMMIES - 1)));
 }
 }  // namespace
 
-// per (chunk, k-mer): pieces of its neighbourhood list and the segment ends (in pieces)
+// per (chunk, k-mer): 16-bit pieces of its neighbourhood list and the segment ends (pieces)
 __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
                                                        const uint32_t *__restrict__ xoff,
                                                        uint32_t *__restrict__ hist,
@@ -127,131 +114,14 @@ __global__ __launch_bounds__(256) void nb_count_kernel(int k, int64_t nbins,
   seg[b] = make_uint2(p0, p0 + p1);
 }
 
-// One WAVE per (chunk, k-mer) bin, four waves a workgroup, grid-stride over the bins.
-//  1. lane l owns the neighbours t in [l R, l R + R) (R = ceil(nb / 64)): their posting
-//     ranges (all loads issued before any is used), a wave prefix sum gives each run's start
-//     in the unpadded concatenation; starts and sources go to the wave's LDS tables;
-//  2. the runs are copied by groups of LG lanes, one run a group (LG ~ the mean run length:
-//     chunk x P / 4^k occurrences of a k-mer, 7 at N=20000 and k = 9), 64 / LG runs a step
-//     and NB_STEPS steps' loads in flight; the runs of a step are consecutive in the list, so
-//     a wave's 2-byte stores land on ~128 contiguous bytes.
-// (Round 4's first forms -- a workgroup per bin with one dependent load per copied entry,
-// and an entry-parallel copy through an LDS run map, ~60 VALU per entry -- took 1.7-3.0 ms
-// per 262144 bins at N=20000.)
-constexpr int NB_MAXR = 10;    // neighbours a lane in step 1: ceil(631 / 64) at k = 12
-constexpr int NB_MAXN = 640;   // neighbour tables per wave (631 at k = 12, + the end)
-constexpr int NB_STEPS = 8;
-
-template <int LG>
-__global__ __launch_bounds__(NB_FILL_THREADS) void nb_fill_kernel(
-    int k, int64_t nbins, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
-    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
-    uint32_t pad_col) {
-  constexpr int G = 64 / LG;  // runs a step
-  __shared__ uint32_t npre_all[NB_FILL_THREADS / 64][NB_MAXN];
-  __shared__ uint32_t nsrc_all[NB_FILL_THREADS / 64][NB_MAXN];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int grp = lane / LG, gl = lane % LG;
-  uint32_t *npre = npre_all[wave];
-  uint32_t *nsrc = nsrc_all[wave];
-  const uint32_t nkeys = 1u << (2 * k);
-  const int nbn = nb_neighbours(k);
-  const int R = (nbn + 63) >> 6;
-  const int t0 = lane * R;
-  const int t2 = 1 + 3 * k;  // first Hamming-2 neighbour
-  const int64_t wstride = (int64_t)gridDim.x * (NB_FILL_THREADS / 64);
-  for (int64_t b = (int64_t)blockIdx.x * (NB_FILL_THREADS / 64) + wave; b < nbins; b += wstride) {
-    const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
-    if (tot == 0) continue;  // wave-uniform
-    const uint32_t u = (uint32_t)b & (nkeys - 1u);
-    const uint32_t *off = xoff + (b - u);
-    const uint2 sg = nbseg[b];
-    uint32_t src[NB_MAXR], cnt[NB_MAXR];
-#pragma unroll
-    for (int j = 0; j < NB_MAXR; ++j) {
-      cnt[j] = 0;
-      src[j] = 0;
-      if (j < R && t0 + j < nbn) {
-        int sgm;
-        const uint32_t v = nb_neighbour(u, k, t0 + j, sgm);
-        src[j] = off[v];
-        cnt[j] = off[v + 1] - src[j];
-      }
-    }
-    uint32_t s = 0;
-#pragma unroll
-    for (int j = 0; j < NB_MAXR; ++j) s += cnt[j];
-    const uint32_t inc = nb_wave_incl_scan(s);
-    const uint32_t total = __shfl(inc, 63, 64);
-    {
-      uint32_t r = inc - s;
-#pragma unroll
-      for (int j = 0; j < NB_MAXR; ++j) {
-        if (j < R && t0 + j < nbn) {
-          npre[t0 + j] = r;
-          nsrc[t0 + j] = src[j];
-        }
-        r += cnt[j];
-      }
-    }
-    if (lane == 0) npre[nbn] = total;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const uint32_t n0 = npre[1];
-    const uint32_t pre2 = t2 < nbn ? npre[t2] : total;
-    uint16_t *dst = table + (size_t)start * 8u;
-    // (segment base - unpadded segment start) per segment
-    const uint32_t dlt0 = 0u, dlt1 = sg.x * 8u - n0, dlt2 = sg.y * 8u - pre2;
-    for (int t00 = 0; t00 < nbn; t00 += G * NB_STEPS) {
-      uint32_t sa[NB_STEPS], pa[NB_STEPS], ca[NB_STEPS];
-#pragma unroll
-      for (int q = 0; q < NB_STEPS; ++q) {
-        const int t = t00 + q * G + grp;
-        ca[q] = 0;
-        if (t < nbn) {
-          const uint32_t p0 = npre[t];
-          ca[q] = npre[t + 1] - p0;
-          sa[q] = nsrc[t];
-          pa[q] = p0 + (t == 0 ? dlt0 : t < t2 ? dlt1 : dlt2);
-        }
-      }
-      // first LG entries of every run of the steps: loads first, then the stores
-      uint16_t v[NB_STEPS];
-#pragma unroll
-      for (int q = 0; q < NB_STEPS; ++q)
-        if ((uint32_t)gl < ca[q]) v[q] = xent[sa[q] + gl];
-#pragma unroll
-      for (int q = 0; q < NB_STEPS; ++q)
-        if ((uint32_t)gl < ca[q]) dst[pa[q] + gl] = v[q];
-      // runs longer than LG (rare at the chosen LG)
-#pragma unroll
-      for (int q = 0; q < NB_STEPS; ++q)
-        for (uint32_t e = LG + gl; e < ca[q]; e += LG) dst[pa[q] + e] = xent[sa[q] + e];
-    }
-    // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
-    if (lane < 24) {
-      const int sgi = lane >> 3, e = lane & 7;
-      const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
-      const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
-      const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
-      const uint32_t pos = segb + segn + (uint32_t)e;
-      if (pos < segend) dst[pos] = (uint16_t)(pad_col + (pos & 63u));
-    }
-    __builtin_amdgcn_wave_barrier();  // the next bin overwrites the tables
-  }
-}
-
-// ------------------------------------------------------------------ grouped list fill
+// ------------------------------------------------------------------ group tables
 // The lists of the 4^S k-mers u = (prefix P, suffix s_u) that share their first k - S letters
 // are built together by one workgroup.  Every Hamming <= 2 neighbour of such a u is
 // (prefix w, suffix s) with ham(w, P) + ham(s, s_u) <= 2, and the 4^S bins of one prefix w
 // are ADJACENT in the exact index (key order): the workgroup loads the m_S = 1 + 3(k-S) +
-// 9 C(k-S, 2) ranges [w 4^S, (w + 1) 4^S) of bins into LDS once (k = 9, S = 2: 211 ranges of
-// ~113 entries at N=20000), then every wave assembles lists from LDS: 352 runs a list in
-// segment order, a wave prefix sum placing each run, lane-per-run copies LDS -> HBM.  Per
-// list that is ~13 ranges' line requests instead of 352 runs' (the per-list fill above
-// gathered each run from L2 / the Infinity Cache: ~2.5 ms at N=20000).  A group whose ranges
-// overflow the LDS image (repetitive data) copies straight from the index (flat pointer).
+// 9 C(k-S, 2) ranges [w 4^S, (w + 1) 4^S) of bin offsets into LDS once (k = 9, S = 2: 211
+// ranges), then every wave assembles lists: 352 runs a list in segment order, a wave prefix
+// sum placing each run.
 template <int S>
 __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmask, int &h) {
   // run j of a list, segment order: (prefix range r, suffix xor dmask, Hamming class h)
@@ -289,31 +159,10 @@ __device__ __forceinline__ void nb_run_desc(int j, int k, int &r, uint32_t &dmas
   r = 1 + 3 * kp + j; dmask = 0;  // prefix Hamming 2, suffix 0
 }
 
-// copy one run of n uint16 entries to o (any alignment): WS = 1 one 2-byte store an entry;
-// WS = 2 dword stores of entry pairs (o aligned to 4 bytes in the middle); WS = 4 also
-// 8-byte stores of aligned quads
-template <int WS, typename Src>
+// copy one run of n uint16 entries to o (2-byte stores)
+template <typename Src>
 __device__ __forceinline__ void nb_copy_run(uint16_t *o, const Src *src, uint32_t n) {
-  uint32_t e = 0;
-  if constexpr (WS >= 2) {
-    if (n && (((uintptr_t)o) & 2)) {
-      o[0] = src[0];
-      e = 1;
-    }
-    if constexpr (WS >= 4) {
-      if (e + 1 < n && (((uintptr_t)(o + e)) & 4)) {
-        *(uint32_t *)(o + e) = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
-        e += 2;
-      }
-      for (; e + 3 < n; e += 4) {
-        const uint32_t lo = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
-        const uint32_t hi = (uint32_t)src[e + 2] | ((uint32_t)src[e + 3] << 16);
-        *(uint2 *)(o + e) = make_uint2(lo, hi);
-      }
-    }
-    for (; e + 1 < n; e += 2) *(uint32_t *)(o + e) = (uint32_t)src[e] | ((uint32_t)src[e + 1] << 16);
-  }
-  for (; e < n; ++e) o[e] = src[e];
+  for (uint32_t e = 0; e < n; ++e) o[e] = src[e];
 }
 
 // pieces of a list the piece fill assembles in LDS (longer lists: lane-per-run copies)
@@ -389,13 +238,214 @@ __device__ __forceinline__ void nb_load_range_offsets(const uint32_t *__restrict
   }
 }
 
-template <int S, int NT, int WS>
-__global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
+// ------------------------------------------------------------------ lane-per-run list copy
+// One wave builds list b (16-bit pieces, all three segments) of a group whose range offsets
+// are in LDS: the 352 runs in segment order, a wave prefix sum placing each run, lane-per-run
+// 2-byte copies straight from the index (L2 / the Infinity Cache; an LDS range image measured
+// slower, profiles/r04_nb_fill.jsonl r04o), the dummy tail of each segment.
+__device__ __forceinline__ void nb_list_lane_per_run(int k, int su, const uint32_t *rt,
+                                                     const uint32_t *roff, const uint16_t *xent,
+                                                     uint32_t tot, uint2 sg, uint16_t *dst,
+                                                     uint32_t pad_col) {
+  constexpr int SW = 16;
+  const int lane = threadIdx.x & 63;
+  const int nbn = nb_neighbours(k), t2 = 1 + 3 * k;  // (t2 < 64 for k <= 21)
+  uint32_t carry = 0, n0 = 0, pre2 = 0;
+  for (int j0 = 0; j0 < nbn; j0 += 64) {
+    const int j = j0 + lane;
+    uint32_t cnt = 0, srcp = 0, h = 2;
+    if (j < nbn) {
+      const uint32_t d = rt[j];
+      const uint32_t *ro = roff + (d & 0xFFFFu) * (SW + 1);
+      const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
+      h = d >> 24;
+      srcp = ro[sidx];
+      cnt = ro[sidx + 1] - srcp;
+    }
+    const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
+    const uint32_t pos = carry + inc - cnt;
+    if (j0 == 0) {
+      n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
+      pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);
+    }
+    carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
+    nb_copy_run(dst + dpos, xent + srcp, cnt);
+  }
+  const uint32_t total = carry;
+  // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
+  if (lane < 24) {
+    const int sgi = lane >> 3, e = lane & 7;
+    const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
+    const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
+    const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
+    const uint32_t pp = segb + segn + (uint32_t)e;
+    if (pp < segend) dst[pp] = nb_dummy(pad_col, pp);
+  }
+}
+
+// ------------------------------------------------------------------ sorted (packed) fill
+// One 1024-thread workgroup per group of 16 lists (S = 2), one wave a list, the list's
+// segment 2 counting-sorted in a per-wave LDS buffer:
+//  1. the 352 runs in segment order (wave prefix sums, 64 runs a step, lane j run j);
+//     segments 0 and 1 are copied from the exact index into the table (16-bit pieces);
+//     segment 2's runs into the buffer, each entry also counted in a histogram of 64-column
+//     buckets -- a run read as two whole 16-byte pieces of the index (texture-address work
+//     is per load instruction: 2 a lane instead of one per entry) and shifted into place by
+//     register selects;
+//  2. the histogram's exclusive scan -> bucket starts;
+//  3. the buffer into registers (ds_read_b64, 4 entries a lane), then every entry to slot
+//     p + p / 15 of its bucket position p (ds_add_rtn on the bucket start): the segment in
+//     column >> 6 order, as runs of 15 entries in 16-slot (32-byte) rows;
+//  4. nb_pack_seg2: a row of 15 (two ds_read_b128) spanning <= 254 columns becomes a packed
+//     piece, else its entries go to the 16-bit part.
+// ~4.5 LDS operations a segment-2 entry (7 in round 5's first form, 1.8 ms at N=20000).
+// Segment 2 past the buffer (cap2 entries, from the LDS left over) stays 16-bit.
+constexpr int NBS_RW = 14;                 // ds_read_b64 registers (4 entries each) a lane
+constexpr int NBS_MAXCAP = 256 * NBS_RW;   // 3584 entries a wave sorts
+constexpr int NBS_BSH = 6;                 // bucket = column >> 6
+
+__host__ __device__ inline int nbs_table_words(int k) {
+  const int kp = k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+  const int nbn = 1 + 3 * k + 9 * k * (k - 1) / 2;
+  return (nbn + mr + mr * 17 + 3) & ~3;
+}
+// per wave: the histogram (nbk words, 16-byte aligned) + the buffer (cap2 entries in 16-slot
+// rows of 15)
+__host__ __device__ inline int nbs_wave_words(int nbk, int cap2) {
+  return ((nbk + 3) & ~3) + ((cap2 + 14) / 15) * 8;
+}
+
+// segment 2 (n2 entries, column >> 6 order, runs of 15 in 16-slot rows at sb, 16-byte
+// aligned) -> packed pieces + 16-bit spills of the list at dst (16-bit part from piece s1);
+// two passes (count the spills, then write), so the packed start n16 is known before any
+// piece is written; returns (n16, packed pieces)
+__device__ __forceinline__ uint2 nb_pack_seg2(const uint16_t *sb, uint32_t n2, uint16_t *dst,
+                                              uint32_t s1, uint32_t pad_col) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t ltmask = (1ull << lane) - 1ull;
+  const uint32_t nc = n2 / 15u;
+  auto load15 = [&](uint32_t cc, uint32_t *v) {
+    const uint4 a = *(const uint4 *)(sb + 16u * cc), b = *(const uint4 *)(sb + 16u * cc + 8u);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 15; ++e) v[e] = (e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
+  };
+  uint32_t nfail = 0;
+  for (uint32_t c0 = 0; c0 < nc; c0 += 64u) {
+    const uint32_t cc = c0 + (uint32_t)lane;
+    bool bad = false;
+    if (cc < nc) {
+      uint32_t v[15];
+      load15(cc, v);
+      uint32_t mn = v[0], mx = v[0];
+#pragma unroll
+      for (int e = 1; e < 15; ++e) {
+        mn = min(mn, v[e]);
+        mx = max(mx, v[e]);
+      }
+      bad = mx - mn > 254u;
+    }
+    nfail += (uint32_t)__popcll(__ballot(bad));
+  }
+  const uint32_t nt = n2 - 15u * nc;               // the last entries, past the runs of 15
+  const uint32_t nleft = 15u * nfail + nt;         // entries of the 16-bit part
+  const uint32_t l16 = (nleft + 7u) >> 3;
+  const uint32_t n16 = s1 + l16;
+  uint16_t *ldst = dst + s1 * 8u;
+  uint4 *pdst = (uint4 *)(dst + n16 * 8u);
+  uint32_t okc = 0, fc = 0;
+  for (uint32_t c0 = 0; c0 < nc; c0 += 64u) {
+    const uint32_t cc = c0 + (uint32_t)lane;
+    const bool act = cc < nc;
+    uint32_t v[15];
+    uint32_t mn = 0xFFFFu, mx = 0u;
+    if (act) {
+      load15(cc, v);
+#pragma unroll
+      for (int e = 0; e < 15; ++e) {
+        mn = min(mn, v[e]);
+        mx = max(mx, v[e]);
+      }
+    }
+    const bool ok = act && mx - mn <= 254u;
+    const uint64_t om = __ballot(ok), fm = __ballot(act && !ok);
+    if (ok) {
+      // the minimum to slot 0: its first occurrence takes v[0]'s value
+      bool done = v[0] == mn;
+#pragma unroll
+      for (int e = 1; e < 15; ++e) {
+        const bool sw = !done && v[e] == mn;
+        v[e] = sw ? v[0] : v[e];
+        done = done || sw;
+      }
+      uint32_t o[15];
+#pragma unroll
+      for (int e = 1; e < 15; ++e) o[e] = v[e] - mn;
+      pdst[okc + (uint32_t)__popcll(om & ltmask)] =
+          make_uint4(mn | (o[1] << 16) | (o[2] << 24), o[3] | (o[4] << 8) | (o[5] << 16) | (o[6] << 24),
+                     o[7] | (o[8] << 8) | (o[9] << 16) | (o[10] << 24),
+                     o[11] | (o[12] << 8) | (o[13] << 16) | (o[14] << 24));
+    } else if (act) {
+      const uint32_t l0 = 15u * (fc + (uint32_t)__popcll(fm & ltmask));
+#pragma unroll
+      for (int e = 0; e < 15; ++e) ldst[l0 + e] = (uint16_t)v[e];
+    }
+    okc += (uint32_t)__popcll(om);
+    fc += (uint32_t)__popcll(fm);
+  }
+  // the last nt entries (row nc of the buffer), then the dummy columns of the last 16-bit piece
+  if ((uint32_t)lane < nt) ldst[15u * nfail + lane] = sb[16u * nc + lane];
+  {
+    const uint32_t pp = nleft + (uint32_t)lane;
+    if (lane < 8 && pp < l16 * 8u) ldst[pp] = nb_dummy(pad_col, s1 * 8u + pp);
+  }
+  return make_uint2(n16, nc - nfail);
+}
+
+// lane-level: run [srcp, srcp + cnt) of the index into LDS at od (any alignment); HIST also
+// counts each entry in the 64-column bucket histogram.  Two whole 16-byte pieces of the index
+// hold the run's first 16 - (srcp & 7) entries (>= 9; a run has ~7 at N=20000), shifted into
+// place by register selects (texture-address work is per load instruction: 2 a lane instead of
+// one per entry); longer runs finish with 2-byte loads.
+template <bool HIST>
+__device__ __forceinline__ void nb_run_to_lds(const uint16_t *__restrict__ xent, uint32_t srcp,
+                                              uint32_t cnt, uint16_t *od, uint32_t *hist) {
+  if (cnt == 0) return;
+  const uint32_t a = srcp & 7u;
+  const uint4 *pp = (const uint4 *)(xent + (srcp - a));
+  const uint4 p0 = pp[0];
+  const uint4 p1 = a + cnt > 8u ? pp[1] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t w[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, 0u, 0u, 0u, 0u};
+  const uint32_t ad = a >> 1;
+  uint32_t o[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t lo = ad == 0 ? w[q] : ad == 1 ? w[q + 1] : ad == 2 ? w[q + 2] : w[q + 3];
+    const uint32_t hi = ad == 0 ? w[q + 1] : ad == 1 ? w[q + 2] : ad == 2 ? w[q + 3] : w[q + 4];
+    o[q] = (a & 1u) ? __builtin_amdgcn_alignbyte(hi, lo, 2) : lo;
+  }
+  const uint32_t nfit = min(cnt, 16u - a);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    if ((uint32_t)e < nfit) {
+      const uint32_t v = (o[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+      od[e] = (uint16_t)v;
+      if (HIST) atomicAdd(&hist[v >> NBS_BSH], 1u);
+    }
+  }
+  for (uint32_t e = nfit; e < cnt; ++e) {
+    const uint32_t v = xent[srcp + e];
+    od[e] = (uint16_t)v;
+    if (HIST) atomicAdd(&hist[v >> NBS_BSH], 1u);
+  }
+}
+
+__global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
-    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
-    uint32_t pad_col, int cap) {
-  constexpr int SW = 1 << (2 * S);
-  constexpr int NW = NT / 64;
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
+    uint16_t *__restrict__ table, uint32_t pad_col, int cap2, int nbk) {
+  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
   extern __shared__ __align__(16) uint32_t fsm[];
   const int kp = k - S;
   const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
@@ -403,118 +453,239 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
   uint32_t *rt = fsm;                        // [nbn] run j: r | suffix xor << 16 | class << 24
   uint32_t *pm = rt + nbn;                   // [mr] prefix xor of range r
   uint32_t *roff = pm + mr;                  // [mr][SW + 1] absolute index offsets
-  uint32_t *rbase = roff + mr * (SW + 1);    // [mr + 1] LDS position of each range
-  uint32_t *wtot = rbase + mr + 1;           // [NW] scan scratch
-  uint16_t *ent = (uint16_t *)(wtot + NW);   // [cap] the ranges' entries
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t *hist = fsm + nbs_table_words(k) + wave * nbs_wave_words(nbk, cap2);  // [nbk]
+  uint16_t *sbuf = (uint16_t *)(hist + ((nbk + 3) & ~3));                      // 16-byte aligned
   const uint32_t npref = 1u << (2 * kp);
-  // the run and range tables, once per workgroup (the grid is persistent)
   nb_group_tables<S>(k, NT, rt, pm);
   __syncthreads();
-  const int rpt = (mr + NT - 1) / NT;
-  const int t2 = 1 + 3 * k;
+  const int t2 = 1 + 3 * k;  // first Hamming-2 run (< 64 for k <= 21)
   for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
     const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
-    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 4^S lists empty (uniform)
-    // ---- 1. the ranges' bin offsets and sizes; their LDS positions (block scan): thread t
-    // owns the ranges [t RPT, t RPT + RPT)
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 16 lists empty (uniform)
     nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
     __syncthreads();
-    uint32_t myn = 0;
-    for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r)
-      myn += roff[r * (SW + 1) + SW] - roff[r * (SW + 1)];
-    {
-      const uint32_t inc = nb_wave_incl_scan_dpp(myn);
-      if (lane == 63) wtot[wave] = inc;
-      __syncthreads();
-      uint32_t base = 0, total = 0;
-      for (int w2 = 0; w2 < NW; ++w2) {
-        base += w2 < wave ? wtot[w2] : 0u;
-        total += wtot[w2];
-      }
-      uint32_t run = base + inc - myn;
-      for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
-        rbase[r] = run;
-        run += roff[r * (SW + 1) + SW] - roff[r * (SW + 1)];
-      }
-      if (threadIdx.x == 0) rbase[mr] = total;
-      __syncthreads();
-    }
-    const uint32_t etot = rbase[mr];
-    const bool staged = etot <= (uint32_t)cap;
-    // ---- 2. the ranges into LDS, one wave a range, all of a range's loads in flight
-    if (staged) {
-      for (int r = wave; r < mr; r += NW) {
-        const uint32_t a = roff[r * (SW + 1)], n = roff[r * (SW + 1) + SW] - a, d = rbase[r];
-        for (uint32_t j0 = 0; j0 < n; j0 += 256) {
-          uint16_t v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t j = j0 + 64u * q + lane;
-            if (j < n) v[q] = xent[a + j];
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t j = j0 + 64u * q + lane;
-            if (j < n) ent[d + j] = v[q];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- 3. the 4^S lists, one wave a list, 64 runs at a time in segment order: lane j
-    // places run j (wave prefix sum) and copies it
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
       if (tot == 0) continue;  // wave-uniform
       const uint2 sg = nbseg[b];
       uint16_t *dst = table + (size_t)start * 8u;
+      if ((tot - sg.y) * 8u > (uint32_t)cap2) {  // segment 2 past the buffer: 16-bit lists
+        nb_list_lane_per_run(k, su, rt, roff, xent, tot, sg, dst, pad_col);
+        if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
+        continue;
+      }
+      for (int q = lane; q < nbk; q += 64) hist[q] = 0u;
+      nb_wave_sync();
+      // ---- 1. runs: segments 0 / 1 to the table, segment 2 to the buffer (+ histogram)
       uint32_t carry = 0, n0 = 0, pre2 = 0;
       for (int j0 = 0; j0 < nbn; j0 += 64) {
         const int j = j0 + lane;
         uint32_t cnt = 0, srcp = 0, h = 2;
         if (j < nbn) {
           const uint32_t d = rt[j];
-          const uint32_t r = d & 0xFFFFu;
-          h = d >> 24;
-          const uint32_t *ro = roff + r * (SW + 1);
+          const uint32_t *ro = roff + (d & 0xFFFFu) * (SW + 1);
           const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
-          const uint32_t a0 = ro[sidx];
-          cnt = ro[sidx + 1] - a0;
-          srcp = staged ? rbase[r] + (a0 - ro[0]) : a0;
+          h = d >> 24;
+          srcp = ro[sidx];
+          cnt = ro[sidx + 1] - srcp;
         }
         const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
         const uint32_t pos = carry + inc - cnt;
         if (j0 == 0) {
           n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
-          pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);  // (t2 < 64 for k <= 21)
+          pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);
+        }
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if (h < 2) {
+          nb_copy_run(dst + (h == 0 ? 0u : sg.x * 8u - n0) + pos, xent + srcp, cnt);
+        } else {
+          nb_run_to_lds<true>(xent, srcp, cnt, sbuf + (pos - pre2), hist);
+        }
+      }
+      const uint32_t n2 = carry - pre2;
+      // dummy columns after segments 0 and 1
+      if (lane < 16) {
+        const int sgi = lane >> 3, e = lane & 7;
+        const uint32_t segb = sgi == 0 ? 0u : sg.x * 8u;
+        const uint32_t segn = sgi == 0 ? n0 : pre2 - n0;
+        const uint32_t segend = sgi == 0 ? sg.x * 8u : sg.y * 8u;
+        const uint32_t pp = segb + segn + (uint32_t)e;
+        if (pp < segend) dst[pp] = nb_dummy(pad_col, pp);
+      }
+      nb_wave_sync();
+      // ---- 2. bucket starts
+      {
+        const int per = (nbk + 63) >> 6, lo = lane * per, hi = min(nbk, lo + per);
+        uint32_t s = 0;
+        for (int q = lo; q < hi; ++q) s += hist[q];
+        uint32_t run = nb_wave_incl_scan_dpp(s) - s;
+        for (int q = lo; q < hi; ++q) {
+          const uint32_t t = hist[q];
+          hist[q] = run;
+          run += t;
+        }
+      }
+      // ---- 3. counting sort through registers (0xFFFF: no entry; columns < 65408)
+      {
+        uint2 rv[NBS_RW];
+#pragma unroll
+        for (int r = 0; r < NBS_RW; ++r) {
+          const uint32_t e = 256u * (uint32_t)r + 4u * (uint32_t)lane;
+          rv[r] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+          if (e < n2) {
+            rv[r] = *(const uint2 *)(sbuf + e);
+            // entries past n2 in the last read: no entry
+            if (e + 1 >= n2) rv[r].x |= 0xFFFF0000u;
+            if (e + 2 >= n2) rv[r].y |= 0x0000FFFFu;
+            if (e + 3 >= n2) rv[r].y |= 0xFFFF0000u;
+          }
+        }
+        nb_wave_sync();
+#pragma unroll
+        for (int r = 0; r < NBS_RW; ++r) {
+          if (256u * (uint32_t)r < n2) {  // wave-uniform
+            const uint32_t c4[4] = {rv[r].x & 0xFFFFu, rv[r].x >> 16, rv[r].y & 0xFFFFu, rv[r].y >> 16};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              if (c4[h] != 0xFFFFu) {
+                const uint32_t p = atomicAdd(&hist[c4[h] >> NBS_BSH], 1u);
+                sbuf[p + p / 15u] = (uint16_t)c4[h];
+              }
+            }
+          }
+        }
+      }
+      nb_wave_sync();
+      // ---- 4. pack
+      const uint2 us = nb_pack_seg2(sbuf, n2, dst, sg.y, pad_col);
+      if (lane == 0) nbuse[b] = us;
+      nb_wave_sync();  // the next list reuses the histogram and the buffer
+    }
+    __syncthreads();  // the next group overwrites the range offsets
+  }
+}
+
+
+// ------------------------------------------------------------------ staged 16-bit fill
+// The 16-bit lists through LDS: one wave a list assembles the whole list (three segments,
+// dummy tails) in a per-wave LDS buffer from 16-byte piece loads of the index
+// (nb_run_to_lds), then writes it with 16-byte stores, 1 KB a wave instruction -- against
+// two 2-byte texture-address operations an entry for the lane-per-run copies (~25 TA cycles
+// an instruction: the grouped fill is TA-bound, profiles/r04t_pmc_fill.txt, r05k).  Lists past
+// the buffer take the lane-per-run copies.
+__global__ __launch_bounds__(1024) void nb_fill_staged_kernel(
+    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
+    uint16_t *__restrict__ table, uint32_t pad_col, int cap16) {
+  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  extern __shared__ __align__(16) uint32_t fsm[];
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  const int nbn = nb_neighbours(k);
+  uint32_t *rt = fsm;
+  uint32_t *pm = rt + nbn;
+  uint32_t *roff = pm + mr;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint16_t *sbuf = (uint16_t *)(fsm + nbs_table_words(k) + wave * (cap16 / 2));  // 16-byte aligned
+  const uint32_t npref = 1u << (2 * kp);
+  nb_group_tables<S>(k, NT, rt, pm);
+  __syncthreads();
+  const int t2 = 1 + 3 * k;
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    const int64_t cbase = (gi - P) * SW;
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;
+    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
+    __syncthreads();
+    for (int su = wave; su < SW; su += NW) {
+      const int64_t b = cbase + (int64_t)P * SW + su;
+      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+      if (tot == 0) continue;  // wave-uniform
+      const uint2 sg = nbseg[b];
+      uint16_t *dst = table + (size_t)start * 8u;
+      if (tot * 8u > (uint32_t)cap16) {
+        nb_list_lane_per_run(k, su, rt, roff, xent, tot, sg, dst, pad_col);
+        if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
+        continue;
+      }
+      uint32_t carry = 0, n0 = 0, pre2 = 0;
+      for (int j0 = 0; j0 < nbn; j0 += 64) {
+        const int j = j0 + lane;
+        uint32_t cnt = 0, srcp = 0, h = 2;
+        if (j < nbn) {
+          const uint32_t d = rt[j];
+          const uint32_t *ro = roff + (d & 0xFFFFu) * (SW + 1);
+          const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
+          h = d >> 24;
+          srcp = ro[sidx];
+          cnt = ro[sidx + 1] - srcp;
+        }
+        const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
+        const uint32_t pos = carry + inc - cnt;
+        if (j0 == 0) {
+          n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
+          pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);
         }
         carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        {
-          uint16_t *o = dst + dpos;
-          if (staged)
-            nb_copy_run<WS>(o, ent + srcp, cnt);
-          else
-            nb_copy_run<WS>(o, xent + srcp, cnt);
-        }
+        nb_run_to_lds<false>(xent, srcp, cnt, sbuf + dpos, nullptr);
       }
       const uint32_t total = carry;
-      // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
-      if (lane < 24) {
+      if (lane < 24) {  // dummy columns after each segment
         const int sgi = lane >> 3, e = lane & 7;
         const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
         const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
         const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
         const uint32_t pp = segb + segn + (uint32_t)e;
-        if (pp < segend) dst[pp] = (uint16_t)(pad_col + (pp & 63u));
+        if (pp < segend) sbuf[pp] = nb_dummy(pad_col, pp);
       }
+      nb_wave_sync();
+      for (uint32_t q = (uint32_t)lane; q < tot; q += 64u) ((uint4 *)dst)[q] = ((const uint4 *)sbuf)[q];
+      if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
+      nb_wave_sync();  // the next list reuses the buffer
     }
-    __syncthreads();  // the next group overwrites the LDS image
+    __syncthreads();
   }
 }
+
+// ------------------------------------------------------------------ 16-bit grouped fill
+// One workgroup per group of 16 lists, one wave a list (nb_list_lane_per_run).
+__global__ __launch_bounds__(1024) void nb_fill_grouped_kernel(
+    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
+    uint16_t *__restrict__ table, uint32_t pad_col) {
+  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  extern __shared__ __align__(16) uint32_t fsm[];
+  const int kp = k - S;
+  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  const int nbn = nb_neighbours(k);
+  uint32_t *rt = fsm;
+  uint32_t *pm = rt + nbn;
+  uint32_t *roff = pm + mr;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t npref = 1u << (2 * kp);
+  nb_group_tables<S>(k, NT, rt, pm);
+  __syncthreads();
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    const int64_t cbase = (gi - P) * SW;
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;
+    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
+    __syncthreads();
+    for (int su = wave; su < SW; su += NW) {
+      const int64_t b = cbase + (int64_t)P * SW + su;
+      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
+      if (tot == 0) continue;  // wave-uniform
+      nb_list_lane_per_run(k, su, rt, roff, xent, tot, nbseg[b], table + (size_t)start * 8u, pad_col);
+      if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
+    }
+    __syncthreads();
+  }
+}
+
 
 // ------------------------------------------------------------------ piece-assembled fill
 // The lane-per-run copies above are bound by the texture-address unit, not by bytes: their
@@ -531,12 +702,11 @@ __global__ __launch_bounds__(NT) void nb_fill_grouped_kernel(
 //     per store instruction (~5 a list instead of ~90).
 // Groups whose image exceeds the LDS, and lists of more than NBP_MAXP pieces, take the
 // lane-per-run copy from the index.
-template <int NL>
-__global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
+__global__ __launch_bounds__(1024) void nb_fill_pieces_kernel(
     int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
-    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
-    uint32_t pad_col, int cap) {
-  constexpr int S = 2, SW = 16, NT = NL * 64, NW = NL, NH = SW / NL;
+    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
+    uint16_t *__restrict__ table, uint32_t pad_col, int cap) {
+  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
   extern __shared__ __align__(16) uint32_t fsm[];
   const int kp = k - S;
   const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
@@ -555,28 +725,20 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
   __syncthreads();
   const int rpt = (mr + NT - 1) / NT;
   const int t2 = 1 + 3 * k;
-  const int nfull = 1 + 3 * kp;  // ranges whose every sub-bin a half group takes
   const uint64_t ltmask = (1ull << lane) - 1ull;
   uint16_t *re = tabs + wave * tw;   // [nbn + 1] destination end of non-empty run idx
   uint16_t *rsd = re + nbn + 1;      // [nbn + 1] image offset - destination start
   uint16_t *pst = rsd + nbn + 1;     // [NBP_MAXP] first run reaching piece p
-  for (int64_t bi = blockIdx.x; bi < ngroups * NH; bi += gridDim.x) {
-    const int64_t gi = bi / NH;
-    const int hh = (int)(bi - gi * NH);  // which NL of the group's 16 lists (suffixes)
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
     const int64_t cbase = (gi - P) * SW;
-    if (nboff[gi * SW + hh * NL + NL] == nboff[gi * SW + hh * NL]) continue;  // uniform
-    // sub-bins [slo, shi) of range r the block's lists take: all 16 of the own prefix and the
-    // Hamming-1 prefixes (suffix Hamming <= 1 reaches every first letter), only the block's
-    // own suffixes [hh NL, hh NL + NL) of the Hamming-2 prefixes
-    auto slo = [&](int r) { return r < nfull ? 0 : hh * NL; };
-    auto shi = [&](int r) { return r < nfull ? SW : hh * NL + NL; };
+    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // uniform
     // ---- 1. ranges: offsets, image positions (n + 14 words each: 8-aligned + source phase)
     nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
     __syncthreads();
     uint32_t myn = 0;
     for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r)
-      myn += roff[r * (SW + 1) + shi(r)] - roff[r * (SW + 1) + slo(r)] + 14u;
+      myn += roff[r * (SW + 1) + SW] - roff[r * (SW + 1)] + 14u;
     {
       const uint32_t inc = nb_wave_incl_scan_dpp(myn);
       if (lane == 63) wtot[wave] = inc;
@@ -588,9 +750,9 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
       }
       uint32_t run = base + inc - myn;
       for (int r = threadIdx.x * rpt; r < min(mr, (int)(threadIdx.x + 1) * rpt); ++r) {
-        const uint32_t a = roff[r * (SW + 1) + slo(r)];
+        const uint32_t a = roff[r * (SW + 1)];
         rbase[r] = ((run + 7u) & ~7u) + (a & 7u);
-        run += roff[r * (SW + 1) + shi(r)] - a + 14u;
+        run += roff[r * (SW + 1) + SW] - a + 14u;
       }
       if (threadIdx.x == 0) rbase[mr] = total;
       __syncthreads();
@@ -599,7 +761,7 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
     // ---- 2. the image: whole 16-byte pieces of each range, one wave a range
     if (staged) {
       for (int r = wave; r < mr; r += NW) {
-        const uint32_t a = roff[r * (SW + 1) + slo(r)], n = roff[r * (SW + 1) + shi(r)] - a;
+        const uint32_t a = roff[r * (SW + 1)], n = roff[r * (SW + 1) + SW] - a;
         if (n == 0) continue;
         const uint32_t fp = a >> 3, lp = (a + n + 7u) >> 3;
         uint16_t *d0 = img + (rbase[r] - (a & 7u));
@@ -608,8 +770,8 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
       }
     }
     __syncthreads();
-    // ---- 3. the block's NL lists, one wave a list
-    for (int su = hh * NL + wave; su < hh * NL + NL; su += NW) {
+    // ---- 3. the group's 16 lists, one wave a list
+    for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
       if (tot == 0) continue;  // wave-uniform
@@ -628,7 +790,7 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
           const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
           a0 = ro[sidx];
           cnt = ro[sidx + 1] - a0;
-          si = rbase[r] + (a0 - ro[slo((int)r)]);
+          si = rbase[r] + (a0 - ro[0]);
         }
         const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
         const uint32_t pos = carry + inc - cnt;
@@ -647,7 +809,7 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
           }
           nzc += (uint32_t)__popcll(bal);
         } else {
-          nb_copy_run<1>(dst + dpos, xent + a0, cnt);
+          nb_copy_run(dst + dpos, xent + a0, cnt);
         }
       }
       const uint32_t total = carry;
@@ -656,14 +818,12 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
           re[nzc] = (uint16_t)(tot * 8u);  // sentinel: past every entry
           rsd[nzc] = 0;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        nb_wave_sync();
         for (uint32_t idx = (uint32_t)lane; idx <= nzc; idx += 64u) {
           const uint32_t lo = idx ? re[idx - 1] : 0u, hi = re[idx];
           for (uint32_t p = (lo + 7u) >> 3; p < ((hi + 7u) >> 3); ++p) pst[p] = (uint16_t)idx;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        nb_wave_sync();
         // dummy columns: [n0, sx), [e1, sy), [e2, tot * 8)
         const uint32_t sx = sg.x * 8u, sy = sg.y * 8u;
         const uint32_t e1 = sx + (pre2 - n0), e2 = sy + (total - pre2);
@@ -697,7 +857,7 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
               }
               uint32_t v;
               if ((d >= n0 && d < sx) || (d >= e1 && d < sy) || d >= e2)
-                v = (pad_col + (d & 63u)) & 0xFFFFu;
+                v = nb_dummy(pad_col, d);
               else
                 v = img[(sdj + d) & 0xFFFFu];
               if (q & 1) w[q >> 1] |= v << 16;
@@ -719,7 +879,7 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
           }
           *(uint4 *)(dst + d0) = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        __builtin_amdgcn_wave_barrier();  // the next list overwrites the tables
+        nb_wave_sync();  // the next list overwrites the tables
       } else if (lane < 24) {
         // dummy columns after each segment, spread over 64 LDS words of the Gram kernel
         const int sgi = lane >> 3, e = lane & 7;
@@ -727,180 +887,74 @@ __global__ __launch_bounds__(NL * 64) void nb_fill_pieces_kernel(
         const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
         const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
         const uint32_t pp = segb + segn + (uint32_t)e;
-        if (pp < segend) dst[pp] = (uint16_t)(pad_col + (pp & 63u));
+        if (pp < segend) dst[pp] = nb_dummy(pad_col, pp);
       }
+      if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
     }
     __syncthreads();  // the next group overwrites the image
   }
 }
 
-// ------------------------------------------------------------------ range-major fill
-// The grouped fill's copies run range-major: the 16 lists of a group (S = 2) take their runs
-// from the 211 prefix ranges, and the 16 sub-bins of one range are contiguous in the index.
-//  1. the ranges' sub-bin offsets (as the grouped fill);
-//  2. one wave a list places its 352 runs (wave prefix sums in segment order) into an LDS
-//     position table pos[list][run] and writes the segments' dummy tails;
-//  3. one wave a range copies the range's entries 64 at a time (coalesced 2-byte loads),
-//     each entry to every list that takes its sub-bin (1 list for the 189 Hamming-2 prefix
-//     ranges, 7 for the 21 Hamming-1 ones, 16 for the group's own prefix): the sub-bin from
-//     the 17 offsets held in SGPRs, the run from an inverse table inv[range][suffix xor].
-// Per group ~420 load and ~700 store instructions, against ~2900 for lane-per-run copies
-// whose lanes idle past the mean run (7 entries of a 64-run chunk whose longest has ~15).
-__global__ __launch_bounds__(1024) void nb_fill_ranges_kernel(
-    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
-    const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint16_t *__restrict__ table,
-    uint32_t pad_col) {
-  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
-  extern __shared__ __align__(16) uint32_t fsm[];
-  const int kp = k - S;
-  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
-  const int nbn = nb_neighbours(k);
-  uint32_t *rt = fsm;                        // [nbn] run j: r | suffix xor << 16 | class << 24
-  uint32_t *pm = rt + nbn;                   // [mr] prefix xor of range r
-  uint32_t *roff = pm + mr;                  // [mr][17] absolute index offsets
-  uint32_t *pos = roff + mr * (SW + 1);      // [SW][nbn] list position of run j (entries)
-  uint32_t *lst = pos + SW * nbn;            // [SW] list start (pieces)
-  uint16_t *inv = (uint16_t *)(lst + SW);    // [mr][16] run of (range, suffix xor); 0xFFFF none
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t npref = 1u << (2 * kp);
-  for (int j = threadIdx.x; j < mr * SW; j += NT) inv[j] = 0xFFFFu;
-  for (int r = threadIdx.x; r < mr; r += NT) {
-    uint32_t w = 0;
-    if (r > 0) {
-      int t = r - 1;
-      if (t < 3 * kp) {
-        const int p = t / 3;
-        w = (uint32_t)(t - 3 * p + 1) << (2 * (kp - 1 - p));
-      } else {
-        t -= 3 * kp;
-        const int pi = t / 9, rr = t - 9 * pi;
-        int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)pi)) * 0.5f);
-        while (q * (q - 1) / 2 > pi) --q;
-        while ((q + 1) * q / 2 <= pi) ++q;
-        const int p = pi - q * (q - 1) / 2;
-        w = ((uint32_t)(rr / 3 + 1) << (2 * (kp - 1 - p))) ^
-            ((uint32_t)(rr - 3 * (rr / 3) + 1) << (2 * (kp - 1 - q)));
-      }
-    }
-    pm[r] = w;
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < nbn; j += NT) {
-    int r, h;
-    uint32_t dm;
-    nb_run_desc<S>(j, k, r, dm, h);
-    rt[j] = (uint32_t)r | (dm << 16) | ((uint32_t)h << 24);
-    inv[r * SW + (int)dm] = (uint16_t)j;
-  }
-  __syncthreads();
-  const int t2 = 1 + 3 * k;
-  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
-    const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
-    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 16 lists empty (uniform)
-    // ---- 1. the ranges' sub-bin offsets
-    for (int r = threadIdx.x; r < mr; r += NT) {
-      const uint32_t *o = xoff + cbase + (int64_t)(P ^ pm[r]) * SW;
-#pragma unroll
-      for (int q = 0; q <= SW; ++q) roff[r * (SW + 1) + q] = o[q];
-    }
-    __syncthreads();
-    // ---- 2. run positions of the 16 lists, one wave a list
-    {
-      const int su = wave;
-      const int64_t b = cbase + (int64_t)P * SW + su;
-      const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
-      if (lane == 0) lst[su] = start;
-      if (tot > 0) {  // wave-uniform
-        const uint2 sg = nbseg[b];
-        uint32_t carry = 0, n0 = 0, pre2 = 0;
-        for (int j0 = 0; j0 < nbn; j0 += 64) {
-          const int j = j0 + lane;
-          uint32_t cnt = 0, h = 2;
-          if (j < nbn) {
-            const uint32_t d = rt[j];
-            const uint32_t *ro = roff + (d & 0xFFFFu) * (SW + 1);
-            const uint32_t sidx = (uint32_t)su ^ ((d >> 16) & 0xFFu);
-            cnt = ro[sidx + 1] - ro[sidx];
-            h = d >> 24;
-          }
-          const uint32_t inc = nb_wave_incl_scan(cnt);
-          const uint32_t p0 = carry + inc - cnt;
-          if (j0 == 0) {
-            n0 = __shfl(cnt, 0, 64);
-            pre2 = __shfl(p0, t2 & 63, 64);  // (t2 = 1 + 3k < 64 for k <= 21)
-          }
-          carry += __shfl(inc, 63, 64);
-          if (j < nbn)
-            pos[su * nbn + j] = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + p0;
-        }
-        const uint32_t total = carry;
-        if (lane < 24) {  // dummy columns after each segment (64 distinct LDS words)
-          const int sgi = lane >> 3, e = lane & 7;
-          const uint32_t segb = sgi == 0 ? 0u : sgi == 1 ? sg.x * 8u : sg.y * 8u;
-          const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
-          const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
-          const uint32_t pp = segb + segn + (uint32_t)e;
-          if (pp < segend) table[(size_t)start * 8u + pp] = (uint16_t)(pad_col + (pp & 63u));
-        }
-      }
-    }
-    __syncthreads();
-    // ---- 3. range-major copies, one wave a range
-    for (int r = wave; r < mr; r += NW) {
-      const uint32_t myoff = lane <= SW ? roff[r * (SW + 1) + lane] : 0u;
-      uint32_t so[SW + 1];
-#pragma unroll
-      for (int q = 0; q <= SW; ++q) so[q] = __builtin_amdgcn_readlane(myoff, q);
-      const uint32_t base = so[0], n = so[SW] - base;
-      const int hp = r == 0 ? 0 : r <= 3 * kp ? 1 : 2;
-      for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-        const uint32_t e = e0 + lane;
-        if (e >= n) continue;
-        const uint16_t v = xent[base + e];
-        int sb = 0;
-#pragma unroll
-        for (int q = 1; q < SW; ++q) sb += (base + e >= so[q]) ? 1 : 0;
-        const uint32_t t = base + e - so[sb];
-        const uint16_t *iv = inv + r * SW;
-        if (hp == 2) {  // only the list with suffix sb
-          table[(size_t)lst[sb] * 8u + pos[sb * nbn + iv[0]] + t] = v;
-        } else if (hp == 1) {  // the lists within one suffix letter of sb
-#pragma unroll
-          for (int x = 0; x < 7; ++x) {
-            const int dmx = x == 0 ? 0 : x <= 3 ? x : (x - 3) << 2;
-            const int su = sb ^ dmx;
-            table[(size_t)lst[su] * 8u + pos[su * nbn + iv[dmx]] + t] = v;
-          }
-        } else {  // the group's own prefix: every list
-#pragma unroll
-          for (int dmx = 0; dmx < SW; ++dmx) {
-            const int su = sb ^ dmx;
-            table[(size_t)lst[su] * 8u + pos[su * nbn + iv[dmx]] + t] = v;
-          }
-        }
-      }
-    }
-    __syncthreads();  // the next group overwrites the tables
-  }
+// ------------------------------------------------------------------ Gram
+// One workgroup per (row i, column chunk c) -- an ITEM of the row-accumulator grid
+// (rowacc_block: chunk-major, upper block triangle for a full square K) -- accumulating
+// the row over the chunk in an int32 LDS accumulator, then streaming it out through the
+// fused normalize_K epilogue (emit_row).  The row's window table -- per window (list start,
+// 16-bit pieces, segment ends, packed pieces) and two prefix sums -- splits the row's
+// pieces evenly over the 16 waves: first the 16-bit pieces (8 columns, weight by segment),
+// then the packed ones (15 columns, weight w2), NB_UNROLL 16-byte loads a lane a batch, one
+// ds_add a column.
+// TWO workgroups a CU: their table build, epilogue and streaming overlap.  At a 20000-column
+// chunk (configs 3 and 5) the accumulator alone is 80000 B of the 81920 B each may hold, so
+// the table is kept to 4 P + 2 words (segment ends as two halfwords, 16 dummy columns) --
+// the round-4 measurement of the same kernel with one workgroup a CU (a double-buffered
+// table, 84.9 KB) was 22 % slower (2.60 vs 2.13 ms, N=20000, profiles/r05g_*: half the
+// resident waves); a persistent form (a wave building the next row's table) and two load
+// batches in flight a wave measured slower still (profiles/r05f_*).
+namespace {
+// descriptor words of one row: wst[P] wc16[P+1] wseg[P] wcp[P+1] srec[ldp]
+__host__ __device__ inline int nb_desc_words(int P, int64_t ldp) { return 4 * P + 2 + (int)ldp; }
+
+// the segment ends of a list as halfwords (s0 | s1 << 16); 0xFFFFFFFF when s1 >= 0xFFFF
+// (lists of more than ~520000 Hamming <= 1 entries in one chunk): the stream re-reads them
+__device__ __forceinline__ uint32_t nb_seg_word(uint2 sg) {
+  return sg.y < 0xFFFFu ? (sg.x | (sg.y << 16)) : 0xFFFFFFFFu;
 }
 
-// One workgroup per (row i, column chunk c) (rowacc_block: chunk-major, upper block
-// triangle for a full square K).
-// A16: 16-bit column counters, two a dword (the LDS of a chunk halves: two workgroups a CU
-// at N=200000's 28572-column chunks instead of one).  Exact while no count reaches 2^16:
-// K is a Gram matrix (K_ij = <phi(x_i), phi(x_j)>), so K_ij^2 <= K_ii K_jj, and a (row,
-// chunk) whose K_ii x max_{j in chunk} K_jj < 2^32 cannot overflow; any other takes two
-// passes over its list with 32-bit counters for half the chunk's columns each.
-template <int K, int NB_UNROLL, bool A16>
+// one wave: inclusive prefix of wc[1 .. P] (wc[0] = 0)
+__device__ __forceinline__ void nb_wave_prefix(uint32_t *wc, int P) {
+  const int lane = threadIdx.x & 63;
+  const int per = (P + 63) >> 6, lo = lane * per, hi = min(P, lo + per);
+  uint32_t s = 0;
+  for (int a = lo; a < hi; ++a) s += wc[a + 1];
+  uint32_t run = nb_wave_incl_scan_dpp(s) - s;
+  for (int a = lo; a < hi; ++a) {
+    run += wc[a + 1];
+    wc[a + 1] = run;
+  }
+  if (lane == 0) wc[0] = 0;
+}
+
+// the window of piece q: the last a with wc[a] <= q
+__device__ __forceinline__ int nb_find_window(const uint32_t *wc, int P, uint32_t q) {
+  int lo = 0, hi = P - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (wc[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+}  // namespace
+
+template <int K, int NB_UNROLL>
 __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
                                                        const uint32_t *__restrict__ nboff,
                                                        const uint2 *__restrict__ nbseg,
+                                                       const uint2 *__restrict__ nbuse,
                                                        const uint4 *__restrict__ table,
                                                        int64_t row0, int64_t rows, int w0, int w1,
-                                                       int w2, OutSpec o,
-                                                       const double *__restrict__ kdiag,
-                                                       const double *__restrict__ kdmax) {
+                                                       int w2, OutSpec o) {
   extern __shared__ __align__(16) uint32_t smem[];
   int c;
   int64_t il;
@@ -910,76 +964,65 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int accw = ((g.chunk + 3) >> 2) << 2;
-  const int accn = A16 ? (((accw >> 1) + 32 + 3) & ~3) : accw + 64;  // counter words (+ dummies)
+  const int accn = accw + NB_DUMMIES;  // counters + the dummy columns
   const int P = g.pmax;
   uint32_t *wst = smem + accn;        // [P] list start of window a (pieces)
-  uint32_t *wcum = wst + P;           // [P + 1] pieces of windows < a
-  uint32_t *ws0 = wcum + P + 1;       // [P] end of segment 0 (pieces, list-relative)
-  uint32_t *ws1 = ws0 + P;            // [P] end of segment 1
-  uint32_t *srec = ws1 + P;           // packed row record
+  uint32_t *wc16 = wst + P;           // [P + 1] 16-bit pieces of windows < a
+  uint32_t *wseg = wc16 + P + 1;      // [P] segment ends (nb_seg_word)
+  uint32_t *wcp = wseg + P;           // [P + 1] packed pieces of windows < a
+  uint32_t *srec = wcp + P + 1;       // packed row record
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   stage_record(pk, i, srec);
   __syncthreads();
   const uint32_t cbase = (uint32_t)c << (2 * K);
   for (int a = threadIdx.x; a < P; a += blockDim.x) {
     const uint32_t u = pk_window(srec, pk.cw, a, K);
-    uint32_t st = 0, n = 0, s0 = 0, s1 = 0;
+    uint32_t st = 0, n16 = 0, sw = 0, np = 0;
     if (u != KMG_INVALID) {
       const uint32_t b = cbase + u;
       st = nboff[b];
-      n = nboff[b + 1] - st;
-      const uint2 sg = nbseg[b];
-      s0 = sg.x;
-      s1 = sg.y;
+      const uint32_t en = nboff[b + 1];
+      const uint2 sg = nbseg[b], us = nbuse[b];  // (nbuse is stale for an empty list)
+      if (en != st) {
+        sw = nb_seg_word(sg);
+        n16 = us.x;
+        np = us.y;
+      }
     }
     wst[a] = st;
-    wcum[a + 1] = n;
-    ws0[a] = s0;
-    ws1[a] = s1;
+    wc16[a + 1] = n16;
+    wseg[a] = sw;
+    wcp[a + 1] = np;
+  }
+  {
+    uint4 *acc4 = (uint4 *)smem;
+    for (int w = threadIdx.x; w < (accn >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  if (wave == 0) {  // inclusive prefix of wcum[1 .. P] (one wave, contiguous runs a lane)
-    const int per = (P + 63) >> 6, lo = lane * per, hi = min(P, lo + per);
-    uint32_t s = 0;
-    for (int a = lo; a < hi; ++a) s += wcum[a + 1];
-    uint32_t run = nb_wave_incl_scan(s) - s;
-    for (int a = lo; a < hi; ++a) {
-      run += wcum[a + 1];
-      wcum[a + 1] = run;
-    }
-    if (lane == 0) wcum[0] = 0;
-  }
-  // 16-bit counters for this (row, chunk), or two 32-bit passes over column halves
-  const bool c16 = A16 && kdiag[i] * kdmax[c] < 4294967296.0;
-  const int npass = (!A16 || c16) ? 1 : 2;
-  const uint32_t half = (uint32_t)((((cw + 1) >> 1) + 7) & ~7);  // pass 1's first column
-  const bool norm = o.normalize && o.diagv[0] != 1.0;
-  for (int pass = 0; pass < npass; ++pass) {
-    // pass columns [plo, plo + pcw) (relative to col0); 32-bit counters at acc[x - plo]
-    const uint32_t plo = npass == 1 ? 0u : pass * half;
-    // (a chunk's last columns can be fewer than half: pass 0 takes them all, pass 1 none)
-    const uint32_t ucw = (uint32_t)cw;
-    const uint32_t pcw = npass == 1 ? ucw : pass ? (ucw > half ? ucw - half : 0u) : min(half, ucw);
-    {
-      uint4 *acc4 = (uint4 *)smem;
-      for (int w = threadIdx.x; w < (accn >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    // this wave's share of the row's pieces; lane l takes pieces qb + l, qb + l + 64, ...
-    const uint32_t T = wcum[P];
+  if (wave == 0) nb_wave_prefix(wc16, P);
+  if (wave == 1) nb_wave_prefix(wcp, P);
+  __syncthreads();
+  int32_t *acc = (int32_t *)smem;
+  char *accb = (char *)smem;
+  // ---- 16-bit pieces: segment 0 (w0), segment 1 (w1), the 16-bit part of segment 2 (w2)
+  {
+    const uint32_t T = wc16[P];
     const uint32_t qb = (uint32_t)(((uint64_t)T * wave) / nw), qe = (uint32_t)(((uint64_t)T * (wave + 1)) / nw);
     uint32_t q = qb + lane;
-    int a = 0;  // window of piece q: the last a with wcum[a] <= q
-    {
-      int lo = 0, hi = P - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (wcum[mid] <= q) lo = mid;
-        else hi = mid - 1;
+    int a = q < qe ? nb_find_window(wc16, P, q) : 0;
+    uint32_t abeg = wc16[a], aend = wc16[a + 1], ast = wst[a], as0 = 0, as1 = 0;
+    auto segs = [&]() {
+      const uint32_t sw = wseg[a];
+      if (sw != 0xFFFFFFFFu) {
+        as0 = sw & 0xFFFFu;
+        as1 = sw >> 16;
+      } else {  // ends past 16 bits: from the table of segment ends
+        const uint2 sg = nbseg[cbase + pk_window(srec, pk.cw, a, K)];
+        as0 = sg.x;
+        as1 = sg.y;
       }
-      a = lo;
-    }
-    uint32_t abeg = wcum[a], aend = wcum[a + 1], ast = wst[a], as0 = ws0[a], as1 = ws1[a];
+    };
+    segs();
     for (; q < qe; q += 64 * NB_UNROLL) {
       uint4 v[NB_UNROLL];
       int wt[NB_UNROLL];
@@ -991,10 +1034,9 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
           while (qq >= aend) {
             ++a;
             abeg = aend;
-            aend = wcum[a + 1];
+            aend = wc16[a + 1];
             ast = wst[a];
-            as0 = ws0[a];
-            as1 = ws1[a];
+            segs();
           }
           const uint32_t rel = qq - abeg;
           v[t] = table[(uint64_t)ast + rel];
@@ -1005,64 +1047,66 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
       for (int t = 0; t < NB_UNROLL; ++t) {
         if (wt[t]) {
           const uint32_t x[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
-          if (!A16) {
-            int32_t *acc = (int32_t *)smem;
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              atomicAdd(&acc[x[h] & 0xFFFFu], wt[t]);
-              atomicAdd(&acc[x[h] >> 16], wt[t]);
-            }
-          } else if (c16) {
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const uint32_t xl = x[h] & 0xFFFFu, xh = x[h] >> 16;
-              atomicAdd(&smem[xl >> 1], (uint32_t)wt[t] << ((xl & 1u) << 4));
-              atomicAdd(&smem[xh >> 1], (uint32_t)wt[t] << ((xh & 1u) << 4));
-            }
-          } else {  // 32-bit counters of this pass's columns (dummies >= accw never land)
-            int32_t *acc = (int32_t *)smem;
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const uint32_t xl = (x[h] & 0xFFFFu) - plo, xh = (x[h] >> 16) - plo;
-              if (xl < pcw) atomicAdd(&acc[xl], wt[t]);
-              if (xh < pcw) atomicAdd(&acc[xh], wt[t]);
-            }
+          for (int h = 0; h < 4; ++h) {
+            atomicAdd(&acc[x[h] & 0xFFFFu], wt[t]);
+            atomicAdd(&acc[x[h] >> 16], wt[t]);
           }
         }
       }
     }
-    __syncthreads();
-    if (c16)
-      emit_row<true, true>(o, il, i, col0, cw, (const int32_t *)smem, norm);
-    else
-      emit_row<true>(o, il, i, col0 + plo, (int)pcw, (const int32_t *)smem, norm);
-    if (pass + 1 < npass) __syncthreads();
   }
-}
-
-// per column chunk, the largest raw diagonal K_jj of its columns (the 16-bit counters' bound)
-__global__ __launch_bounds__(256) void chunk_dmax_kernel(const double *__restrict__ kdiag, int64_t n,
-                                                         int chunk, double *__restrict__ dmax) {
-  __shared__ double red[256];
-  const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = min(n, c0 + chunk);
-  double m = 0.0;
-  for (int64_t j = c0 + threadIdx.x; j < c1; j += 256) m = fmax(m, kdiag[j]);
-  red[threadIdx.x] = m;
+  // ---- packed pieces of segment 2: column c0 (low half of word 0) + 14 byte offsets
+  {
+    const uint32_t T = wcp[P];
+    const uint32_t qb = (uint32_t)(((uint64_t)T * wave) / nw), qe = (uint32_t)(((uint64_t)T * (wave + 1)) / nw);
+    uint32_t q = qb + lane;
+    int a = q < qe ? nb_find_window(wcp, P, q) : 0;
+    uint32_t abeg = wcp[a], aend = wcp[a + 1], ast = wst[a] + (wc16[a + 1] - wc16[a]);
+    for (; q < qe; q += 64 * NB_UNROLL) {
+      uint4 v[NB_UNROLL];
+      bool ok[NB_UNROLL];
+#pragma unroll
+      for (int t = 0; t < NB_UNROLL; ++t) {
+        const uint32_t qq = q + 64u * t;
+        ok[t] = qq < qe;
+        if (ok[t]) {
+          while (qq >= aend) {
+            ++a;
+            abeg = aend;
+            aend = wcp[a + 1];
+            ast = wst[a] + (wc16[a + 1] - wc16[a]);
+          }
+          v[t] = table[(uint64_t)ast + (qq - abeg)];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NB_UNROLL; ++t) {
+        if (ok[t]) {
+          // byte addresses: 4 (c0 + o) = 4 c0 + ((word >> (8 b - 2)) & 0x3FC) for byte b
+          const uint32_t b4 = (v[t].x & 0xFFFFu) << 2;
+          atomicAdd((int *)(accb + b4), w2);
+          atomicAdd((int *)(accb + b4 + ((v[t].x >> 14) & 0x3FCu)), w2);
+          atomicAdd((int *)(accb + b4 + ((v[t].x >> 22) & 0x3FCu)), w2);
+          const uint32_t y[3] = {v[t].y, v[t].z, v[t].w};
+#pragma unroll
+          for (int h = 0; h < 3; ++h) {
+            atomicAdd((int *)(accb + b4 + ((y[h] << 2) & 0x3FCu)), w2);
+            atomicAdd((int *)(accb + b4 + ((y[h] >> 6) & 0x3FCu)), w2);
+            atomicAdd((int *)(accb + b4 + ((y[h] >> 14) & 0x3FCu)), w2);
+            atomicAdd((int *)(accb + b4 + ((y[h] >> 22) & 0x3FCu)), w2);
+          }
+        }
+      }
+    }
+  }
   __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + st]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dmax[blockIdx.x] = red[0];
+  const bool norm = o.normalize && o.diagv[0] != 1.0;
+  emit_row<true>(o, il, i, col0, cw, acc, norm);
 }
 
-hipError_t launch_chunk_dmax(const double *kdiag, int64_t n, int chunk, int nchunks, double *dmax,
-                             hipStream_t s) {
-  if (nchunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(chunk_dmax_kernel, dim3((unsigned)nchunks), dim3(256), 0, s, kdiag, n, chunk, dmax);
-  return hipGetLastError();
-}
 
+// ------------------------------------------------------------------ host side
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
   // every occurrence sits in the lists of its 1 + 3k + 9k(k-1)/2 neighbours; a non-empty list
   // pads each of its three segments by at most 7 entries
@@ -1070,9 +1114,44 @@ int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
   return e + 21 * std::min(nbins, e);
 }
 
-size_t nb_gram_lds(const IndexGeom &g, const Packed &pk, bool a16) {
+size_t nb_gram_lds(const IndexGeom &g, const Packed &pk) {
   const int accw = ((g.chunk + 3) >> 2) << 2;
-  return (size_t)((a16 ? (((accw >> 1) + 32 + 3) & ~3) : accw + 64) + 4 * g.pmax + 1 + pk.ldp) * 4;
+  return (size_t)(accw + NB_DUMMIES + nb_desc_words(g.pmax, pk.ldp)) * 4;
+}
+
+// Hamming-2 entries of a list per column of the chunk (chunk x P / 4^k occurrences of a
+// k-mer, 9 k (k-1) / 2 neighbours)
+static double nb_seg2_density(int k, int pmax) {
+  return 4.5 * k * (k - 1) * (double)pmax / (double)(1ull << (2 * k));
+}
+
+int nb_sorted_cap(int k, int pmax, int chunk) {
+  if (k < 4 || k > 12) return 0;
+  const double dens = nb_seg2_density(k, pmax);
+  // 15 entries must span <= 254 columns: at ~12 columns between entries (14 x 12 = 168) the
+  // runs still fit; k = 10 (28 columns) would spill nearly every run
+  if (dens < 1.0 / 12.0) return 0;
+  const int nbk = (chunk + (1 << NBS_BSH) - 1) >> NBS_BSH;
+  const int64_t per_wave = (160 * 1024 / 4 - nbs_table_words(k)) / 16;  // words, 16 waves
+  // buffer words a wave: 8 a row of 15 entries
+  const int64_t rows = (per_wave - ((nbk + 3) & ~3)) / 8;
+  int64_t cap = std::min<int64_t>(rows * 15, NBS_MAXCAP);
+  // the buffer holds segment 2 of a list of the mean + 25 % (longer lists stay 16-bit)
+  if (cap <= 0 || (double)cap < 1.25 * dens * chunk) return 0;
+  return (int)(cap & ~7LL);
+}
+
+int nb_sorted_max_chunk(int k, int pmax) {
+  const double dens = nb_seg2_density(k, pmax);
+  if (k < 4 || k > 12 || dens < 1.0 / 12.0) return 0;
+  int lo = 8, hi = 65536 - 128;
+  if (!nb_sorted_cap(k, pmax, lo)) return 0;
+  while (lo < hi) {  // nb_sorted_cap is non-zero on a prefix of chunk sizes
+    const int mid = (lo + hi + 1) / 2;
+    if (nb_sorted_cap(k, pmax, mid)) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo & ~7;
 }
 
 hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *hist,
@@ -1086,143 +1165,90 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 }
 
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
-                          const uint32_t *nboff, const uint2 *nbseg, uint16_t *table,
-                          hipStream_t s, int form, int cap_override) {
+                          const uint32_t *nboff, const uint2 *nbseg, uint2 *nbuse,
+                          uint16_t *table, hipStream_t s, int form) {
   const int64_t nbins = g.nbins();
-  if (g.copies != 1 || g.k < 2 || g.k > 12) return hipErrorInvalidValue;
+  if (g.copies != 1 || g.k < 4 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
   const double mean = (double)g.chunk * g.pmax / (double)g.nkeys;  // occurrences of a k-mer
-  if (form == 6 && g.k >= 4) {
-    // range-major grouped fill (S = 2)
-    const int kp = g.k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
-    const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
-    const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * 17 + 16 * (size_t)nbn + 16) +
-                       sizeof(uint16_t) * (size_t)mr * 16;
-    if (lds <= 160 * 1024) {
-      const int64_t ngroups = nbins / 16;
-      const int64_t blocks = std::min<int64_t>(ngroups, 256 * 8);
-      hipLaunchKernelGGL(nb_fill_ranges_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
-                         ngroups, xoff, xent, nboff, nbseg, table, pad_col);
-      return hipGetLastError();
-    }
-  }
-  // auto: the piece-assembled fill where a list's runs are long enough for its fixed cost per
-  // group (~7 us of range offsets + image loads) to pay: N=200000 rank slab (7 chunks of
-  // 28572 columns, 10.1 occurrences a k-mer and chunk) fill 9.1 -> 7.0 ms; at N=20000 (7.1)
-  // the lane-per-run copies stay ahead, 1.25 vs 1.30 ms (profiles/r04_nb_fill.jsonl r04z)
-  if (form == 0 && mean >= 8.5) form = 9;
-  if ((form == 9 || form == 10) && g.k >= 4 && (((uintptr_t)xent) & 15u) == 0) {
-    // piece-assembled grouped fill (S = 2): 16 lists a 1024-thread workgroup (form 9) or 8
-    // lists a 512-thread one (form 10: half the LDS image, two workgroups a CU, measured
-    // slower: each half group reloads the 211 ranges' offsets); the LDS left after the
-    // tables is the image
-    const int nl = form == 9 ? 16 : 8, nt = nl * 64;
-    const int bpc = form == 9 ? 1 : 2;  // workgroups a CU the LDS is split for
-    const size_t fixed = 4 * (size_t)nb_pieces_img_word(g.k, nt);
-    const size_t avail = (size_t)160 * 1024 / bpc;
-    int cap = fixed < avail ? (int)std::min<size_t>((avail - fixed) / 2, 65528) & ~7 : 0;
-    if (cap_override >= 0) cap = std::min(cap, cap_override & ~7);
-    if (cap >= 1024) {
-      const size_t lds = fixed + 2 * (size_t)cap;
-      const int64_t ngroups = nbins / 16;
-      const int64_t blocks = std::min<int64_t>(ngroups * (16 / nl), 256 * bpc);
-      if (nl == 16)
-        hipLaunchKernelGGL(nb_fill_pieces_kernel<16>, dim3((unsigned)blocks), dim3(nt), lds, s, g.k,
-                           ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
-      else
-        hipLaunchKernelGGL(nb_fill_pieces_kernel<8>, dim3((unsigned)blocks), dim3(nt), lds, s, g.k,
-                           ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap);
-      return hipGetLastError();
-    }
-  }
-  if (form != 1 && g.k >= 4) {
-    // grouped fill: S = 2 (16 lists a workgroup of 1024 threads) while the expected LDS
-    // image stays <= 48 KB, else S = 1 (4 lists, 256 threads); the image is sized at 2x the
-    // expectation (larger groups copy straight from the index)
-    auto ranges = [&](int S) { const int kp = g.k - S; return 1 + 3 * kp + 9 * kp * (kp - 1) / 2; };
-    const double e2 = ranges(2) * 16.0 * mean, e1 = ranges(1) * 4.0 * mean;  // LDS entries
-    // S = 2 unless forced: it beat S = 1 at both sizes measured, also where the range image
-    // overflows the LDS for part of the groups (N=200000 rank slab: fill 13.2 vs 23.3 ms;
-    // N=20000: 1.44 vs 2.43 ms, profiles/r04_nb_fill.jsonl)
-    const int S = form == 2 ? 1 : 2;
-    const int SW = 1 << (2 * S), mr = ranges(S);
-    const int nt = S == 2 ? 1024 : 512;
-    const double e = S == 2 ? e2 : e1;
-    int cap = (int)std::min(1.5 * e + 1024.0, S == 2 ? 40960.0 : 24576.0);
-    cap = (cap + 7) & ~7;
-    // no LDS range image by default: copying the runs straight from the index (L2 /
-    // Infinity Cache) measured faster than staging them (N=20000 fill 1.49 -> 1.27 ms, rank
-    // slab equal; profiles/r04_nb_fill.jsonl r04o); KMG_NB_CAP > 0 stages up to that many
-    cap = cap_override >= 0 ? std::min(cap, cap_override & ~7) : 0;
-    const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
-    const int ws = form == 4 ? 2 : form == 5 ? 4 : 1;
-    const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * (SW + 1) + mr + 1 + nt / 64) +
-                       2 * (size_t)cap;
-    const int64_t ngroups = nbins / SW;
-    const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
-    // store width: 1 / 2 / 4 entries (KMG_NB_FILL 3 / 4 / 5; auto 1: the wider stores measured
-    // equal or slower, N=200000 rank slab fill 9.1 -> 15.1 ms, profiles/r04_nb_fill.jsonl r04n)
-#define KMG_NBG(S_, NT_, WS_)                                                                  \
-  hipLaunchKernelGGL((nb_fill_grouped_kernel<S_, NT_, WS_>), dim3((unsigned)blocks), dim3(NT_), \
-                     lds, s, g.k, ngroups, xoff, xent, nboff, nbseg, table, pad_col, cap)
-    if (S == 2) {
-      if (ws == 1) KMG_NBG(2, 1024, 1);
-      else if (ws == 2) KMG_NBG(2, 1024, 2);
-      else KMG_NBG(2, 1024, 4);
-    } else {
-      KMG_NBG(1, 512, 4);
-    }
-#undef KMG_NBG
+  const int64_t ngroups = nbins / 16;
+  const int cap = nb_sorted_cap(g.k, g.pmax, g.chunk);
+  if ((form == 0 || form == 1) && cap > 0) {
+    // sorted fill, packed segment 2 (the Gram reads ~0.6x the bytes of 16-bit lists)
+    const int nbk = (g.chunk + (1 << NBS_BSH) - 1) >> NBS_BSH;
+    const size_t lds = 4 * ((size_t)nbs_table_words(g.k) + 16 * (size_t)nbs_wave_words(nbk, cap));
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int64_t blocks = std::min<int64_t>(ngroups, 256);
+    hipLaunchKernelGGL(nb_fill_sorted_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
+                       ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap, nbk);
     return hipGetLastError();
   }
-  const int64_t wpb = NB_FILL_THREADS / 64;
-  // waves in flight: 32 a CU x 256 CUs, each walking bins in key order (neighbouring
-  // k-mers share most of their neighbours' posting lines in L2)
-  const int64_t fill_blocks = std::min<int64_t>((nbins + wpb - 1) / wpb, 8 * 256);
-  // lanes a run: the mean occurrences of a k-mer in a chunk, to a power of two in [4, 32]
-  const int lg = mean <= 4.0 ? 4 : mean <= 8.0 ? 8 : mean <= 16.0 ? 16 : 32;
-#define KMG_NBF(LG_)                                                                             \
-  hipLaunchKernelGGL(nb_fill_kernel<LG_>, dim3((unsigned)fill_blocks), dim3(NB_FILL_THREADS), 0, \
-                     s, g.k, nbins, xoff, xent, nboff, nbseg, table, pad_col)
-  if (lg == 4) KMG_NBF(4);
-  else if (lg == 8) KMG_NBF(8);
-  else if (lg == 16) KMG_NBF(16);
-  else KMG_NBF(32);
-#undef KMG_NBF
+  if (form == 1) return hipErrorInvalidValue;  // forced sorted fill where it cannot run
+  if (form == 0 || form == 4 || form == 5) {
+    // staged 16-bit fill: the whole list in a per-wave LDS buffer, 16-byte stores
+    const int cap16 = ((160 * 1024 / 4 - nbs_table_words(g.k)) / 16 * 2) & ~7;
+    const double mean_list = (double)(1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2) * mean;
+    if (cap16 >= 1.25 * mean_list + 64) {
+      const size_t lds = 4 * ((size_t)nbs_table_words(g.k) + 16 * (size_t)(cap16 / 2));
+      const int64_t blocks = std::min<int64_t>(ngroups, 256);
+      hipLaunchKernelGGL(nb_fill_staged_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
+                         ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16);
+      return hipGetLastError();
+    }
+    if (form == 4) return hipErrorInvalidValue;
+  }
+  // 16-bit lists.  The piece-assembled fill where a list's runs are long enough for its fixed
+  // cost per group (~7 us of range offsets + image loads) to pay: N=200000 rank slab (7
+  // chunks of 28572 columns, 10.1 occurrences a k-mer and chunk) fill 9.1 -> 7.0 ms; at
+  // N=20000 (7.1) the lane-per-run copies stay ahead, 1.25 vs 1.30 ms
+  // (profiles/r04_nb_fill.jsonl r04z).  KMG_NB_FILL: 2 grouped, 3 pieces.
+  const bool pieces = form == 3 || (form != 2 && mean >= 8.5);
+  if (pieces && (((uintptr_t)xent) & 15u) == 0) {
+    const size_t fixed = 4 * (size_t)nb_pieces_img_word(g.k, 1024);
+    const size_t avail = (size_t)160 * 1024;
+    const int cap = fixed < avail ? (int)std::min<size_t>((avail - fixed) / 2, 65528) & ~7 : 0;
+    if (cap >= 1024) {
+      const size_t lds = fixed + 2 * (size_t)cap;
+      const int64_t blocks = std::min<int64_t>(ngroups, 256);
+      hipLaunchKernelGGL(nb_fill_pieces_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
+                         ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap);
+      return hipGetLastError();
+    }
+  }
+  const int kp = g.k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+  const int nbn = 1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2;
+  const size_t lds = sizeof(uint32_t) * ((size_t)nbn + mr + (size_t)mr * 17);
+  const int64_t blocks = std::min<int64_t>(ngroups, 256 * 16);
+  hipLaunchKernelGGL(nb_fill_grouped_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
+                     ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col);
   return hipGetLastError();
 }
 
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
-                                    const uint2 *nbseg, const uint4 *table, int64_t row0,
-                                    int64_t row1, int w0, int w1, int w2, const OutSpec &o,
-                                    hipStream_t s, int threads, int unroll, const double *kdiag,
-                                    const double *kdmax) {
+                                    const uint2 *nbseg, const uint2 *nbuse, const uint4 *table,
+                                    int64_t row0, int64_t row1, int w0, int w1, int w2,
+                                    const OutSpec &o, hipStream_t s, int threads, int unroll) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
-  if (g.k < 3 || g.k > 12 || g.copies != 1) return hipErrorNotSupported;
+  if (g.k < 4 || g.k > 12 || g.copies != 1) return hipErrorNotSupported;
   if (threads != 512 && threads != 1024) return hipErrorInvalidValue;
-  const bool a16 = kdiag != nullptr && kdmax != nullptr;
   const int64_t nblk = rowacc_blocks(g, o, row0, rows);
   if (nblk * threads >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
-  if (g.chunk + 64 + 63 >= 65536) return hipErrorInvalidValue;      // uint16 columns + dummies
-  const size_t lds = nb_gram_lds(g, pk, a16);
+  if (g.chunk + NB_DUMMIES + 63 >= 65536) return hipErrorInvalidValue;  // uint16 columns
+  const size_t lds = nb_gram_lds(g, pk);
   if (lds > (threads == 512 ? 80 : 160) * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk);
   switch (g.k) {
 #define KMG_NB(KK)                                                                              \
   case KK:                                                                                      \
-    if (a16)                                                                                    \
-      hipLaunchKernelGGL((gram_nb_kernel<KK, 4, true>), grid, dim3(threads), lds, s, g, pk,     \
-                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
-    else if (unroll == 8)                                                                       \
-      hipLaunchKernelGGL((gram_nb_kernel<KK, 8, false>), grid, dim3(threads), lds, s, g, pk,    \
-                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
+    if (unroll == 4)                                                                            \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 4>), grid, dim3(threads), lds, s, g, pk, nboff,   \
+                         nbseg, nbuse, table, row0, rows, w0, w1, w2, o);                       \
     else                                                                                        \
-      hipLaunchKernelGGL((gram_nb_kernel<KK, 4, false>), grid, dim3(threads), lds, s, g, pk,    \
-                         nboff, nbseg, table, row0, rows, w0, w1, w2, o, kdiag, kdmax);         \
+      hipLaunchKernelGGL((gram_nb_kernel<KK, 8>), grid, dim3(threads), lds, s, g, pk, nboff,   \
+                         nbseg, nbuse, table, row0, rows, w0, w1, w2, o);                       \
     break;
-    KMG_NB(3) KMG_NB(4) KMG_NB(5) KMG_NB(6) KMG_NB(7) KMG_NB(8) KMG_NB(9) KMG_NB(10) KMG_NB(11)
-    KMG_NB(12)
+    KMG_NB(4) KMG_NB(5) KMG_NB(6) KMG_NB(7) KMG_NB(8) KMG_NB(9) KMG_NB(10) KMG_NB(11) KMG_NB(12)
 #undef KMG_NB
   }
   return hipGetLastError();

@@ -1,5 +1,5 @@
 // kmg_rowacc.h — shared pieces of the row-accumulator Gram kernels (kmg_gram.hip,
-// kmg_pairs.hip): a workgroup accumulates one row of K (one column chunk) in LDS, then
+// kmg_nbhd.hip): a workgroup accumulates one row of K (one column chunk) in LDS, then
 // streams it to HBM.  Device code only; included by the .hip translation units.
 #pragma once
 #include "kmg_internal.h"
@@ -23,9 +23,8 @@ __host__ __device__ __forceinline__ int64_t rowacc_blocks(const IndexGeom &g, co
   for (int c = 0; c < g.nchunks; ++c) t += tri_rows(g.n, g.chunk, c, row0, rows);
   return t;
 }
-__device__ __forceinline__ void rowacc_block(const IndexGeom &g, const OutSpec &o, int64_t row0,
-                                             int64_t rows, int &c, int64_t &il) {
-  int64_t b = (int64_t)blockIdx.x;
+__device__ __forceinline__ void rowacc_item(const IndexGeom &g, const OutSpec &o, int64_t row0,
+                                            int64_t rows, int64_t b, int &c, int64_t &il) {
   if (!o.tri) {
     c = (int)(b / rows);
     il = b - (int64_t)c * rows;
@@ -37,6 +36,11 @@ __device__ __forceinline__ void rowacc_block(const IndexGeom &g, const OutSpec &
     b -= rc;
   }
   il = b;
+}
+// (item b = blockIdx.x: one workgroup per item)
+__device__ __forceinline__ void rowacc_block(const IndexGeom &g, const OutSpec &o, int64_t row0,
+                                             int64_t rows, int &c, int64_t &il) {
+  rowacc_item(g, o, row0, rows, (int64_t)blockIdx.x, c, il);
 }
 
 // copy the packed record of sequence i into LDS (every thread of the block takes part)

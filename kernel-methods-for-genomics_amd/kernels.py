@@ -152,8 +152,9 @@ def _codes_of_rows(rows, k):
 
 
 def _string_beta_cols(betas, k):
-    """get_phi_u's string betas -> column codes.  A beta of another length than k equals
-    no window (x[i:i+k] always holds k symbols); the device scores ACGT k-mers."""
+    """get_phi_u's string betas -> column codes, or None when a beta of length k holds a
+    letter outside A/C/G/T (those take the symbol columns).  A beta of another length than k
+    equals no window (x[i:i+k] always holds k symbols)."""
     if not all(isinstance(b, str) for b in betas):
         raise TypeError("get_phi_u: betas must be strings (kernels.py:37)")
     cols = np.full(len(betas), _NO_MATCH, dtype=np.uint32)
@@ -162,12 +163,74 @@ def _string_beta_cols(betas, k):
         try:
             raw = "".join(b for b, t in zip(betas, sel) if t).encode("ascii")
         except UnicodeEncodeError:
-            raw = None
-        letters = None if raw is None else _ACGT_CODE[np.frombuffer(raw, dtype=np.uint8)]
-        if letters is None or (letters > 3).any():
-            raise NotImplementedError("get_phi_u: betas outside the A/C/G/T alphabet")
+            return None
+        letters = _ACGT_CODE[np.frombuffer(raw, dtype=np.uint8)]
+        if (letters > 3).any():
+            return None
         cols[sel] = _codes_of_rows(letters.reshape(-1, k), k)
     return cols
+
+
+# ---- symbol columns: any letter / value compares by identity (kmg_features_sym)
+_PAD = 255  # the code no window holds
+
+
+def _symbol_codes(keys):
+    """A code per distinct key: A/C/G/T (or format()ed 1..4) -> 0..3 in the reference's beta
+    order, every other key its own code from 4 (< 255: the padding code)."""
+    table = {}
+    for key in keys:
+        if key not in table:
+            table[key] = None
+    out, nxt = {}, 4
+    for key in table:
+        fixed = _FIXED_CODE.get(key)
+        if fixed is not None:
+            out[key] = fixed
+        else:
+            out[key] = nxt
+            nxt += 1
+    if nxt > _PAD:
+        raise NotImplementedError("feature maps: more than 251 distinct symbols outside A/C/G/T")
+    return out
+
+
+_FIXED_CODE = {"A": 0, "C": 1, "G": 2, "T": 3, 1: 0, 2: 1, 3: 2, 4: 3}
+
+
+def _sym_columns(rows, k, code):
+    """Beta symbol lists -> uint8 [len(rows), 16] columns (None: a beta no window equals)."""
+    cols = np.zeros((len(rows), 16), dtype=np.uint8)
+    for j, r in enumerate(rows):
+        if r is None:
+            cols[j, :k] = _PAD
+        else:
+            cols[j, :k] = [code[s] for s in r]
+    return cols
+
+
+def _phi_u_symbols(x, k, betas):
+    """get_phi_u with betas outside A/C/G/T: x and the betas in one symbol code space, string
+    equality by code identity on the device."""
+    code = _symbol_codes(list(x) + [c for b in betas if len(b) == k for c in b])
+    xc = np.array([[code[c] for c in x]], dtype=np.uint8).reshape(1, -1)
+    codes = np.full((1, max(4, -(-len(x) // 4) * 4)), _PAD, dtype=np.uint8)
+    codes[0, :len(x)] = xc
+    rows = [list(b) if len(b) == k else None for b in betas]
+    return _eng().features_sym(_L.KMG_SPECTRUM, codes, np.array([len(x)], dtype=np.int32), k,
+                               _sym_columns(rows, k, code))[0]
+
+
+def _phi_km_symbols(xa, k, m, B, bcast):
+    """get_phi_km over format()ed values outside 1..4 (in x or in the betas) or with numpy's
+    broadcast of short k-mers: integer equality by code identity on the device."""
+    xs = [v.item() if hasattr(v, "item") else v for v in xa.reshape(-1)]
+    bs = [[v.item() if hasattr(v, "item") else v for v in row] for row in B]
+    code = _symbol_codes(xs + [v for row in bs for v in row])
+    codes = np.full((1, max(4, -(-len(xs) // 4) * 4)), _PAD, dtype=np.uint8)
+    codes[0, :len(xs)] = [code[v] for v in xs]
+    return _eng().features_sym(_L.KMG_MISMATCH, codes, np.array([len(xs)], dtype=np.int32), k,
+                               _sym_columns(bs, k, code), m=m, bcast=bcast)[0]
 
 
 def _format_rows(a):
@@ -216,7 +279,11 @@ def get_phi_u(x, k, betas):
     betas = list(betas)
     if not betas:
         return np.zeros(0)
+    if k > 16:
+        raise NotImplementedError("get_phi_u: k > 16")
     cols = _string_beta_cols(betas, k)
+    if cols is None:
+        return _phi_u_symbols(x, k, betas)
     return _eng().features(_L.KMG_SPECTRUM, [x], k, cols)[0]
 
 
@@ -232,10 +299,10 @@ def get_phi_km(x, k, m, betas):
     n_x = len(xa)
     if len(betas) == 0:
         return np.zeros(0)
+    quirk = False
     if n_x < 101:
         # window lengths min(k, n_x - i), i in range(101 - k + 1): numpy broadcasts a
         # short k-mer of 1 symbol (or 0 at k = 1) against the beta and raises for others
-        quirk = False
         for i in range(101 - k + 1):
             ln = max(0, min(k, n_x - i))
             if ln == k:
@@ -245,10 +312,18 @@ def get_phi_km(x, k, m, betas):
                 continue
             raise ValueError(f"operands could not be broadcast together with shapes ({ln},) "
                              f"({k},) ")
-        if quirk:
-            raise NotImplementedError("get_phi_km: a row shorter than 101 whose short k-mers "
-                                      "numpy broadcasts (1 symbol) is not supported")
-    cols = _formatted_beta_cols(betas, k, "get_phi_km")
+    if k > 16:
+        raise NotImplementedError("get_phi_km: k > 16")
+    B = np.asarray(betas)
+    if B.ndim == 1 and k == 1:
+        B = B.reshape(-1, 1)
+    if B.ndim != 2 or B.shape[1] != k:
+        raise NotImplementedError(f"get_phi_km: betas must be format()ed {k}-mers")
+    _, x_ok = _format_rows(xa)
+    _, b_ok = _format_rows(B)
+    if quirk or not x_ok or not b_ok:
+        return _phi_km_symbols(xa, k, m, B, quirk)
+    cols = _codes_of_rows(_format_rows(B)[0], k)
     return _eng().features(_L.KMG_MISMATCH, [_decoded(xa)], k, cols, m=m)[0]
 
 

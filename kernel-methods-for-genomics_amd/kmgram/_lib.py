@@ -36,7 +36,10 @@ EXPORTS = (
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
     "kmg_gram_to_host", "kmg_gram_blocks_wire", "kmg_last_plan", "kmg_features",
+    "kmg_last_factorisation", "kmg_features_sym",
 )
+KMG_FEATURES_BCAST = 1
+KMG_FACTOR_CHOLESKY, KMG_FACTOR_LU_ASYMMETRIC, KMG_FACTOR_LU_INDEFINITE = 1, 2, 3
 
 
 class KmgParams(ctypes.Structure):
@@ -92,6 +95,8 @@ def load():
                                  I64], ctypes.c_int),
             "kmg_features": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, P, I64, P, I64],
                              ctypes.c_int),
+            "kmg_features_sym": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, P, I64, I32, P,
+                                  I64], ctypes.c_int),
             "kmg_normalize": ([P, P, I64, I64, ctypes.POINTER(I32)], ctypes.c_int),
             "kmg_center": ([P, P, I64, P, I64, I64], ctypes.c_int),
             "kmg_dmalloc": ([P, ctypes.POINTER(P), SZ], ctypes.c_int),
@@ -105,6 +110,7 @@ def load():
             "kmg_timing_reset": ([P], ctypes.c_int),
             "kmg_stage_ms": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "kmg_last_plan": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+            "kmg_last_factorisation": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
             "kmg_stage_stats": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(I32)], ctypes.c_int),
             "kmg_comm_unique_id": ([P], ctypes.c_int),
@@ -210,6 +216,18 @@ class Context:
         out = np.empty((n, len(cols)), dtype=np.float64)
         check(self.lib.kmg_features(self._h, ctypes.byref(params), ptr(codes), ptr(lens), n, ldc,
                                     ptr(cols), len(cols), ptr(out), len(cols)))
+        return out
+
+    def features_sym(self, params, codes, lens, cols, flags=0):
+        """float64 [n, len(cols)] feature rows over symbol columns (kmg_features_sym): cols is
+        uint8 [ncols, 16], column j the k symbol codes cols[j, :k] in the rows' code space."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        cols = np.ascontiguousarray(cols, dtype=np.uint8).reshape(-1, 16)
+        n, ldc = codes.shape
+        out = np.empty((n, len(cols)), dtype=np.float64)
+        check(self.lib.kmg_features_sym(self._h, ctypes.byref(params), ptr(codes), ptr(lens), n,
+                                        ldc, ptr(cols), len(cols), int(flags), ptr(out), len(cols)))
         return out
 
     def gram_device(self, params, d_codes, d_lens, n, ldc, row0, row1, out_dtype, d_out, ld):
@@ -384,12 +402,21 @@ class Context:
 
     def last_plan(self):
         """How the last spectrum / mismatch call was built (include/kmgram.h kmg_last_plan)."""
-        v = (ctypes.c_int32 * 5)()
+        v = (ctypes.c_int32 * 6)()
         check(self.lib.kmg_last_plan(self._h, v))
+        # (5, "pair_lines": round 3's pair-lines table, removed in round 5)
         names = ("dense", "hamming", "posting", "slots", "pairs", "pair_lines", "neighbourhood",
                  "generic")
         return {"formulation": names[v[0]] if 0 <= v[0] < len(names) else None,
-                "chunk": v[1], "nchunks": v[2], "triangle": bool(v[3]), "threads": v[4]}
+                "chunk": v[1], "nchunks": v[2], "triangle": bool(v[3]), "threads": v[4],
+                "packed": bool(v[5])}
+
+    def last_factorisation(self):
+        """The last KRR / KLR solve's factorisation: "cholesky", "lu_asymmetric",
+        "lu_indefinite" or None (include/kmgram.h kmg_last_factorisation)."""
+        v = ctypes.c_int32(0)
+        check(self.lib.kmg_last_factorisation(self._h, ctypes.byref(v)))
+        return {1: "cholesky", 2: "lu_asymmetric", 3: "lu_indefinite"}.get(v.value)
 
     def stage_ms(self, stage):
         v = ctypes.c_double(0.0)

@@ -189,6 +189,15 @@ class GramEngine:
         p = P.make(kind, k=int(k), m=int(m), g=int(g), window=101)
         return self.ctx.features(p, codes, lens, cols)
 
+    def features_sym(self, kind, codes, lens, k, col_syms, m=0, bcast=False):
+        """float64 [n, len(col_syms)] over symbol columns (kmg_features_sym): codes / lens are
+        the rows in the caller's symbol code space, col_syms uint8 [ncols, 16] the betas' codes
+        in the same space; bcast: get_phi_km's numpy broadcast of short k-mers (rows shorter
+        than the 101 window)."""
+        p = P.make(kind, k=int(k), m=int(m), window=101)
+        return self.ctx.features_sym(p, codes, lens, col_syms,
+                                     L.KMG_FEATURES_BCAST if bcast else 0)
+
     def substring_b_pair(self, x, y, lbda, k):
         """B_k(lbda, k, x, y) of the substring kernel's recursion (kernels.py:322-342) at the
         full strings, from the device sweep (la_mode KMG_MODE_SS_B)."""

@@ -493,13 +493,22 @@ def phi_u(x, k, betas):
 
 
 def phi_km(x, k, m, betas):
-    """get_phi_km (kernels.py:161-175) for one format()ed row (len >= 101): phi[j] =
-    #{i < 101-k+1 : #(x[i:i+k] != betas[j]) <= m}."""
+    """get_phi_km (kernels.py:161-175) for one format()ed row: phi[j] = #{i < 101-k+1 :
+    #(x[i:i+k] != betas[j]) <= m}.  A row shorter than 101 (kernels.py:171 still walks 101-k+1
+    windows) compares its short k-mers as numpy does: one symbol broadcasts against every
+    letter of the beta, none (k = 1) sums to 0 mismatches, and any other length raises."""
     x = np.asarray(x).reshape(-1)
     B = np.asarray(betas).reshape(len(betas), -1)
-    W = np.stack([x[i:i + k] for i in range(101 - k + 1)])       # windows x k
-    H = (W[:, None, :] != B[None, :, :]).sum(axis=2)                # windows x betas
-    return (H <= m).sum(axis=0).astype(np.float64)
+    if len(x) >= 101:
+        W = np.stack([x[i:i + k] for i in range(101 - k + 1)])       # windows x k
+        H = (W[:, None, :] != B[None, :, :]).sum(axis=2)                # windows x betas
+        return (H <= m).sum(axis=0).astype(np.float64)
+    out = np.zeros(len(B))
+    for i in range(101 - k + 1):
+        kmer = x[i:i + k]
+        for j, b in enumerate(B):
+            out[j] += (np.sum(kmer != b) <= m)
+    return out
 
 
 def gappy1_phi(x, betas):

@@ -9,8 +9,10 @@ PREFIXES = ("PHIU_", "PHIKM_", "GAPK_", "BK_")
 
 
 def fmt(s):
-    """kernels.format: 'A','C','G','T' -> 1..4 (the oracle side of the tests)."""
-    return np.array([" ACGT".index(c) for c in s], dtype=np.int64)
+    """kernels.format (kernels.py:187-193): 'A','C','G','T' -> 1..4, digits stay their value
+    (the round-5 fixtures pass values outside 1..4 this way), anything else raises."""
+    return np.array([int(c) for c in s.replace("A", "1").replace("C", "2").replace("G", "3")
+                     .replace("T", "4")], dtype=np.int64)
 
 
 def betas(entry):

@@ -182,6 +182,26 @@ def main():
             jobs.append((f"PHIKM_x{xi}_k{k}_m{m}", "get_phi_km", {"k": k, "m": m, "betas": "canonical"}, [x]))
     kcustom = [[1, 2, 3], [4, 4, 4], [2, 2, 1], [3, 1, 4]]
     jobs.append(("PHIKM_x0_k3_m1_custom", "get_phi_km", {"k": 3, "m": 1, "betas": kcustom}, [kmx[0]]))
+    # round 5: betas and sequences outside A/C/G/T (string / integer identity), and the rows
+    # shorter than get_phi_km's 101 window whose short k-mers numpy broadcasts
+    nb3 = ["GTN", "TNA", "NAC", "ACG", "NNN", "CGT", "GTA", "AC", "N"]
+    for xi in (0, 2):
+        jobs.append((f"PHIU_sym_x{xi}_k3", "get_phi_u", {"k": 3, "betas": nb3}, [phx[xi]]))
+    jobs.append(("PHIU_sym_x7_k2", "get_phi_u", {"k": 2, "betas": ["XX", "AX", "GX", "XA", "AC", "xA", "X"]},
+                 ["AXXCGXAXXA"]))
+    jobs.append(("PHIU_sym_x8_k1", "get_phi_u", {"k": 1, "betas": ["A", "N", "-", "C", "n", ""]},
+                 ["AN-CnNNA--"]))
+    xd = seqs[0][:50] + "5" + seqs[0][51:70] + "0" + seqs[0][71:]
+    vb = [[1, 5, 3], [5, 5, 5], [0, 1, 2], [2, 2, 1], [1, 0, 4], [4, 4, 4]]
+    for m in (0, 1, 2):
+        jobs.append((f"PHIKM_sym_xd_k3_m{m}", "get_phi_km", {"k": 3, "m": m, "betas": vb}, [xd]))
+    jobs.append(("PHIKM_sym_xd_k3_m1_canon", "get_phi_km", {"k": 3, "m": 1, "betas": "canonical"}, [xd]))
+    jobs.append(("PHIKM_sym_x0_k2_m0_vals", "get_phi_km", {"k": 2, "m": 0, "betas": [[1, 7], [7, 7], [2, 2]]},
+                 [seqs[0]]))
+    for xi, (x, k, m) in enumerate(((seqs[1][:100], 2, 0), (seqs[1][:100], 2, 1), (seqs[2][:60], 1, 0),
+                                    (seqs[2][:60], 1, 1), (seqs[3][:100], 2, 2), ("", 1, 0),
+                                    (seqs[4][:99], 2, 1))):
+        jobs.append((f"PHIKM_sym_short{xi}_k{k}_m{m}", "get_phi_km", {"k": k, "m": m, "betas": "canonical"}, [x]))
     for xi, x in enumerate([seqs[0], "ACGA", "", seqs[5][:60]]):
         jobs.append((f"GAPK_x{xi}_k1_g0", "gappy_k", {"k": 1, "g": 0, "betas": "canonical"}, [x]))
     for k, g in ((3, 1), (3, 0), (2, 3), (3, 2), (3, 3), (1, 1)):

@@ -141,7 +141,7 @@ def test_config5_mismatch_k9_n200000_full_one_gpu(ctx, tune, form):
                         d_lens, n, codes.shape[1], 0, n, L.KMG_I32, d_K, n)
         ctx.synchronize()
         plan = ctx.last_plan()
-        assert plan["formulation"] in ("slots", "pair_lines", "neighbourhood") and plan["triangle"], plan
+        assert plan["formulation"] in ("slots", "neighbourhood") and plan["triangle"], plan
         assert plan["nchunks"] >= 2 and plan["chunk"] * plan["nchunks"] >= n, plan
         ch = plan["chunk"]
         edges = [c * ch for c in range(1, plan["nchunks"]) if c * ch < n]

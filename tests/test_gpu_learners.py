@@ -164,3 +164,38 @@ def test_krr_klr_asymmetric_K_match_inv(ctx):
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
     sym = ctx.krr_solve((K + K.T) / 2, y, lb)
     assert not np.allclose(sym, got, rtol=1e-9, atol=0)  # the triangle read would differ
+
+
+def test_engine_gram_takes_cholesky(ctx):
+    """Every Gram kmg_gram returns is bitwise symmetric, so KRR / KLR on it factorise by
+    Cholesky (rocSOLVER dpotrf), never by the per-column LU of an asymmetric K."""
+    from kmgram import _lib as L, encode as E, params as P
+    codes, lens = E.synthetic(700, 101, seed=17)
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
+                 L.KMG_F64)
+    assert np.array_equal(K, K.T)
+    y = np.where(np.random.default_rng(3).random(700) > 0.5, 1.0, -1.0)
+    got = ctx.krr_solve(K, y, 0.01)
+    assert ctx.last_factorisation() == "cholesky"
+    np.testing.assert_allclose(got, cpu_ref.krr_alpha(K, y, 0.01), rtol=1e-9, atol=1e-12)
+    ctx.klr_fit(K, y, 0.01, 1e-5, 3)
+    assert ctx.last_factorisation() == "cholesky"
+
+
+def test_factorisation_branches_reported(ctx):
+    """The three branches of the solve (Cholesky, LU of an asymmetric K, LU after a failed
+    Cholesky) are what kmg_last_factorisation reports."""
+    rng = np.random.default_rng(21)
+    n = 120
+    A = rng.standard_normal((n, 30))
+    K = A @ A.T / 30 + 0.5 * np.eye(n)
+    y = rng.standard_normal(n)
+    ctx.krr_solve(K, y, 0.1)
+    assert ctx.last_factorisation() == "cholesky"
+    Ka = K.copy()
+    Ka[5, 9] += 1e-12
+    ctx.krr_solve(Ka, y, 0.1)
+    assert ctx.last_factorisation() == "lu_asymmetric"
+    B = rng.standard_normal((n, n))
+    ctx.krr_solve((B + B.T) / 2, y, 0.0)
+    assert ctx.last_factorisation() == "lu_indefinite"

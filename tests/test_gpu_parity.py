@@ -152,38 +152,33 @@ def test_spectrum_long_sequences_unpacked(ctx):
 
 
 def _form(tune, form):
-    """"F" -> KMG_MM_FORM=F; "F:T" also KMG_PL_THREADS=T (pair lines, 512: two workgroups a CU,
-    1024: one; unset: by size) or KMG_NB_THREADS=T (neighbourhood lists); "4:T:L" also
-    KMG_NB_FILL=L (the list fill: 1 per list, 2 / 3 grouped by 4 / 16 lists)"""
+    """"F" -> KMG_MM_FORM=F; "4:T" also KMG_NB_THREADS=T (neighbourhood lists); "4:T:L" also
+    KMG_NB_FILL=L (the list fill: 1 sorted + packed, 2 grouped lane-per-run, 3 piece-assembled,
+    4 staged)"""
     f, _, rest = form.partition(":")
     t, _, fill = rest.partition(":")
-    tune(KMG_MM_FORM=f, KMG_PL_THREADS=(t or None) if f == "3" else None,
-         KMG_NB_THREADS=(t or None) if f == "4" else None,
+    tune(KMG_MM_FORM=f, KMG_NB_THREADS=(t or None) if f == "4" else None,
          KMG_NB_FILL=(fill or None) if f == "4" else None)
 
 
-@pytest.mark.parametrize("form", ["0", "3:1024", "3:512", "4:1024", "4:512"])
+@pytest.mark.parametrize("form", ["0", "4:1024:1", "4:1024:2", "4:512"])
 def test_mismatch_k9_n20000(ctx, tune, form):
     """BASELINE configs[2] workload: N=20000 mismatch (9,1), float64 normalised, bit-exact rows
-    (default formulation, the pair-lines table and the neighbourhood lists at both workgroup
-    sizes)."""
+    (default formulation: the neighbourhood lists, 16-bit from the staged fill -- a list is
+    read ~7 times here, too few to repay the packed segment 2's sort; the sorted fill with
+    packed segments 2; the grouped fill; 512-thread workgroups)."""
     _form(tune, form)
     codes, lens = E.synthetic(20000, 101, seed=3)
     K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens,
                  L.KMG_F64)
     plan = ctx.last_plan()
+    assert plan["formulation"] == "neighbourhood"
     if form.startswith("4"):
-        assert plan["formulation"] == "neighbourhood" and plan["threads"] == int(form[2:])
+        assert plan["threads"] == int(form.split(":")[1])
         assert plan["triangle"] == (plan["nchunks"] > 1)
-    elif form == "0":           # default at k = 9: the neighbourhood lists, one chunk
-        assert plan["formulation"] == "neighbourhood"
-        assert (plan["threads"], plan["nchunks"], plan["triangle"]) == (1024, 1, False)
-    else:
-        assert plan["formulation"] == "pair_lines"
-    if form == "3:512":         # 512 threads: 2 chunks of 10000, upper block triangle + mirror
-        assert (plan["threads"], plan["nchunks"], plan["chunk"], plan["triangle"]) == (512, 2, 10000, True)
-    elif form == "3:1024":      # 1024 threads: chunks of up to ~24000 columns (cost model)
-        assert plan["threads"] == 1024 and plan["triangle"] == (plan["nchunks"] > 1)
+        assert plan["packed"] == form.endswith(":1")
+    else:                       # default at k = 9: one chunk, 16-bit lists
+        assert (plan["threads"], plan["nchunks"], plan["triangle"], plan["packed"]) == (1024, 1, False, False)
     rows = [0, 1, 7777, 10000, 19999]
     for r in rows:
         ref = cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0]
@@ -195,21 +190,57 @@ def test_mismatch_k9_n20000(ctx, tune, form):
     assert np.array_equal(raw[:16].astype(np.int64), cref.mismatch_raw(codes[:3000], lens[:3000], 9, 1, rows=(0, 16)))
 
 
-@pytest.mark.parametrize("k", [4, 9, 12])
-@pytest.mark.parametrize("fill", ["1", "2", "3", "5", "6", "9", "10"])
+@pytest.mark.parametrize("k", [4, 8, 9, 12])
+@pytest.mark.parametrize("fill", ["0", "1", "2", "3", "4"])
 def test_mismatch_nb_fill_forms(ctx, tune, k, fill):
-    """The three neighbourhood-list fills (per list; grouped by the 4 / 16 lists sharing a
-    prefix, ranges staged in LDS) build the same lists: raw K bit-exact over several column
-    chunkings, one of them small enough to overflow the LDS range image (direct copies)."""
+    """The neighbourhood-list fills (0 auto -- 16-bit from k = 8: 600 rows read a list < 16
+    times --, 1 sorted with a packed segment 2, 2 grouped lane-per-run, 3 piece-
+    assembled, 4 staged 16-bit lists) build lists of the same K: raw K bit-exact
+    over several column chunkings; 40 poly-A rows make lists past every LDS buffer.  The
+    sorted fill refuses (KMG_EUNSUPPORTED) where segment 2 is too sparse to pack (k = 12);
+    elsewhere forcing it caps the chunk at the buffer's size (k = 4: ~130 columns)."""
     codes, lens = E.synthetic(600, 101, seed=90 + k)
     codes[:40] = 0  # poly-A rows: long runs, groups past the LDS image
     ref = cref.mismatch_raw(codes, lens, k, 1)
     tune(KMG_MM_FORM=4, KMG_NB_FILL=fill)
     for chunk in (("96", "20480") if k < 12 else ("20480",)):  # (k = 12: 4^12 bins a chunk)
         tune(KMG_MM_CHUNK=chunk)
-        raw = ctx.gram(P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
-                       L.KMG_I32)
+        params = P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0)
+        if fill == "1" and k == 12:  # ~300 columns between Hamming-2 entries: no packing
+            with pytest.raises(L.KmgError, match="sorted fill"):
+                ctx.gram(params, codes, lens, L.KMG_I32)
+            continue
+        raw = ctx.gram(params, codes, lens, L.KMG_I32)
         assert np.array_equal(raw.astype(np.int64), ref), chunk
+        if fill == "0" and k >= 8:  # a list read 600 x 94 / 4^k < 16 times: 16-bit
+            assert not ctx.last_plan()["packed"], chunk
+
+
+def _near_poly_a(n_poly, n_near, seed):
+    """n_poly poly-A rows, then n_near rows of A with a C every 4th position (their 9-mers
+    hold 2-3 C: Hamming 2 from A^9 and from each other), then random rows."""
+    codes, lens = E.synthetic(600, 101, seed=seed)
+    codes[:n_poly] = 0
+    near = np.zeros(101, dtype=codes.dtype)
+    near[::4] = 1
+    codes[n_poly:n_poly + n_near] = near
+    for r in range(n_near):  # shifted copies, so the windows differ between rows
+        codes[n_poly + r] = np.roll(near, r % 4)
+    return codes, lens
+
+
+@pytest.mark.parametrize("chunk", ["96", "600", "20480"])
+def test_mismatch_nb_sorted_spills_and_overflow(ctx, tune, chunk):
+    """The sorted fill's exits: lists whose segment 2 exceeds the per-wave LDS buffer (the
+    A^9 occurrences of 40 poly-A rows are 3720 Hamming-2 entries of every near-A k-mer's list)
+    stay 16-bit; runs of 15 spanning more than 254 columns (sparse, clustered columns) spill
+    into the 16-bit part.  Raw and normalised K bit-exact against the oracle."""
+    codes, lens = _near_poly_a(40, 40, 96)
+    tune(KMG_MM_FORM=4, KMG_NB_FILL="1", KMG_MM_CHUNK=chunk)
+    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
+    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1))
+    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
+    assert np.array_equal(K, cref.mismatch_rows(codes, lens, 9, 1))
 
 
 def test_mismatch_triangle_mirror_ragged_chunks(ctx, tune):
@@ -227,35 +258,15 @@ def test_mismatch_triangle_mirror_ragged_chunks(ctx, tune):
     assert np.array_equal(K, cref.mismatch_rows(codes, lens, 9, 1))
 
 
-@pytest.mark.parametrize("chunk", ["96", "20480"])
-def test_mismatch_nb_acc16(ctx, tune, chunk):
-    """16-bit LDS counters in the neighbourhood-list Gram (KMG_NB_ACC16): exact by the
-    Gram-matrix bound K_ij^2 <= K_ii K_jj.  20 poly-A rows (K_ii = 93 * 93 * 28) exceed it
-    against each other and take two 32-bit passes over column halves; the random rows, also
-    in chunks holding a poly-A column, stay 16-bit.  Raw and normalised K bit-exact."""
-    codes, lens = E.synthetic(600, 101, seed=98)
-    codes[:20] = 0
-    tune(KMG_MM_FORM=4, KMG_NB_ACC16=1, KMG_MM_CHUNK=chunk)
-    # a chunk narrower than the two-pass half width (5 columns: pass 0 takes them all)
-    raw5 = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes[17:22],
-                    lens[17:22], L.KMG_I32)  # rows 17..19 poly-A: two passes
-    assert np.array_equal(raw5.astype(np.int64), cref.mismatch_raw(codes[17:22], lens[17:22], 9, 1))
-    raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens, L.KMG_I32)
-    assert np.array_equal(raw.astype(np.int64), cref.mismatch_raw(codes, lens, 9, 1))
-    assert raw[0, 0] == 93 * 93 * 28
-    K = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), codes, lens, L.KMG_F64)
-    assert np.array_equal(K, cref.mismatch_rows(codes, lens, 9, 1))
-
-
-@pytest.mark.parametrize("cap", ["-1", "4096"])
-def test_mismatch_nb_piece_fill_fallbacks(ctx, tune, cap):
-    """The piece-assembled fill's two fallbacks: lists longer than its piece table (80 poly-A
-    rows: the A^9 list holds 7440 entries, 930 pieces) and groups whose range image overflows
-    the LDS (cap 4096: the poly-A groups) take the lane-per-run copies; raw K bit-exact."""
+@pytest.mark.parametrize("fill", ["3", "4"])
+def test_mismatch_nb_piece_fill_fallbacks(ctx, tune, fill):
+    """The piece-assembled and staged fills' fallback: lists longer than the piece table or
+    the per-wave LDS buffer (80 poly-A rows: the A^9 list holds 7440 entries, 930 pieces)
+    take the lane-per-run copies; raw K bit-exact."""
     codes, lens = E.synthetic(600, 101, seed=97)
     codes[:80] = 0
     ref = cref.mismatch_raw(codes, lens, 9, 1)
-    tune(KMG_MM_FORM=4, KMG_NB_FILL="9", KMG_NB_CAP=cap)
+    tune(KMG_MM_FORM=4, KMG_NB_FILL=fill)
     for chunk in ("96", "20480"):
         tune(KMG_MM_CHUNK=chunk)
         raw = ctx.gram(P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), codes, lens,
@@ -290,12 +301,12 @@ def test_mismatch_slots_k_range(ctx, tune, k):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["2", "3", "3:1024", "4", "4:512"])
+@pytest.mark.parametrize("form", ["2", "4", "4:512", "4::2"])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_mismatch_pairs_k_range(ctx, tune, k, form):
-    """Drop-two tables (2: pair table with per-group headers, 3: pair lines) and the
-    neighbourhood lists (4) at every compiled k, raw and normalised, over several column
-    chunkings (chunk = columns per group table / list set)."""
+    """The drop-two pair table (2) and the neighbourhood lists (4; 16-bit lists 4::2) at every
+    compiled k, raw and normalised, over several column chunkings (chunk = columns per group
+    table / list set)."""
     codes, lens = E.synthetic(500, 101, seed=80 + k)
     ref = cref.mismatch_raw(codes, lens, k, 1)
     _form(tune, form)
@@ -309,7 +320,7 @@ def test_mismatch_pairs_k_range(ctx, tune, k, form):
     assert np.array_equal(Kn, cref.mismatch_rows(codes, lens, k, 1))
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4", "4::1", "4::2", "4::3"])
+@pytest.mark.parametrize("form", ["1", "2", "4", "4::1", "4::2", "4::3"])
 def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     """Drop-one slots: groups longer than the 60 inline entries (CSR tail) and groups of
     >= 65535 entries (16-bit header overflow, CSR only).  Pair table: groups past 255
@@ -329,7 +340,7 @@ def test_mismatch_slots_overflow_and_big_groups(ctx, tune, form):
     assert np.array_equal(raw, raw.T)
 
 
-@pytest.mark.parametrize("form", ["1", "2", "3", "3:1024", "4", "4::1", "4::2", "4::3"])
+@pytest.mark.parametrize("form", ["1", "2", "4", "4::1", "4::2", "4::3"])
 def test_mismatch_stress_repeats(ctx, tune, form):
     _form(tune, form)
     codes, lens = E.synthetic(40, 101, seed=12)

@@ -14,5 +14,5 @@ for CTRS in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIV
   timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d "$OUT/p$i" -o run \
      -- python3 tools/time_mm.py "$CASES" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
-python3 tools/pmc_report.py "$OUT" gram_mm > "$OUT/report.txt"
+python3 tools/pmc_report.py "$OUT" "${KSUB:-gram_mm}" > "$OUT/report.txt"
 cat "$OUT/report.txt"

@@ -10,7 +10,7 @@ sys.path[:0] = [os.path.join(ROOT, "kernel-methods-for-genomics_amd"), os.path.j
 import numpy as np  # noqa: E402
 from kmgram import _lib as L, encode as E, params as P  # noqa: E402
 
-STAGES = ("count", "place", "fine", "pack", "lists", "slots", "diag", "gram", "mirror")
+STAGES = ("count", "place", "fine", "pack", "lists", "slots", "nbfill", "diag", "gram", "mirror")
 
 
 def main():
