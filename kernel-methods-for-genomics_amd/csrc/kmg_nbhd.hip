@@ -238,6 +238,33 @@ __device__ __forceinline__ void nb_load_range_offsets(const uint32_t *__restrict
   }
 }
 
+// the same offsets in two halves, so a group's loads can be in flight while the previous
+// group's lists are assembled: nb_ranges_issue (global -> registers) and nb_ranges_store
+template <int SW, int NT, int NLD>
+__device__ __forceinline__ void nb_ranges_issue(const uint32_t *__restrict__ xoff, int64_t cbase,
+                                                uint32_t P, const uint32_t *pm, int mr,
+                                                uint32_t (&v)[NLD]) {
+  const int tot = mr * (SW + 1);
+#pragma unroll
+  for (int t = 0; t < NLD; ++t) {
+    const int w = (int)threadIdx.x + t * NT;
+    v[t] = 0u;
+    if (w < tot) {
+      const int r = w / (SW + 1), q = w - r * (SW + 1);
+      v[t] = xoff[cbase + (int64_t)(P ^ pm[r]) * SW + q];
+    }
+  }
+}
+template <int SW, int NT, int NLD>
+__device__ __forceinline__ void nb_ranges_store(int mr, const uint32_t (&v)[NLD], uint32_t *roff) {
+  const int tot = mr * (SW + 1);
+#pragma unroll
+  for (int t = 0; t < NLD; ++t) {
+    const int w = (int)threadIdx.x + t * NT;
+    if (w < tot) roff[w] = v[t];
+  }
+}
+
 // ------------------------------------------------------------------ lane-per-run list copy
 // One wave builds list b (16-bit pieces, all three segments) of a group whose range offsets
 // are in LDS: the 352 runs in segment order, a wave prefix sum placing each run, lane-per-run
@@ -310,10 +337,16 @@ __host__ __device__ inline int nbs_table_words(int k) {
   const int nbn = 1 + 3 * k + 9 * k * (k - 1) / 2;
   return (nbn + mr + mr * 17 + 3) & ~3;
 }
-// per wave: the histogram (nbk words, 16-byte aligned) + the buffer (cap2 entries in 16-slot
-// rows of 15)
+// the staged fill's tables: nbs_table_words + a second range-offset buffer
+__host__ __device__ inline int nb_staged_table_words(int k) {
+  const int kp = k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
+  return (nbs_table_words(k) + mr * 17 + 3) & ~3;
+}
+// per wave: the histogram (nbk words, 16-byte aligned), segments 0 + 1 (NBS_S01 words), 64
+// trash words, the buffer (cap2 entries in 16-slot rows of 15)
+constexpr int NBS_S01 = 256;
 __host__ __device__ inline int nbs_wave_words(int nbk, int cap2) {
-  return ((nbk + 3) & ~3) + ((cap2 + 14) / 15) * 8;
+  return ((nbk + 3) & ~3) + NBS_S01 + 64 + ((cap2 + 14) / 15) * 8;
 }
 
 // segment 2 (n2 entries, column >> 6 order, runs of 15 in 16-slot rows at sb, 16-byte
@@ -403,86 +436,139 @@ __device__ __forceinline__ uint2 nb_pack_seg2(const uint16_t *sb, uint32_t n2, u
   return make_uint2(n16, nc - nfail);
 }
 
-// lane-level: run [srcp, srcp + cnt) of the index into LDS at od (any alignment); HIST also
-// counts each entry in the 64-column bucket histogram.  Two whole 16-byte pieces of the index
-// hold the run's first 16 - (srcp & 7) entries (>= 9; a run has ~7 at N=20000), shifted into
-// place by register selects (texture-address work is per load instruction: 2 a lane instead of
-// one per entry); longer runs finish with 2-byte loads.
-template <bool HIST>
-__device__ __forceinline__ void nb_run_to_lds(const uint16_t *__restrict__ xent, uint32_t srcp,
-                                              uint32_t cnt, uint16_t *od, uint32_t *hist) {
-  if (cnt == 0) return;
-  const uint32_t a = srcp & 7u;
-  const uint4 *pp = (const uint4 *)(xent + (srcp - a));
-  const uint4 p0 = pp[0];
-  const uint4 p1 = a + cnt > 8u ? pp[1] : make_uint4(0u, 0u, 0u, 0u);
-  const uint32_t w[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, 0u, 0u, 0u, 0u};
-  const uint32_t ad = a >> 1;
-  uint32_t o[8];
+typedef uint32_t nb_u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+
+struct NbStaged {
+  uint32_t *dst;    // LDS words the run's destination entries are counted from
+  uint32_t w[12];   // raw index words from base
+  uint32_t dpos;    // destination entry
+  uint32_t sh;      // source entry parity vs destination (0 / 1)
+  uint32_t cm;      // entries moved through the words (the rest: 2-byte copies)
+  uint32_t cnt, srcp;
+};
+
+__device__ __forceinline__ void nb_staged_load(NbStaged &r, const uint16_t *__restrict__ xent,
+                                               uint32_t srcp, uint32_t cnt, uint32_t *dst,
+                                               uint32_t dpos) {
+  r.dst = dst;
+  r.dpos = dpos;
+  r.cnt = cnt;
+  r.srcp = srcp;
+  const uint32_t odd = dpos & 1u;
+  r.cm = 0;
+  r.sh = 0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint32_t lo = ad == 0 ? w[q] : ad == 1 ? w[q + 1] : ad == 2 ? w[q + 2] : w[q + 3];
-    const uint32_t hi = ad == 0 ? w[q + 1] : ad == 1 ? w[q + 2] : ad == 2 ? w[q + 3] : w[q + 4];
-    o[q] = (a & 1u) ? __builtin_amdgcn_alignbyte(hi, lo, 2) : lo;
-  }
-  const uint32_t nfit = min(cnt, 16u - a);
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    if ((uint32_t)e < nfit) {
-      const uint32_t v = (o[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
-      od[e] = (uint16_t)v;
-      if (HIST) atomicAdd(&hist[v >> NBS_BSH], 1u);
-    }
-  }
-  for (uint32_t e = nfit; e < cnt; ++e) {
-    const uint32_t v = xent[srcp + e];
-    od[e] = (uint16_t)v;
-    if (HIST) atomicAdd(&hist[v >> NBS_BSH], 1u);
-  }
+  for (int q = 0; q < 12; ++q) r.w[q] = 0u;
+  if (cnt == 0 || srcp < odd) return;  // (srcp < odd: the index's first entry at an odd slot)
+  const uint32_t s0 = srcp - odd;      // source entry of the destination word boundary
+  const uint32_t sh = s0 & 1u, base = s0 - sh;
+  const uint32_t nq = 12u - sh;        // whole shifted words the 3 loads hold
+  const uint32_t cm = min(cnt, 2u * nq - odd);
+  const uint32_t end = sh + odd + cm;  // raw halfwords used
+  const nb_u32x4 *pp = (const nb_u32x4 *)(xent + base);
+  const nb_u32x4 z = {0u, 0u, 0u, 0u};
+  const nb_u32x4 p0 = pp[0];
+  const nb_u32x4 p1 = end > 8u ? pp[1] : z;
+  const nb_u32x4 p2 = end > 16u ? pp[2] : z;
+  r.w[0] = p0.x; r.w[1] = p0.y; r.w[2] = p0.z; r.w[3] = p0.w;
+  r.w[4] = p1.x; r.w[5] = p1.y; r.w[6] = p1.z; r.w[7] = p1.w;
+  r.w[8] = p2.x; r.w[9] = p2.y; r.w[10] = p2.z; r.w[11] = p2.w;
+  r.sh = sh;
+  r.cm = cm;
 }
 
+__device__ __forceinline__ void nb_staged_write(const NbStaged &r, const uint16_t *__restrict__ xent,
+                                                uint32_t *trash) {
+  const uint32_t odd = r.dpos & 1u, wd = r.dpos >> 1, end = odd + r.cm;  // end: halfwords
+  uint32_t *sb32 = r.dst;
+  uint16_t *sb16 = (uint16_t *)sb32;
+  uint32_t o[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q)
+    o[q] = r.sh ? __builtin_amdgcn_alignbyte(q + 1 < 12 ? r.w[q + 1] : 0u, r.w[q], 2) : r.w[q];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    const bool full = (uint32_t)q >= odd && 2u * (uint32_t)q + 2u <= end;
+    *(full ? sb32 + wd + (uint32_t)q : trash) = o[q];
+  }
+  // the two half words: the head (odd destination start) and the tail (odd end)
+  const bool head = odd && r.cm > 0;
+  *(head ? sb16 + r.dpos : (uint16_t *)trash) = (uint16_t)(o[0] >> 16);
+  const uint32_t qt = (end - 1u) >> 1;
+  uint32_t tv = o[0];
+#pragma unroll
+  for (int q = 1; q < 12; ++q) tv = qt == (uint32_t)q ? o[q] : tv;
+  const bool tail = (end & 1u) && r.cm > 0;
+  *(tail ? sb16 + 2u * wd + end - 1u : (uint16_t *)trash) = (uint16_t)tv;
+  // the rest of a long run (or a run the words cannot start): 2-byte copies
+  for (uint32_t e = r.cm; e < r.cnt; ++e) sb16[r.dpos + e] = xent[r.srcp + e];
+}
+
+template <int K>
 __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
-    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
     uint16_t *__restrict__ table, uint32_t pad_col, int cap2, int nbk) {
   constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  constexpr int kp = K - S;
+  constexpr int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  constexpr int nbn = 1 + 3 * K + 9 * K * (K - 1) / 2;
+  constexpr int NIT = (nbn + 63) / 64;
+  constexpr int t2 = 1 + 3 * K;  // first Hamming-2 run (< 64 for k <= 21)
+  constexpr int NLD = (mr * (SW + 1) + NT - 1) / NT;
   extern __shared__ __align__(16) uint32_t fsm[];
-  const int kp = k - S;
-  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
-  const int nbn = nb_neighbours(k);
   uint32_t *rt = fsm;                        // [nbn] run j: r | suffix xor << 16 | class << 24
   uint32_t *pm = rt + nbn;                   // [mr] prefix xor of range r
-  uint32_t *roff = pm + mr;                  // [mr][SW + 1] absolute index offsets
+  uint32_t *roffs = pm + mr;                 // [2][mr][SW + 1] absolute index offsets
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t *hist = fsm + nbs_table_words(k) + wave * nbs_wave_words(nbk, cap2);  // [nbk]
-  uint16_t *sbuf = (uint16_t *)(hist + ((nbk + 3) & ~3));                      // 16-byte aligned
+  uint32_t *hist = fsm + nb_staged_table_words(K) + wave * nbs_wave_words(nbk, cap2);  // [nbk]
+  uint32_t *s01 = hist + ((nbk + 3) & ~3);   // segments 0 and 1 (NBS_S01 words)
+  uint32_t *trash = s01 + NBS_S01 + lane;    // 64 words
+  uint32_t *sb32 = s01 + NBS_S01 + 64;       // segment 2 (16-byte aligned)
+  uint16_t *sbuf = (uint16_t *)sb32;
   const uint32_t npref = 1u << (2 * kp);
-  nb_group_tables<S>(k, NT, rt, pm);
+  nb_group_tables<S>(K, NT, rt, pm);
   __syncthreads();
-  const int t2 = 1 + 3 * k;  // first Hamming-2 run (< 64 for k <= 21)
-  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
-    const int64_t cbase = (gi - P) * SW;  // chunk c's first bin: c * 4^k
-    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;  // all 16 lists empty (uniform)
-    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
-    __syncthreads();
+  auto group_base = [&](int64_t gi, uint32_t &P) {
+    P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    return (gi - P) * SW;  // chunk c's first bin: c * 4^k
+  };
+  uint32_t v[NLD];
+  int64_t gi = blockIdx.x;
+  if (gi < ngroups) {
+    uint32_t P;
+    const int64_t cb = group_base(gi, P);
+    nb_ranges_issue<SW, NT, NLD>(xoff, cb, P, pm, mr, v);
+    nb_ranges_store<SW, NT, NLD>(mr, v, roffs);
+  }
+  __syncthreads();
+  for (int par = 0; gi < ngroups; gi += gridDim.x, par ^= 1) {
+    uint32_t P;
+    const int64_t cbase = group_base(gi, P);
+    const uint32_t *roff = roffs + par * mr * (SW + 1);
+    const int64_t gn = gi + gridDim.x;
+    if (gn < ngroups) {  // the next group's range offsets: in flight during this group
+      uint32_t Pn;
+      const int64_t cbn = group_base(gn, Pn);
+      nb_ranges_issue<SW, NT, NLD>(xoff, cbn, Pn, pm, mr, v);
+    }
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
       if (tot == 0) continue;  // wave-uniform
       const uint2 sg = nbseg[b];
       uint16_t *dst = table + (size_t)start * 8u;
-      if ((tot - sg.y) * 8u > (uint32_t)cap2) {  // segment 2 past the buffer: 16-bit lists
-        nb_list_lane_per_run(k, su, rt, roff, xent, tot, sg, dst, pad_col);
+      // segment 2 past the buffer, or segments 0 + 1 past theirs: 16-bit lists
+      if ((tot - sg.y) * 8u > (uint32_t)cap2 || sg.y * 8u > 2u * NBS_S01) {
+        nb_list_lane_per_run(K, su, rt, roff, xent, tot, sg, dst, pad_col);
         if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
         continue;
       }
       for (int q = lane; q < nbk; q += 64) hist[q] = 0u;
-      nb_wave_sync();
-      // ---- 1. runs: segments 0 / 1 to the table, segment 2 to the buffer (+ histogram)
+      // ---- 1. runs: segments 0 / 1 to s01 at their list positions, segment 2 to the buffer
       uint32_t carry = 0, n0 = 0, pre2 = 0;
-      for (int j0 = 0; j0 < nbn; j0 += 64) {
-        const int j = j0 + lane;
+      auto stage = [&](int it, NbStaged &r) {
+        const int j = it * 64 + lane;
         uint32_t cnt = 0, srcp = 0, h = 2;
         if (j < nbn) {
           const uint32_t d = rt[j];
@@ -494,16 +580,21 @@ __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
         }
         const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
         const uint32_t pos = carry + inc - cnt;
-        if (j0 == 0) {
+        if (it == 0) {
           n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
           pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);
         }
         carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        if (h < 2) {
-          nb_copy_run(dst + (h == 0 ? 0u : sg.x * 8u - n0) + pos, xent + srcp, cnt);
-        } else {
-          nb_run_to_lds<true>(xent, srcp, cnt, sbuf + (pos - pre2), hist);
-        }
+        if (h < 2) nb_staged_load(r, xent, srcp, cnt, s01, (h == 0 ? 0u : sg.x * 8u - n0) + pos);
+        else nb_staged_load(r, xent, srcp, cnt, sb32, pos - pre2);
+      };
+      NbStaged cur, nxt;
+      stage(0, cur);
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        if (it + 1 < NIT) stage(it + 1, nxt);
+        nb_staged_write(cur, xent, trash);
+        if (it + 1 < NIT) cur = nxt;
       }
       const uint32_t n2 = carry - pre2;
       // dummy columns after segments 0 and 1
@@ -513,47 +604,53 @@ __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
         const uint32_t segn = sgi == 0 ? n0 : pre2 - n0;
         const uint32_t segend = sgi == 0 ? sg.x * 8u : sg.y * 8u;
         const uint32_t pp = segb + segn + (uint32_t)e;
-        if (pp < segend) dst[pp] = nb_dummy(pad_col, pp);
+        if (pp < segend) ((uint16_t *)s01)[pp] = nb_dummy(pad_col, pp);
+      }
+      nb_wave_sync();
+      // segments 0 and 1 out (16-byte stores); segment 2 into registers + its histogram
+      if ((uint32_t)lane < sg.y) ((uint4 *)dst)[lane] = ((const uint4 *)s01)[lane];
+      for (uint32_t q = 64u + (uint32_t)lane; q < sg.y; q += 64u) ((uint4 *)dst)[q] = ((const uint4 *)s01)[q];
+      uint2 rv[NBS_RW];
+#pragma unroll
+      for (int r = 0; r < NBS_RW; ++r) {
+        const uint32_t e = 256u * (uint32_t)r + 4u * (uint32_t)lane;
+        rv[r] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (e < n2) {
+          rv[r] = *(const uint2 *)(sbuf + e);
+          // entries past n2 in the last read: no entry (0xFFFF; columns < 65408)
+          if (e + 1 >= n2) rv[r].x |= 0xFFFF0000u;
+          if (e + 2 >= n2) rv[r].y |= 0x0000FFFFu;
+          if (e + 3 >= n2) rv[r].y |= 0xFFFF0000u;
+          const uint32_t c4[4] = {rv[r].x & 0xFFFFu, rv[r].x >> 16, rv[r].y & 0xFFFFu, rv[r].y >> 16};
+#pragma unroll
+          for (int hh = 0; hh < 4; ++hh)
+            if (c4[hh] != 0xFFFFu) atomicAdd(&hist[c4[hh] >> NBS_BSH], 1u);
+        }
       }
       nb_wave_sync();
       // ---- 2. bucket starts
       {
         const int per = (nbk + 63) >> 6, lo = lane * per, hi = min(nbk, lo + per);
-        uint32_t s = 0;
-        for (int q = lo; q < hi; ++q) s += hist[q];
-        uint32_t run = nb_wave_incl_scan_dpp(s) - s;
+        uint32_t sum = 0;
+        for (int q = lo; q < hi; ++q) sum += hist[q];
+        uint32_t run = nb_wave_incl_scan_dpp(sum) - sum;
         for (int q = lo; q < hi; ++q) {
           const uint32_t t = hist[q];
           hist[q] = run;
           run += t;
         }
       }
-      // ---- 3. counting sort through registers (0xFFFF: no entry; columns < 65408)
-      {
-        uint2 rv[NBS_RW];
+      nb_wave_sync();
+      // ---- 3. counting sort from the registers: entry -> slot p + p / 15 of its position p
 #pragma unroll
-        for (int r = 0; r < NBS_RW; ++r) {
-          const uint32_t e = 256u * (uint32_t)r + 4u * (uint32_t)lane;
-          rv[r] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-          if (e < n2) {
-            rv[r] = *(const uint2 *)(sbuf + e);
-            // entries past n2 in the last read: no entry
-            if (e + 1 >= n2) rv[r].x |= 0xFFFF0000u;
-            if (e + 2 >= n2) rv[r].y |= 0x0000FFFFu;
-            if (e + 3 >= n2) rv[r].y |= 0xFFFF0000u;
-          }
-        }
-        nb_wave_sync();
+      for (int r = 0; r < NBS_RW; ++r) {
+        if (256u * (uint32_t)r < n2) {  // wave-uniform
+          const uint32_t c4[4] = {rv[r].x & 0xFFFFu, rv[r].x >> 16, rv[r].y & 0xFFFFu, rv[r].y >> 16};
 #pragma unroll
-        for (int r = 0; r < NBS_RW; ++r) {
-          if (256u * (uint32_t)r < n2) {  // wave-uniform
-            const uint32_t c4[4] = {rv[r].x & 0xFFFFu, rv[r].x >> 16, rv[r].y & 0xFFFFu, rv[r].y >> 16};
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              if (c4[h] != 0xFFFFu) {
-                const uint32_t p = atomicAdd(&hist[c4[h] >> NBS_BSH], 1u);
-                sbuf[p + p / 15u] = (uint16_t)c4[h];
-              }
+          for (int hh = 0; hh < 4; ++hh) {
+            if (c4[hh] != 0xFFFFu) {
+              const uint32_t p = atomicAdd(&hist[c4[hh] >> NBS_BSH], 1u);
+              sbuf[p + p / 15u] = (uint16_t)c4[hh];
             }
           }
         }
@@ -562,58 +659,87 @@ __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
       // ---- 4. pack
       const uint2 us = nb_pack_seg2(sbuf, n2, dst, sg.y, pad_col);
       if (lane == 0) nbuse[b] = us;
-      nb_wave_sync();  // the next list reuses the histogram and the buffer
+      nb_wave_sync();  // the next list reuses the histogram and the buffers
     }
-    __syncthreads();  // the next group overwrites the range offsets
+    if (gn < ngroups) nb_ranges_store<SW, NT, NLD>(mr, v, roffs + (par ^ 1) * mr * (SW + 1));
+    __syncthreads();  // the next group reads the other range buffer
   }
 }
 
 
 // ------------------------------------------------------------------ staged 16-bit fill
 // The 16-bit lists through LDS: one wave a list assembles the whole list (three segments,
-// dummy tails) in a per-wave LDS buffer from 16-byte piece loads of the index
-// (nb_run_to_lds), then writes it with 16-byte stores, 1 KB a wave instruction -- against
-// two 2-byte texture-address operations an entry for the lane-per-run copies (~25 TA cycles
-// an instruction: the grouped fill is TA-bound, profiles/r04t_pmc_fill.txt, r05k).  Lists past
-// the buffer take the lane-per-run copies.
+// dummy tails) in a per-wave LDS buffer, then writes it with 16-byte stores (1 KB a wave
+// instruction).  Lane j moves run j: three dword-aligned 16-byte loads of the index (the
+// index is 2-byte entries; a dwordx4 load needs 4-byte alignment only) starting at the entry
+// that lands on a destination word boundary, a 2-byte register shift when source and
+// destination parities differ, then 32-bit LDS writes of the words whose halves are both the
+// run's and 16-bit writes at its two ends -- ~9 LDS writes and 3 texture-address operations a
+// run of ~7 entries, against 2 x 7 2-byte global operations for the lane-per-run copies
+// (~25 TA cycles an instruction: the grouped fill is TA-bound, profiles/r04t_pmc_fill.txt).
+// Writes that a lane does not need go to its own trash word (no exec-mask branching).  The
+// runs of iteration i + 1 are loaded before iteration i's writes.  Lists past the buffer take
+// the lane-per-run copies.
+template <int K>
 __global__ __launch_bounds__(1024) void nb_fill_staged_kernel(
-    int k, int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
+    int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
     uint16_t *__restrict__ table, uint32_t pad_col, int cap16) {
   constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  constexpr int kp = K - S;
+  constexpr int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
+  constexpr int nbn = 1 + 3 * K + 9 * K * (K - 1) / 2;
+  constexpr int NIT = (nbn + 63) / 64;
+  constexpr int t2 = 1 + 3 * K;
   extern __shared__ __align__(16) uint32_t fsm[];
-  const int kp = k - S;
-  const int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
-  const int nbn = nb_neighbours(k);
+  constexpr int NLD = (mr * (SW + 1) + NT - 1) / NT;
   uint32_t *rt = fsm;
   uint32_t *pm = rt + nbn;
-  uint32_t *roff = pm + mr;
+  uint32_t *roffs = pm + mr;  // [2][mr][SW + 1]: this group's and the next one's
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint16_t *sbuf = (uint16_t *)(fsm + nbs_table_words(k) + wave * (cap16 / 2));  // 16-byte aligned
+  uint32_t *sb32 = fsm + nb_staged_table_words(K) + wave * (cap16 / 2);  // 16-byte aligned
+  uint32_t *trash = sb32 + cap16 / 2 - 64 + lane;                  // the buffer's last 64 words
+  const uint32_t lcap = (uint32_t)cap16 - 128u;                    // entries a list may use
   const uint32_t npref = 1u << (2 * kp);
-  nb_group_tables<S>(k, NT, rt, pm);
+  nb_group_tables<S>(K, NT, rt, pm);
   __syncthreads();
-  const int t2 = 1 + 3 * k;
-  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const uint32_t P = (uint32_t)(gi & (int64_t)(npref - 1u));
-    const int64_t cbase = (gi - P) * SW;
-    if (nboff[gi * SW + SW] == nboff[gi * SW]) continue;
-    nb_load_range_offsets<SW, NT>(xoff, cbase, P, pm, mr, roff);
-    __syncthreads();
+  auto group_base = [&](int64_t gi, uint32_t &P) {
+    P = (uint32_t)(gi & (int64_t)(npref - 1u));
+    return (gi - P) * SW;
+  };
+  uint32_t v[NLD];
+  int64_t gi = blockIdx.x;
+  if (gi < ngroups) {
+    uint32_t P;
+    const int64_t cb = group_base(gi, P);
+    nb_ranges_issue<SW, NT, NLD>(xoff, cb, P, pm, mr, v);
+    nb_ranges_store<SW, NT, NLD>(mr, v, roffs);
+  }
+  __syncthreads();
+  for (int par = 0; gi < ngroups; gi += gridDim.x, par ^= 1) {
+    uint32_t P;
+    const int64_t cbase = group_base(gi, P);
+    const uint32_t *roff = roffs + par * mr * (SW + 1);
+    const int64_t gn = gi + gridDim.x;
+    if (gn < ngroups) {  // the next group's range offsets: in flight during this group
+      uint32_t Pn;
+      const int64_t cbn = group_base(gn, Pn);
+      nb_ranges_issue<SW, NT, NLD>(xoff, cbn, Pn, pm, mr, v);
+    }
     for (int su = wave; su < SW; su += NW) {
       const int64_t b = cbase + (int64_t)P * SW + su;
       const uint32_t start = nboff[b], tot = nboff[b + 1] - start;
       if (tot == 0) continue;  // wave-uniform
       const uint2 sg = nbseg[b];
       uint16_t *dst = table + (size_t)start * 8u;
-      if (tot * 8u > (uint32_t)cap16) {
-        nb_list_lane_per_run(k, su, rt, roff, xent, tot, sg, dst, pad_col);
+      if (tot * 8u > lcap) {
+        nb_list_lane_per_run(K, su, rt, roff, xent, tot, sg, dst, pad_col);
         if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
         continue;
       }
       uint32_t carry = 0, n0 = 0, pre2 = 0;
-      for (int j0 = 0; j0 < nbn; j0 += 64) {
-        const int j = j0 + lane;
+      auto stage = [&](int it, NbStaged &r) {
+        const int j = it * 64 + lane;
         uint32_t cnt = 0, srcp = 0, h = 2;
         if (j < nbn) {
           const uint32_t d = rt[j];
@@ -625,13 +751,21 @@ __global__ __launch_bounds__(1024) void nb_fill_staged_kernel(
         }
         const uint32_t inc = nb_wave_incl_scan_dpp(cnt);
         const uint32_t pos = carry + inc - cnt;
-        if (j0 == 0) {
+        if (it == 0) {
           n0 = (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0);
           pre2 = (uint32_t)__builtin_amdgcn_readlane((int)pos, t2 & 63);
         }
         carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         const uint32_t dpos = (h == 0 ? 0u : h == 1 ? sg.x * 8u - n0 : sg.y * 8u - pre2) + pos;
-        nb_run_to_lds<false>(xent, srcp, cnt, sbuf + dpos, nullptr);
+        nb_staged_load(r, xent, srcp, cnt, sb32, dpos);
+      };
+      NbStaged cur, nxt;
+      stage(0, cur);
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        if (it + 1 < NIT) stage(it + 1, nxt);
+        nb_staged_write(cur, xent, trash);
+        if (it + 1 < NIT) cur = nxt;
       }
       const uint32_t total = carry;
       if (lane < 24) {  // dummy columns after each segment
@@ -640,13 +774,14 @@ __global__ __launch_bounds__(1024) void nb_fill_staged_kernel(
         const uint32_t segn = sgi == 0 ? n0 : sgi == 1 ? pre2 - n0 : total - pre2;
         const uint32_t segend = sgi == 0 ? sg.x * 8u : sgi == 1 ? sg.y * 8u : tot * 8u;
         const uint32_t pp = segb + segn + (uint32_t)e;
-        if (pp < segend) sbuf[pp] = nb_dummy(pad_col, pp);
+        if (pp < segend) ((uint16_t *)sb32)[pp] = nb_dummy(pad_col, pp);
       }
       nb_wave_sync();
-      for (uint32_t q = (uint32_t)lane; q < tot; q += 64u) ((uint4 *)dst)[q] = ((const uint4 *)sbuf)[q];
+      for (uint32_t q = (uint32_t)lane; q < tot; q += 64u) ((uint4 *)dst)[q] = ((const uint4 *)sb32)[q];
       if (lane == 0) nbuse[b] = make_uint2(tot, 0u);
       nb_wave_sync();  // the next list reuses the buffer
     }
+    if (gn < ngroups) nb_ranges_store<SW, NT, NLD>(mr, v, roffs + (par ^ 1) * mr * (SW + 1));
     __syncthreads();
   }
 }
@@ -1132,12 +1267,13 @@ int nb_sorted_cap(int k, int pmax, int chunk) {
   // runs still fit; k = 10 (28 columns) would spill nearly every run
   if (dens < 1.0 / 12.0) return 0;
   const int nbk = (chunk + (1 << NBS_BSH) - 1) >> NBS_BSH;
-  const int64_t per_wave = (160 * 1024 / 4 - nbs_table_words(k)) / 16;  // words, 16 waves
+  const int64_t per_wave = (160 * 1024 / 4 - nb_staged_table_words(k)) / 16;  // words, 16 waves
   // buffer words a wave: 8 a row of 15 entries
-  const int64_t rows = (per_wave - ((nbk + 3) & ~3)) / 8;
+  const int64_t rows = (per_wave - ((nbk + 3) & ~3) - NBS_S01 - 64) / 8;
   int64_t cap = std::min<int64_t>(rows * 15, NBS_MAXCAP);
-  // the buffer holds segment 2 of a list of the mean + 25 % (longer lists stay 16-bit)
-  if (cap <= 0 || (double)cap < 1.25 * dens * chunk) return 0;
+  // the buffer holds segment 2 of a list of the mean + 10 % (a sum of ~320 runs: sizes stay
+  // within a few % of the mean; a longer list stays 16-bit)
+  if (cap <= 0 || (double)cap < 1.1 * dens * chunk + 64) return 0;
   return (int)(cap & ~7LL);
 }
 
@@ -1176,23 +1312,43 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
   if ((form == 0 || form == 1) && cap > 0) {
     // sorted fill, packed segment 2 (the Gram reads ~0.6x the bytes of 16-bit lists)
     const int nbk = (g.chunk + (1 << NBS_BSH) - 1) >> NBS_BSH;
-    const size_t lds = 4 * ((size_t)nbs_table_words(g.k) + 16 * (size_t)nbs_wave_words(nbk, cap));
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds = 4 * ((size_t)nb_staged_table_words(g.k) + 16 * (size_t)nbs_wave_words(nbk, cap));
+    if (lds > 160 * 1024 || (((uintptr_t)xent) & 3u) != 0) return hipErrorInvalidValue;
     const int64_t blocks = std::min<int64_t>(ngroups, 256);
-    hipLaunchKernelGGL(nb_fill_sorted_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
-                       ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap, nbk);
+    switch (g.k) {
+#define KMG_NB_SORTED(KK)                                                                        \
+  case KK:                                                                                       \
+    hipLaunchKernelGGL(nb_fill_sorted_kernel<KK>, dim3((unsigned)blocks), dim3(1024), lds, s,    \
+                       ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap, nbk);      \
+    break;
+      KMG_NB_SORTED(4) KMG_NB_SORTED(5) KMG_NB_SORTED(6) KMG_NB_SORTED(7) KMG_NB_SORTED(8)
+      KMG_NB_SORTED(9) KMG_NB_SORTED(10) KMG_NB_SORTED(11) KMG_NB_SORTED(12)
+#undef KMG_NB_SORTED
+      default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   if (form == 1) return hipErrorInvalidValue;  // forced sorted fill where it cannot run
   if (form == 0 || form == 4 || form == 5) {
     // staged 16-bit fill: the whole list in a per-wave LDS buffer, 16-byte stores
-    const int cap16 = ((160 * 1024 / 4 - nbs_table_words(g.k)) / 16 * 2) & ~7;
+    // (lists are sums of ~350 runs: their sizes stay within a few % of the mean; the rare
+    // longer one takes the lane-per-run copies)
+    const int cap16 = ((160 * 1024 / 4 - nb_staged_table_words(g.k)) / 16 * 2) & ~7;
     const double mean_list = (double)(1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2) * mean;
-    if (cap16 >= 1.25 * mean_list + 64) {
-      const size_t lds = 4 * ((size_t)nbs_table_words(g.k) + 16 * (size_t)(cap16 / 2));
+    if (cap16 >= 1.08 * mean_list + 192 && (((uintptr_t)xent) & 3u) == 0) {
+      const size_t lds = 4 * ((size_t)nb_staged_table_words(g.k) + 16 * (size_t)(cap16 / 2));
       const int64_t blocks = std::min<int64_t>(ngroups, 256);
-      hipLaunchKernelGGL(nb_fill_staged_kernel, dim3((unsigned)blocks), dim3(1024), lds, s, g.k,
-                         ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16);
+      switch (g.k) {
+#define KMG_NB_STAGED(KK)                                                                        \
+  case KK:                                                                                       \
+    hipLaunchKernelGGL(nb_fill_staged_kernel<KK>, dim3((unsigned)blocks), dim3(1024), lds, s,    \
+                       ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16);         \
+    break;
+        KMG_NB_STAGED(4) KMG_NB_STAGED(5) KMG_NB_STAGED(6) KMG_NB_STAGED(7) KMG_NB_STAGED(8)
+        KMG_NB_STAGED(9) KMG_NB_STAGED(10) KMG_NB_STAGED(11) KMG_NB_STAGED(12)
+#undef KMG_NB_STAGED
+        default: return hipErrorInvalidValue;
+      }
       return hipGetLastError();
     }
     if (form == 4) return hipErrorInvalidValue;
