@@ -819,7 +819,8 @@ def _compact_record(rec):
     out["stages_ms"] = {k: _r(st[k]) for k in _STAGE_KEYS if k in st}
     pl = rec.get("plan") or {}
     if pl:
-        out["plan"] = {k: pl.get(k) for k in ("formulation", "nchunks", "chunk", "triangle")}
+        out["plan"] = {k: pl.get(k) for k in ("formulation", "nchunks", "chunk", "triangle", "packed")
+                       if k in pl}
     for k in ("hbm_frac_of_gram_and_mirror", "gram_hbm_frac"):
         if k in rec:
             out[k] = _r(rec[k])
@@ -996,11 +997,8 @@ def main():
             "N": args.mm_n, "value": mm["pairs_per_s"], "unit": "Gram pairs/s",
             "ms_per_step": mm["ms_per_step"], "stages_ms": mm["stages_ms"], "plan": mm["plan"],
             "hbm_frac_of_gram_and_mirror": mm_bytes / (mm_k_ms / 1e3) / HBM_PEAK,
-            # the kernel's other bound: random 128-B posting lines from the Infinity Cache.
-            # N <= 24000 runs the pair-lines table: per row window and chunk 27 uniform
-            # groups of E[ceil(X / 64)] lines and 9 correction groups of E[ceil((8 + X) / 64)],
-            # X ~ Poisson(16 * chunk * 93 / 4^9) (kmg_pairs.hip); the slot table above that
-            # (117 one-line lists per window and chunk)
+            # the Gram launch against HBM: the neighbourhood lists' bytes (mm_nbhd_roofline;
+            # the slot table's model, random 128-B lines, if a KMG_MM_FORM forces it)
             "gather_roofline": mm_gather_roofline(args.mm_n, mm_rows_launch,
                                                   mm["stages_ms"]["gram"], mm["plan"]),
             "spot_check": mm["spot_check"],

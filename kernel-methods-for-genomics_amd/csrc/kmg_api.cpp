@@ -799,17 +799,18 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   const bool mm = p->kind == KMG_MISMATCH;
   const int k = p->k;
   const bool exact = !mm || p->m == 0;  // spectrum-shaped: only ham 0 counts
-  // mismatch m = 1, auto:
-  //   k = 9 (BASELINE configs[2] and [4]): the neighbourhood lists at every n (N=20000
-  //     normalised build 4.03 -> 3.73 ms, N=200000 one-GPU raw K 185.5 -> 134.8 ms against
-  //     round 3's pair lines / slot table; profiles/r04_nb_*)
-  //   k = 10, 11: the drop-two pair table (k = 10: 4.74 vs 5.98 ms slots; round 2);
-  //   k = 8 and 12: the drop-one slot table (k = 8: 6.70 vs 7.78 pair lines, 15.8 pairs).
+  // mismatch m = 1, auto (N=20000, float64 normalised, profiles/r05s_kforms.jsonl):
+  //   k = 8..10: the neighbourhood lists (k = 8: 4.17 ms vs 6.71 slot table, 15.9 pair
+  //     table; k = 9: 2.9-3.1 ms; k = 10: 4.14 vs 6.13 / 4.95);
+  //   k = 11: the drop-two pair table (8.59 vs 9.11 slots; the lists' fill of 4^11 bins a
+  //     chunk alone takes 11.5 ms);
+  //   k = 12: the drop-one slot table (14.5 ms; the pair table's offsets overflow at N=20000).
+  //   k < 8: the dense count-vector GEMM where counts fit (dense_ok), else all-pairs Hamming.
   const int form = t.mm_form;
   const bool s1 = mm && p->m == 1;
-  const bool use_nb = s1 && k >= 4 && k <= 12 && (form == 4 || (form == 0 && k == 9));
+  const bool use_nb = s1 && k >= 4 && k <= 12 && (form == 4 || (form == 0 && k >= 8 && k <= 10));
   const bool use_pairs = s1 && !use_nb &&
-                         (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k >= 10 && k <= 11));
+                         (form == 2 ? (k >= 3 && k <= 12) : (form == 0 && k == 11));
   const bool use_slots = s1 && !use_pairs && !use_nb && k >= 8 && k <= 12 && form != 2;
   const bool use_index = (exact && k <= 12) || use_slots || use_pairs || use_nb;
   // formulation: dense int8 MFMA GEMM over 4^k count columns for small k (exact when
@@ -1101,6 +1102,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         o.tri = tri_esz > 0 && g.nchunks > 1;
         note_plan(nbt);
         c->plan[5] = (sorted && nb_sorted_cap(k, g.pmax, g.chunk) > 0) ? 1 : 0;
+        if (nb_gram_lds(g, pkd) > 160 * 1024)  // (very long windows: the row table alone)
+          return fail(KMG_EUNSUPPORTED, "neighbourhood lists: %zu B of LDS at %d windows a row "
+                      "(KMG_MM_FORM=1 or 2: the slot / pair tables)", nb_gram_lds(g, pkd), g.pmax);
         KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
         const int64_t nbins = g.nbins();
         const int64_t bound = nb_list_entries_bound(k, n * (int64_t)g.pmax, nbins);

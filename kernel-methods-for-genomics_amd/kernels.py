@@ -353,7 +353,7 @@ def rec(func):
 
     @functools.wraps(func)
     def recd(*args):
-        key = "-".join("[%s]" % (a,) for a in args)
+        key = "-".join("[%s]" % a for a in args)  # (a tuple argument formats as the reference's)
         if key not in memo:
             memo[key] = func(*args)
         return memo[key]

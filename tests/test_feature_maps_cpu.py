@@ -96,6 +96,11 @@ def test_rec_memoises_on_printed_arguments():
     assert f(1, 2) == 12 and f(1, 2) == 12 and len(calls) == 1
     assert f("1", "2") == 12 and len(calls) == 1  # '[1]-[2]' either way
     assert f(2, 1) == 21 and len(calls) == 2
+    # tuple arguments format as in kernels.py:315 ('[%s]' % arg): a 1-tuple prints bare, so
+    # it shares the key of its element; a longer tuple raises TypeError
+    assert f((1,), 2) == 12 and len(calls) == 2
+    with pytest.raises(TypeError):
+        f((1, 2), 3)
 
 
 def test_b_k_base_cases_without_device():
