@@ -358,18 +358,27 @@ def reference_model_s(kind, n):
 
 
 # ----------------------------------------------------------------------- N = 1 extras
-def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, oracle_row):
-    """One workload on rows [r0, r1) x all n columns, device-resident, one launch set."""
+def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, oracle_row,
+             cols=None):
+    """One workload on rows [r0, r1) x all n columns, device-resident, one launch set;
+    cols = (c0, c1): instead the column block K[:, c0:c1] of every row (kmg_gram_device_cols;
+    the same pairs as rows [c0, c1) x all n, K being symmetric), spot rows checked on it."""
     codes, lens = E.synthetic(n, 101, seed=seed)
     ldc = codes.shape[1]
     esz = np.dtype(L.DTYPES[out_dtype]).itemsize
     d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
     ctx.h2d(d_codes, codes)
     ctx.h2d(d_lens, lens)
-    d_out = ctx.dmalloc((r1 - r0) * n * esz)
+    width = n if cols is None else cols[1] - cols[0]
+    nrows = (r1 - r0) if cols is None else n
+    d_out = ctx.dmalloc(nrows * width * esz)
     try:
         def step():
-            ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, d_out, n)
+            if cols is None:
+                ctx.gram_device(params, d_codes, d_lens, n, ldc, r0, r1, out_dtype, d_out, n)
+            else:
+                ctx.gram_device_cols(params, d_codes, d_lens, n, ldc, cols[0], cols[1], out_dtype,
+                                     d_out, width)
 
         for _ in range(warmup):
             step()
@@ -386,18 +395,23 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         plan = ctx.last_plan()
         ok = True
         for r in spot_rows:
-            row = np.empty(n, dtype=L.DTYPES[out_dtype])
-            ctx.d2h(row, ctypes.c_void_p(d_out.value + (r - r0) * n * esz))
+            row = np.empty(width, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + (r - (r0 if cols is None else 0)) * width * esz))
             ref = oracle_row(codes, lens, r)
+            if cols is not None:
+                ref = ref[cols[0]:cols[1]]
             ok &= bool(np.array_equal(row.astype(ref.dtype), ref))
     finally:
         ctx.dfree(d_out)
         ctx.dfree(d_codes)
         ctx.dfree(d_lens)
     ms = wall / steps * 1e3
-    return {"N": n, "rows": r1 - r0, "steps": steps, "ms_per_step": ms,
-            "pairs_per_s": (r1 - r0) * n / (ms / 1e3), "stages_ms": stages, "plan": plan,
-            "spot_check_rows": list(spot_rows), "spot_check": ok}
+    out = {"N": n, "rows": nrows, "steps": steps, "ms_per_step": ms,
+           "pairs_per_s": nrows * width / (ms / 1e3), "stages_ms": stages, "plan": plan,
+           "spot_check_rows": list(spot_rows), "spot_check": ok}
+    if cols is not None:
+        out["cols"] = list(cols)
+    return out
 
 
 def extras(ctx, cpu_rates, steps4):
@@ -423,6 +437,19 @@ def extras(ctx, cpu_rates, steps4):
                       "0..25000 (one of 8 ranks) x 200000 columns, float64 normalised (40 GB)")
     c5["reference_model_s"] = reference_model_s("mismatch_k9_m1", n5)
     out["config5_mismatch_k9_n200000_rank_slab"] = c5
+    # the same share as a column block: K[:, 0:25000] of all 200000 rows (= rows 0..25000
+    # transposed; the lists are built over the block's 25000 sequences only and each is read
+    # by all 200000 rows, so they pack -- DESIGN §5)
+    c5c = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1), L.KMG_F64, n5,
+                   5, 0, n5, 2, 1, (0, n5 - 1), mm, cols=(0, n5 // 8))
+    c5c["workload"] = ("BASELINE configs[4] per-GPU share as a column block: K[:, 0:25000] x "
+                       "all 200000 rows (= the rank slab transposed), float64 normalised (40 GB)")
+    out["config5_mismatch_k9_n200000_rank_colblock"] = c5c
+    c5cr = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32, n5,
+                    5, 0, n5, 2, 1, (0, n5 - 1), mmr, cols=(0, n5 // 8))
+    c5cr["workload"] = ("config-5 raw int32 K's 1/8 share as a column block (the G=8 share of the "
+                        "config5 full_1gpu build, collective-free)")
+    out["config5_mismatch_k9_n200000_colblock_raw_int32"] = c5cr
     c5f = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
                    n5, 5, 0, n5, 1, 1, (0, n5 - 1), mmr)
     c5f["workload"] = ("BASELINE configs[4] on ONE GPU: the full 200000 x 200000 raw int32 K "
@@ -798,6 +825,12 @@ def projection(sp, n, extra):
                         "full_rows_gram_ms_model": g_rows},
             **{str(g): v for g, v in scaling_projection(
                 n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1, chunk=ch5).items()}}
+        cb = (extra or {}).get("config5_mismatch_k9_n200000_colblock_raw_int32")
+        if cb:  # a G=8 share measured on this GPU: the collective-free build, no model
+            out["config5_mismatch_k9_n200000_raw_int32"]["8"]["collective_free_measured_ms"] = \
+                cb["ms_per_step"]
+            out["config5_mismatch_k9_n200000_raw_int32"]["8"]["collective_free_measured_speedup"] = \
+                c5["ms_per_step"] / cb["ms_per_step"]
     return out
 
 
@@ -850,6 +883,9 @@ def _projection_summary(proj):
             g8 = v["8"]
             out[k.split("_")[0]] = {"every_gpu": _r(g8.get("every_gpu_speedup"), 3),
                                    "collective_free": _r(g8.get("collective_free_speedup"), 3)}
+            if "collective_free_measured_speedup" in g8:
+                out[k.split("_")[0]]["collective_free_measured_share"] = _r(
+                    g8["collective_free_measured_speedup"], 3)
     return out
 
 

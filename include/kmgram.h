@@ -126,6 +126,19 @@ int kmg_gram_device(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
                     int32_t out_dtype, void *d_out, int64_t ld_out);
 
 /*
+ * Device-resident column block: K[i][col0 + j] for every row i in [0, n) and j in
+ * [0, col1 - col0), at d_out[i * ld_out + j].  K is symmetric, so this is the row slab
+ * [col0, col1) x all n transposed: one GPU's 1/G share of a sharded build (the pair loops
+ * of kernels.py:211-215 split by columns), with the neighbourhood lists built over the
+ * block's sequences only -- each list read by all n rows.  Mismatch (k, 1), 4 <= k <= 12
+ * (get_mismatch_K, kernels.py:196-217); other kernels return KMG_EUNSUPPORTED.  Runs on
+ * the context stream; returns without synchronising.
+ */
+int kmg_gram_device_cols(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
+                         const int32_t *d_lens, int64_t n, int64_t ldc, int64_t col0,
+                         int64_t col1, int32_t out_dtype, void *d_out, int64_t ld_out);
+
+/*
  * The full K of all n rows into HOST memory h_out (row stride ld_host elements; e.g. a
  * memory-mapped .npy), built on the device in slabs of slab_rows rows: the posting index /
  * features / diagonal are built once for all slabs, and slab t's device-to-host copy (a

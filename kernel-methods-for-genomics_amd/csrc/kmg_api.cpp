@@ -111,9 +111,12 @@ struct Tuning {
                             // was removed in round 5: measured slower than the lists at k = 9)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
+  int nb_wgcu = 2;          // KMG_NB_WGCU: neighbourhood-list Gram workgroups a CU the chunk's
+                            // LDS accumulator is sized for (2: chunks <= ~20000; 1: <= ~40000)
   int nb_unroll = 0;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8;
-                            // 0 auto: 8, or 4 for an upper-block-triangle build -- interleaved
-                            // A/B, profiles/r04x2_nb_unroll_ab.jsonl)
+                            // 0 auto: 8, or 4 for an upper-block-triangle build or packed
+                            // lists -- profiles/r04x2_nb_unroll_ab.jsonl; column block N=200000
+                            // x 25000 Gram 23.6 -> 22.3 ms, profiles/r05x_colblock.jsonl)
   int nb_fill = 0;          // KMG_NB_FILL: list fill, 0 auto (sorted + packed segment 2 where a
                             // list is read >= nb_pack_reads times and nb_sorted_cap allows;
                             // else staged 16-bit lists), 1 sorted, 2 grouped lane-per-run,
@@ -174,6 +177,7 @@ void read_tuning(Tuning &t) {
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_pack_reads = env_or("KMG_NB_PACK_READS", d.nb_pack_reads);
   t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
+  t.nb_wgcu = env_or("KMG_NB_WGCU", d.nb_wgcu) == 1 ? 1 : 2;
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -556,11 +560,12 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
 // 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
 // mirror.  Largest chunk: the int32 LDS accumulator beside the row tables, and where
 // segment 2 packs, the sorted fill's LDS buffer (nb_sorted_max_chunk: ~24900 at k = 9).
-int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted) {
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted,
+             int wgcu) {
   // two workgroups a CU (their table builds, epilogues and streams overlap; one a CU measured
   // 22 % slower at N=20000, profiles/r05g_*): the accumulator, 16 dummy columns and the row
   // table in 80 KB (1024 threads) or 40 KB (512)
-  const int64_t lds_words = (threads == 512 ? 40 : 80) * 1024 / 4;
+  const int64_t lds_words = (threads == 512 ? 40 : 80) * (wgcu == 1 ? 2 : 1) * 1024 / 4;
   int64_t max_chunk = (lds_words - 16 - 4 * (int64_t)pmax - 2 - ldp) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
   const int smax = sorted ? nb_sorted_max_chunk(k, pmax) : 0;
@@ -827,14 +832,20 @@ SmPath sm_path(const Tuning &t, const kmg_params *p, int pmax, int64_t n) {
   return exact ? SM_POSTING : SM_SLOTS;
 }
 
+// cseq0 / ncols >= 0: a column block -- columns j of the output are sequences cseq0 + j,
+// j < ncols (kmg_gram_device_cols; neighbourhood-list formulation only)
 int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const int32_t *d_lens,
                 int maxlen, int64_t n, int64_t ldc, const std::vector<RowRange> &ranges,
-                int32_t dt, int64_t ld, const AfterRange &after = nullptr) {
+                int32_t dt, int64_t ld, const AfterRange &after = nullptr, int64_t cseq0 = 0,
+                int64_t ncols = -1) {
   c->last_call_first = (int)c->ev_log.size();
   c->cur_n = n;
+  const bool colblk = ncols >= 0;
+  if (!colblk) ncols = n;
+  if (cseq0 < 0 || cseq0 + ncols > n) return fail(KMG_EINVAL, "bad column range");
   for (const RowRange &r : ranges)
     if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
-  if (n > 0 && ld < n) return fail(KMG_EINVAL, "ld_out < n");
+  if (n > 0 && ld < ncols) return fail(KMG_EINVAL, "ld_out < columns");
   const bool narrow = dt == KMG_U16 || dt == KMG_U8;
   if (narrow && p->kind != KMG_SPECTRUM && p->kind != KMG_MISMATCH)
     return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
@@ -855,7 +866,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         const int64_t rld = r.ld > 0 ? r.ld : ld;
         KMG_HIP(hipMemset2DAsync((char *)r.out + (size_t)r.col_lo * dtype_size(dt),
                                  (size_t)rld * dtype_size(dt), 0xA5,
-                                 (size_t)(n - r.col_lo) * dtype_size(dt),
+                                 (size_t)(ncols - r.col_lo) * dtype_size(dt),
                                  (size_t)(r.row1 - r.row0), c->stream));
       }
   switch (p->kind) {
@@ -948,7 +959,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         for (int d = 0; d <= 32; ++d) w[d] = d == 0 ? 1 : 0;
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
-      const SmPath path = sm_path(c->tune, p, g.pmax, n);
+      SmPath path = sm_path(c->tune, p, g.pmax, n);
+      if (colblk) {  // column blocks: the neighbourhood lists over the block's sequences
+        if (!(mm && p->m == 1 && k >= 4 && k <= 12) || (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64) ||
+            after || ranges.size() != 1 || ranges[0].col_lo != 0)
+          return fail(KMG_EUNSUPPORTED, "column blocks: mismatch (k, 1) with 4 <= k <= 12 only");
+        path = SM_NB;
+      }
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
       const bool use_nb = path == SM_NB;
       const bool use_index = path == SM_POSTING || use_slots || use_pairs || use_nb;
@@ -956,7 +973,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       // posting-list formulation: built by its upper block triangle, then mirrored
       // (OutSpec::tri; set below once the chunking is known)
       const bool square = ranges.size() == 1 && ranges[0].row0 == 0 && ranges[0].row1 == n &&
-                          ranges[0].col_lo == 0 && !after && !narrow && n > 0;
+                          ranges[0].col_lo == 0 && !after && !narrow && n > 0 && !colblk;
       const int tri_esz = (c->tune.mm_tri && square && (use_slots || use_pairs || use_nb))
                               ? (int)dtype_size(dt) : 0;
       auto mirror = [&]() -> int {
@@ -1085,6 +1102,9 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // k-mer)'s neighbourhood list assembled from it (kmg_nbhd.hip)
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
+        // gc: the column sequences the lists are built over (all n, or a column block's)
+        IndexGeom gc = g;
+        gc.n = ncols;
         const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
         // the sorted fill (packed segment 2) where each list is read often enough to repay its
         // sort: reads a list = rows read x windows a row / 4^k (x (nch + 1) / (2 nch) for a
@@ -1093,21 +1113,34 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         if (c->tune.nb_fill == 0) {
           int64_t rows_read = 0;
           for (const RowRange &r : ranges) rows_read += r.row1 - r.row0;
-          const int ch = nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, true);
-          const int64_t nch = (n + ch - 1) / ch;
+          const int ch = nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
+                                  true, c->tune.nb_wgcu);
+          const int64_t nch = (ncols + ch - 1) / ch;
           const double f = (tri_esz > 0 && nch > 1) ? (double)(nch + 1) / (2.0 * nch) : 1.0;
           sorted = (double)rows_read * g.pmax / (double)pow4(k) * f >= (double)c->tune.nb_pack_reads;
         }
-        choose_chunks(g, nb_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt, sorted));
+        choose_chunks(gc, nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
+                                   sorted, c->tune.nb_wgcu));
+        g.chunk = gc.chunk;
+        g.nchunks = gc.nchunks;
         o.tri = tri_esz > 0 && g.nchunks > 1;
         note_plan(nbt);
         c->plan[5] = (sorted && nb_sorted_cap(k, g.pmax, g.chunk) > 0) ? 1 : 0;
-        if (nb_gram_lds(g, pkd) > 160 * 1024)  // (very long windows: the row table alone)
+        if (nb_gram_lds(gc, pkd) > 160 * 1024)  // (very long windows: the row table alone)
           return fail(KMG_EUNSUPPORTED, "neighbourhood lists: %zu B of LDS at %d windows a row "
-                      "(KMG_MM_FORM=1 or 2: the slot / pair tables)", nb_gram_lds(g, pkd), g.pmax);
-        KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
-        const int64_t nbins = g.nbins();
-        const int64_t bound = nb_list_entries_bound(k, n * (int64_t)g.pmax, nbins);
+                      "(KMG_MM_FORM=1 or 2: the slot / pair tables)", nb_gram_lds(gc, pkd), g.pmax);
+        if (!colblk) {
+          KMG_TRY(build_index(c, gc, pkd, d_codes, d_lens, ldc));
+        } else {  // every row's record, then the index over the block's (already packed) ones
+          {
+            StageTimer t(c, ST_PACK);
+            KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, g.window, c->packed.as<uint32_t>(), c->stream));
+          }
+          const Packed pkc{pkd.w + cseq0 * pkd.ldp, pkd.ldp, pkd.cw};
+          KMG_TRY(build_index(c, gc, pkc));
+        }
+        const int64_t nbins = gc.nbins();
+        const int64_t bound = nb_list_entries_bound(k, ncols * (int64_t)g.pmax, nbins);
         if (bound / 8 + nbins >= 0xFFFFFFF0LL)
           return fail(KMG_EUNSUPPORTED, "neighbourhood lists: more than 2^32 pieces");
         KMG_TRY(c->pr_rtot.ensure(sizeof(uint32_t) * (size_t)(nbins + 1)));
@@ -1119,13 +1152,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         KMG_TRY(c->nb_lines.ensure(sizeof(uint16_t) * (size_t)(bound + 8)));
         {
           StageTimer t(c, ST_LISTS);  // list sizes and starts
-          KMG_HIP(launch_nb_count(g, c->off.as<uint32_t>(), c->pr_rtot.as<uint32_t>(),
+          KMG_HIP(launch_nb_count(gc, c->off.as<uint32_t>(), c->pr_rtot.as<uint32_t>(),
                                   c->pr_rbase.as<uint32_t>(), c->pr_cursor.as<uint32_t>(),
                                   c->nb_seg.as<uint2>(), c->partials.as<uint32_t>(), c->stream));
         }
         {
           StageTimer t(c, ST_NBFILL);  // the lists themselves
-          const hipError_t e = launch_nb_fill(g, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+          const hipError_t e = launch_nb_fill(gc, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                               c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                               c->nb_use.as<uint2>(), c->nb_lines.as<uint16_t>(),
                                               c->stream,
@@ -1143,11 +1176,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             o.dsq = c->dsq.as<double>();
           }
         }
+        o.col_seq0 = cseq0;
         KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-          return launch_gram_mismatch1_nb(g, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
+          return launch_gram_mismatch1_nb(gc, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                           c->nb_use.as<uint2>(), c->nb_lines.as<uint4>(), r0, r1,
                                           (int)w[0], (int)w[1], (int)w[2], oq, c->stream, nbt,
-                                          c->tune.nb_unroll ? c->tune.nb_unroll : (o.tri ? 4 : 8));
+                                          c->tune.nb_unroll ? c->tune.nb_unroll
+                                                            : (o.tri || c->plan[5] ? 4 : 8));
         }, true));
         return mirror();
       }
@@ -1584,6 +1619,18 @@ int kmg_gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
   // max(lens) <= ldc (checked in the host path).  maxlen = ldc bounds every kernel.
   return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, {RowRange{row0, row1, d_out}},
                      out_dtype, ld_out);
+}
+
+int kmg_gram_device_cols(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                         const int32_t *d_lens, int64_t n, int64_t ldc, int64_t col0,
+                         int64_t col1, int32_t out_dtype, void *d_out, int64_t ld_out) {
+  if (!c) return fail(KMG_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(c->mu);
+  KMG_TRY(check_params(p, n, ldc, out_dtype));
+  if (col0 < 0 || col1 > n || col0 >= col1) return fail(KMG_EINVAL, "bad column range");
+  KMG_HIP(hipSetDevice(c->device));
+  return gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, {RowRange{0, n, d_out}},
+                     out_dtype, ld_out, nullptr, col0, col1 - col0);
 }
 
 int kmg_gram_to_host(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,

@@ -167,6 +167,8 @@ struct OutSpec {
   const double *dsq;    // sqrt(raw diagonal) (normalize)
   int64_t col_lo = 0;   // columns < col_lo are not written (upper-triangle multi-GPU
                         // builds; kernels that honour it: spectrum, mismatch slots / pairs)
+  int64_t col_seq0 = 0; // sequence of output column 0 (column blocks, kmg_gram_device_cols):
+                        // the diagonal and the normalisation's K_jj are taken at col_seq0 + j
   int tri = 0;          // full square K (rows [0, n)): the mismatch posting-list kernels
                         // compute only the column chunks that reach column i of row i
                         // (rowacc_block); the caller mirrors the rest (launch_mirror_chunks)

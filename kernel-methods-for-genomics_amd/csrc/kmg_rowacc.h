@@ -74,7 +74,8 @@ __device__ __forceinline__ void emit4(const OutSpec &o, int64_t il, int64_t ig, 
       if (q < cnt) {
         if (norm) {
           // normalize_K: K[i,j] /= (d * diag[j]) with d = sqrt(K[i,i]); diagonal := 1
-          r[q] = (ig == col + q) ? 1.0 : (double)v[q] / (o.dsq[ig] * o.dsq[col + q]);
+          const int64_t cs = o.col_seq0 + col + q;
+          r[q] = (ig == cs) ? 1.0 : (double)v[q] / (o.dsq[ig] * o.dsq[cs]);
         } else {
           r[q] = (double)v[q];
         }
@@ -137,7 +138,7 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
 #pragma unroll
       for (int h = 0; h < 16; ++h) {
         const uint32_t x = q + h < cw ? (A16 ? (uint32_t)a16[q + h] : (uint32_t)acc[q + h]) : 0u;
-        const bool dg = col0 + q + h == i;
+        const bool dg = o.col_seq0 + col0 + q + h == i;
         v[h] = (dg || q + h >= cw) ? 0u : u8_slab_entry(o, i, col0 + q + h, x, big);
       }
       uint8_t *d = prow + q;
@@ -212,7 +213,7 @@ __device__ __forceinline__ void emit_row(const OutSpec &o, int64_t il, int64_t i
       } else {
         w = *(const int2 *)&acc[q];
       }
-      const int64_t c0 = col0 + q;
+      const int64_t c0 = o.col_seq0 + col0 + q;  // the column's sequence
       const bool two = q + 1 < cw;
       double r0 = (double)w.x, r1 = two ? (double)w.y : 0.0;
       if (norm) {  // normalize_K: K[i,j] / (sqrt(K[i,i]) * sqrt(K[j,j])), diagonal := 1

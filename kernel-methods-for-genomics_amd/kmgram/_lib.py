@@ -36,7 +36,7 @@ EXPORTS = (
     "kmg_krr_solve_device", "kmg_klr_fit", "kmg_klr_fit_device", "kmg_svm_fit",
     "kmg_svm_fit_device", "kmg_rows_padded", "kmg_gram_blocks", "kmg_reload_tuning",
     "kmg_gram_to_host", "kmg_gram_blocks_wire", "kmg_last_plan", "kmg_features",
-    "kmg_last_factorisation", "kmg_features_sym",
+    "kmg_last_factorisation", "kmg_features_sym", "kmg_gram_device_cols",
 )
 KMG_FEATURES_BCAST = 1
 KMG_FACTOR_CHOLESKY, KMG_FACTOR_LU_ASYMMETRIC, KMG_FACTOR_LU_INDEFINITE = 1, 2, 3
@@ -93,6 +93,8 @@ def load():
             "kmg_gram": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I32, P, I64], ctypes.c_int),
             "kmg_gram_device": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I64, I64, I32, P,
                                  I64], ctypes.c_int),
+            "kmg_gram_device_cols": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, I64, I64, I32,
+                                      P, I64], ctypes.c_int),
             "kmg_features": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, P, I64, P, I64],
                              ctypes.c_int),
             "kmg_features_sym": ([P, ctypes.POINTER(KmgParams), P, P, I64, I64, P, I64, I32, P,
@@ -233,6 +235,11 @@ class Context:
     def gram_device(self, params, d_codes, d_lens, n, ldc, row0, row1, out_dtype, d_out, ld):
         check(self.lib.kmg_gram_device(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        row0, row1, out_dtype, d_out, ld))
+
+    def gram_device_cols(self, params, d_codes, d_lens, n, ldc, col0, col1, out_dtype, d_out, ld):
+        """Column block K[:, col0:col1] (every row) at d_out, row stride ld (kmg_gram_device_cols)."""
+        check(self.lib.kmg_gram_device_cols(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
+                                            col0, col1, out_dtype, d_out, ld))
 
     def gram_blocks(self, params, d_codes, d_lens, n, ldc, out_dtype, d_out, ld, nranks, rank,
                     block, gather):

@@ -1,0 +1,93 @@
+"""GPU parity of kmg_gram_device_cols: column blocks K[:, col0:col1] of the mismatch (k, 1)
+Gram (kernels.py:196-217) with the neighbourhood lists built over the block's sequences.
+Checked bit-exact against the oracle (raw and normalised), and against the row slab of
+the same sequences transposed (K is symmetric) at N=20000."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import cref
+from kmgram import _lib as L
+from kmgram import encode as E
+from kmgram import params as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _col_block(ctx, params, codes, lens, col0, col1, dt):
+    n = codes.shape[0]
+    w = col1 - col0
+    npdt = L.DTYPES[dt]
+    wa = max(1, w)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(n * wa * np.dtype(npdt).itemsize)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device_cols(params, d_codes, d_lens, n, codes.shape[1], col0, col1, dt, d_out, w)
+        ctx.synchronize()
+        out = np.empty((n, w), dtype=npdt)
+        ctx.d2h(out, d_out)
+        return out
+    finally:
+        for p in (d_out, d_codes, d_lens):
+            ctx.dfree(p)
+
+
+@pytest.mark.parametrize("k", [8, 9, 10])
+@pytest.mark.parametrize("fill", ["0", "1", "4"])
+def test_column_blocks_vs_oracle(ctx, tune, k, fill):
+    """Blocks at the start, inside, at the end and of one column; 30 poly-A rows make lists
+    past the fills' LDS buffers (lane-per-run fallbacks)."""
+    codes, lens = E.synthetic(700, 101, seed=200 + k)
+    codes[:30] = 0
+    tune(KMG_NB_FILL=fill)
+    raw_p = P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0)
+    if fill == "1" and k == 10:  # segment 2 too sparse to pack: the forced sorted fill refuses
+        with pytest.raises(L.KmgUnsupported, match="sorted fill"):
+            _col_block(ctx, raw_p, codes, lens, 0, 700, L.KMG_I32)
+        return
+    ref = cref.mismatch_raw(codes, lens, k, 1)
+    for col0, col1 in ((0, 700), (0, 123), (250, 611), (699, 700)):
+        K = _col_block(ctx, raw_p, codes, lens, col0, col1, L.KMG_I32)
+        assert ctx.last_plan()["formulation"] == "neighbourhood"
+        assert np.array_equal(K.astype(np.int64), ref[:, col0:col1]), (col0, col1)
+    Kn = _col_block(ctx, P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
+                    250, 611, L.KMG_F64)
+    refn = cref.mismatch_rows(codes, lens, k, 1)
+    assert np.array_equal(Kn, refn[:, 250:611])
+
+
+def test_column_block_is_row_slab_transposed_n20000(ctx):
+    """N=20000, columns [5000, 12000): the block equals rows [5000, 12000) of the row-slab
+    path transposed, bit for bit (float64 normalised); oracle rows at both block edges."""
+    n, c0, c1 = 20000, 5000, 12000
+    codes, lens = E.synthetic(n, 101, seed=3)
+    params = P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1)
+    Kc = _col_block(ctx, params, codes, lens, c0, c1, L.KMG_F64)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_K = ctx.dmalloc((c1 - c0) * n * 8)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device(params, d_codes, d_lens, n, codes.shape[1], c0, c1, L.KMG_F64, d_K, n)
+        ctx.synchronize()
+        Kr = np.empty((c1 - c0, n), dtype=np.float64)
+        ctx.d2h(Kr, d_K)
+    finally:
+        for p in (d_K, d_codes, d_lens):
+            ctx.dfree(p)
+    assert np.array_equal(Kc, Kr.T)
+    for r in (c0, c1 - 1):
+        assert np.array_equal(Kr[r - c0], cref.mismatch_rows(codes, lens, 9, 1, rows=(r, r + 1))[0])
+
+
+def test_column_block_argument_checks(ctx):
+    codes, lens = E.synthetic(64, 101, seed=5)
+    with pytest.raises(L.KmgUnsupported):
+        _col_block(ctx, P.make(L.KMG_SPECTRUM, k=8), codes, lens, 0, 32, L.KMG_I32)
+    with pytest.raises(L.KmgUnsupported):
+        _col_block(ctx, P.make(L.KMG_MISMATCH, k=9, m=2, window=101), codes, lens, 0, 32, L.KMG_I32)
+    with pytest.raises(L.KmgError):
+        _col_block(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101), codes, lens, 40, 30, L.KMG_I32)

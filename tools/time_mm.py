@@ -42,15 +42,28 @@ def main():
         dc, dl = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
         ctx.h2d(dc, codes)
         ctx.h2d(dl, lens)
-        do = ctx.dmalloc(rows * n * esz)
         steps = case.get("steps", 5)
-        ctx.gram_device(params, dc, dl, n, codes.shape[1], 0, rows, dt, do, n)
+        cols = case.get("cols")  # [c0, c1]: the column block K[:, c0:c1] (kmg_gram_device_cols)
+        if cols:
+            c0, c1 = cols
+            rows, width = n, c1 - c0
+            do = ctx.dmalloc(n * width * esz)
+
+            def run():
+                ctx.gram_device_cols(params, dc, dl, n, codes.shape[1], c0, c1, dt, do, width)
+        else:
+            width = n
+            do = ctx.dmalloc(rows * n * esz)
+
+            def run():
+                ctx.gram_device(params, dc, dl, n, codes.shape[1], 0, rows, dt, do, n)
+        run()
         ctx.synchronize()
         ctx.set_timing(True)
         ctx.timing_reset()
         t0 = time.perf_counter()
         for _ in range(steps):
-            ctx.gram_device(params, dc, dl, n, codes.shape[1], 0, rows, dt, do, n)
+            run()
         ctx.synchronize()
         wall = (time.perf_counter() - t0) / steps
         st = {}
@@ -71,12 +84,14 @@ def main():
         if case.get("check", True) and kind == "mm":
             import cref
             r = rows - 1
-            row = np.empty(n, dtype=L.DTYPES[dt])
+            row = np.empty(width, dtype=L.DTYPES[dt])
             import ctypes
-            ctx.d2h(row, ctypes.c_void_p(do.value + r * n * esz))
+            ctx.d2h(row, ctypes.c_void_p(do.value + r * width * esz))
             ref = (cref.mismatch_rows(codes, lens, case.get("k", 9), 1, rows=(r, r + 1))[0]
                    if case.get("norm", 1) else
                    cref.mismatch_raw(codes, lens, case.get("k", 9), 1, rows=(r, r + 1))[0])
+            if cols:
+                ref = ref[cols[0]:cols[1]]
             ok = bool(np.array_equal(row.astype(ref.dtype), ref))
         for p in (do, dc, dl):
             ctx.dfree(p)
