@@ -596,7 +596,7 @@ def run_py_workload(ctx, n=9000, reps=5):
 FP64_PEAK = 78.6e12  # MI355X dense fp64 (spec sheet)
 
 
-def downstream(ctx):
+def downstream(ctx, asym=True):
     """§8f consumers of the Gram on device-resident float64 matrices at the production size
     (n = 9000 = train + val + test of the 3 TFs, utils.py:151-153): NLCK combination
     (HBM-bound) and the KRR / KLR / C-SVM solves (fp64 factorisation)."""
@@ -653,19 +653,21 @@ def downstream(ctx):
                 "factorisation": ctx.last_factorisation(),
                 "note": "symmetry check + Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I"}
         # the same solve on the ulp-asymmetric K / d_i / d_j: LU (rocSOLVER dgetrf, launch-bound
-        # per column), what any user-normalised K not symmetrised costs
-        ctx.h2d(dK[1], Ka)
-        m_ = 2000
-        L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[1], n, m_, d_y, 0.1, d_a))
-        ctx.synchronize()
-        ctx.timing_reset()
-        for _ in range(reps):
+        # per column), what any user-normalised K not symmetrised costs (asym=False: skipped,
+        # tools/trace_downstream.py's trace of the symmetric legs)
+        if asym:
+            ctx.h2d(dK[1], Ka)
+            m_ = 2000
             L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[1], n, m_, d_y, 0.1, d_a))
-        tot, cnt = ctx.stage_stats("solve")
-        out["krr_solve_asymmetric_K_n2000"] = {
-            "ms": tot / cnt, "factorisation": ctx.last_factorisation(), "source": "KRR.py:33",
-            "note": "K != K^T by ulps: symmetry check + LU (dgetrf / dgetrs)"}
-        ctx.h2d(dK[1], K)
+            ctx.synchronize()
+            ctx.timing_reset()
+            for _ in range(reps):
+                L.check(ctx.lib.kmg_krr_solve_device(ctx.handle, dK[1], n, m_, d_y, 0.1, d_a))
+            tot, cnt = ctx.stage_stats("solve")
+            out["krr_solve_asymmetric_K_n2000"] = {
+                "ms": tot / cnt, "factorisation": ctx.last_factorisation(), "source": "KRR.py:33",
+                "note": "K != K^T by ulps: symmetry check + LU (dgetrf / dgetrs)"}
+            ctx.h2d(dK[1], K)
         it = ctypes.c_int32(0)
         m_ = 2000
         ctx.timing_reset()
