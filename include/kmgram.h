@@ -316,8 +316,8 @@ int kmg_stage_stats(kmg_ctx *ctx, const char *stage, double *total_ms, int32_t *
 
 /* How the last spectrum / mismatch Gram call on ctx was built (for roofline accounting):
  * plan[0] formulation (0 dense count-vector GEMM, 1 all-pairs Hamming, 2 posting lists,
- * 3 mismatch drop-one slot table, 4 drop-two pair table, 5 pair lines, 6 neighbourhood
- * lists, 7 the generic per-pair kernels of k > 16; -1 none yet or the call failed before
+ * 3 mismatch drop-one slot table, 4 drop-two pair table, 5 (unused: round 3's pair lines,
+ * removed), 6 neighbourhood lists, 7 the generic per-pair kernels of k > 16; -1 none yet or the call failed before
  * choosing),
  * plan[1] columns per chunk, plan[2] column chunks, plan[3] 1 when a full square K was built
  * by its upper block triangle and mirrored, plan[4] Gram workgroup threads (0 where the
