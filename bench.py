@@ -41,8 +41,8 @@ import numpy as np  # noqa: E402
 from kmgram import _lib as L  # noqa: E402
 from kmgram import encode as E  # noqa: E402
 from kmgram import params as P  # noqa: E402
-from kmgram.shard import (block_cyclic_ranges, default_block, rows_padded,  # noqa: E402
-                          scaling_projection, triangle_rounds, weak_scaled_n)
+from kmgram.shard import (block_cyclic_ranges, default_block, rank_rows,  # noqa: E402
+                          rows_padded, scaling_projection, triangle_rounds, weak_scaled_n)
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 GATHER_MODE = 2  # G > 1: upper-triangle round slabs + local mirror (--gather-mode 1: full rows)
@@ -412,6 +412,50 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
     if cols is not None:
         out["cols"] = list(cols)
     return out
+
+
+def run_colblock_dist(ctx, dist, params, out_dtype, n, seed, steps, warmup, oracle_row):
+    """G > 1, collective-free: rank r computes the column block K[:, C_r] of all n rows,
+    C_r = rank_rows(n, G, r) (kmg_gram_device_cols: the lists over the rank's own columns,
+    packed).  Timed like run_build: barrier + synchronise on both sides, max over ranks."""
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    c0, c1 = rank_rows(n, dist.world, dist.rank)
+    w = c1 - c0
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(n * w * esz)
+    try:
+        def step():
+            ctx.gram_device_cols(params, d_codes, d_lens, n, ldc, c0, c1, out_dtype, d_out, w)
+
+        for _ in range(warmup):
+            step()
+        ctx.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.synchronize()
+        dist.barrier()
+        t = dist.max(time.perf_counter() - t0)
+        plan = ctx.last_plan()
+        ok = True
+        for r in (0, n - 1):
+            row = np.empty(w, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * w * esz))
+            ref = oracle_row(codes, lens, r)[c0:c1]
+            ok &= bool(np.array_equal(row.astype(ref.dtype), ref))
+        ok = dist.all_true(ok)
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    ms = t / steps * 1e3
+    return {"N": n, "cols_this_rank": w, "steps": steps, "ms_per_step": ms,
+            "pairs_per_s": n * n / (ms / 1e3), "plan": plan, "spot_check": ok}
 
 
 def extras(ctx, cpu_rates, steps4):
@@ -963,6 +1007,13 @@ def main():
         c5 = run_build(ctx, dist, "mismatch_k9_m1_raw",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
                        200000, 5, 2, 1, check_mismatch_raw)
+    c5cb = None
+    if dist.world > 1 and not args.no_extra:
+        # config 5 collective-free at G > 1: each GPU its column block of the raw int32 K
+        import cref
+        c5cb = run_colblock_dist(ctx, dist, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0),
+                                 L.KMG_I32, 200000, 5, 2, 1,
+                                 lambda c, l, r: cref.mismatch_raw(c, l, 9, 1, rows=(r, r + 1))[0])
     extra = None
     if dist.world == 1 and not args.no_extra:
         extra = extras(ctx, {k: v["value"] for k, v in cpu.items()}, max(20, args.steps))
@@ -1050,6 +1101,12 @@ def main():
             **{k: c5[k] for k in ("ms_per_step", "pairs_per_s", "stages_ms", "block_rows",
                                   "rounds", "spot_check", "collective_free")},
             "gather_roofline": gather_roofline(c5, dist.world, 4)}
+    if c5cb:
+        line["config5_colblock_collective_free"] = {
+            "workload": "BASELINE configs[4]: mismatch (9,1), N=200000, raw int32 K as G column "
+                        "blocks, each GPU K[:, C_g] of all rows (no collective; the G=1 point is "
+                        "configs.config5_mismatch_k9_n200000_full_1gpu)",
+            "scaling": "strong", **c5cb}
     if cpu:
         line["cpu_baseline"] = {k: v for k, v in cpu["spectrum_k8"].items() if k != "one_process"}
         line["cpu_baseline_one_process"] = cpu["spectrum_k8"]["one_process"]

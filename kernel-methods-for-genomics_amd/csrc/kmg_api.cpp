@@ -146,6 +146,8 @@ struct Tuning {
   int dense_bk = 128;       // KMG_DENSE_BK: dense Gram k-stage bytes, 64 or 128 (128: half the
                             // barriers; MM k=7 N=20000 3.38 -> 3.13 ms, k=6 0.92 -> 0.87,
                             // SP k=5 0.38 -> 0.367; profiles/r02ay_dense_bk_ab.jsonl)
+  int dense_stages = 2;     // KMG_DENSE_STAGES: LDS ring stages of the dense Gram's k loop (2, or
+                            // with 64-byte stages 3 / 4: more DMA in flight)
   int dense_half = -1;      // KMG_DENSE_HALF: dense Gram tiles over two 4-wave workgroups (BK
                             // 64), -1: when dp <= 1024 (SP k=5 N=20000 0.41 -> 0.39 ms; at
                             // dp >= 4096 BK 128 wins; profiles/r02bj_dense_epilogue_ab.jsonl)
@@ -185,6 +187,7 @@ void read_tuning(Tuning &t) {
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   t.dense_half = env_or("KMG_DENSE_HALF", d.dense_half);
+  t.dense_stages = env_or("KMG_DENSE_STAGES", d.dense_stages);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -743,7 +746,8 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
     return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
                              c->tune.dense_bk,
-                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0);
+                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0,
+                             c->tune.dense_stages);
   });
 }
 
@@ -790,7 +794,8 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
     return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
                              c->tune.dense_bk,
-                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0);
+                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0,
+                             c->tune.dense_stages);
   });
 }
 

@@ -331,6 +331,7 @@ __device__ __forceinline__ void nb_list_lane_per_run(int k, int su, const uint32
 constexpr int NBS_RW = 14;                 // ds_read_b64 registers (4 entries each) a lane
 constexpr int NBS_MAXCAP = 256 * NBS_RW;   // 3584 entries a wave sorts
 constexpr int NBS_BSH = 6;                 // bucket = column >> 6
+constexpr int NBS_MAXBK = 512;             // buckets a list's sort handles (chunks <= 32768)
 
 __host__ __device__ inline int nbs_table_words(int k) {
   const int kp = k - 2, mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;
@@ -358,25 +359,28 @@ __device__ __forceinline__ uint2 nb_pack_seg2(const uint16_t *sb, uint32_t n2, u
   const int lane = threadIdx.x & 63;
   const uint64_t ltmask = (1ull << lane) - 1ull;
   const uint32_t nc = n2 / 15u;
-  auto load15 = [&](uint32_t cc, uint32_t *v) {
+  // row cc's 16 slots as 8 words (slot 15 unused) and its minimum / maximum column, by
+  // packed 16-bit min / max (v_pk_min_u16 / v_pk_max_u16: 8 + 2 a row instead of 28)
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  auto load_row = [&](uint32_t cc, uint32_t *w, uint32_t &mn, uint32_t &mx) {
     const uint4 a = *(const uint4 *)(sb + 16u * cc), b = *(const uint4 *)(sb + 16u * cc + 8u);
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    us2 lo = __builtin_bit_cast(us2, w[7] | 0xFFFF0000u), hi = __builtin_bit_cast(us2, w[7] & 0xFFFFu);
 #pragma unroll
-    for (int e = 0; e < 15; ++e) v[e] = (e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
+    for (int q = 0; q < 7; ++q) {
+      lo = __builtin_elementwise_min(lo, __builtin_bit_cast(us2, w[q]));
+      hi = __builtin_elementwise_max(hi, __builtin_bit_cast(us2, w[q]));
+    }
+    mn = min((uint32_t)lo.x, (uint32_t)lo.y);
+    mx = max((uint32_t)hi.x, (uint32_t)hi.y);
   };
   uint32_t nfail = 0;
   for (uint32_t c0 = 0; c0 < nc; c0 += 64u) {
     const uint32_t cc = c0 + (uint32_t)lane;
     bool bad = false;
     if (cc < nc) {
-      uint32_t v[15];
-      load15(cc, v);
-      uint32_t mn = v[0], mx = v[0];
-#pragma unroll
-      for (int e = 1; e < 15; ++e) {
-        mn = min(mn, v[e]);
-        mx = max(mx, v[e]);
-      }
+      uint32_t w[8], mn, mx;
+      load_row(cc, w, mn, mx);
       bad = mx - mn > 254u;
     }
     nfail += (uint32_t)__popcll(__ballot(bad));
@@ -394,12 +398,10 @@ __device__ __forceinline__ uint2 nb_pack_seg2(const uint16_t *sb, uint32_t n2, u
     uint32_t v[15];
     uint32_t mn = 0xFFFFu, mx = 0u;
     if (act) {
-      load15(cc, v);
+      uint32_t w[8];
+      load_row(cc, w, mn, mx);
 #pragma unroll
-      for (int e = 0; e < 15; ++e) {
-        mn = min(mn, v[e]);
-        mx = max(mx, v[e]);
-      }
+      for (int e = 0; e < 15; ++e) v[e] = (e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
     }
     const bool ok = act && mx - mn <= 254u;
     const uint64_t om = __ballot(ok), fm = __ballot(act && !ok);
@@ -629,15 +631,19 @@ __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
       }
       nb_wave_sync();
       // ---- 2. bucket starts
-      {
-        const int per = (nbk + 63) >> 6, lo = lane * per, hi = min(nbk, lo + per);
-        uint32_t sum = 0;
-        for (int q = lo; q < hi; ++q) sum += hist[q];
-        uint32_t run = nb_wave_incl_scan_dpp(sum) - sum;
-        for (int q = lo; q < hi; ++q) {
-          const uint32_t t = hist[q];
-          hist[q] = run;
-          run += t;
+      {  // rows of 64 buckets: every read issued first, then one wave scan a row
+        constexpr int NR = NBS_MAXBK / 64;
+        uint32_t hv[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) hv[r] = (r * 64 + lane < nbk) ? hist[r * 64 + lane] : 0u;
+        uint32_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          if (r * 64 < nbk) {  // wave-uniform
+            const uint32_t inc = nb_wave_incl_scan_dpp(hv[r]);
+            if (r * 64 + lane < nbk) hist[r * 64 + lane] = carry + inc - hv[r];
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+          }
         }
       }
       nb_wave_sync();
@@ -1267,6 +1273,7 @@ int nb_sorted_cap(int k, int pmax, int chunk) {
   // runs still fit; k = 10 (28 columns) would spill nearly every run
   if (dens < 1.0 / 12.0) return 0;
   const int nbk = (chunk + (1 << NBS_BSH) - 1) >> NBS_BSH;
+  if (nbk > NBS_MAXBK) return 0;
   const int64_t per_wave = (160 * 1024 / 4 - nb_staged_table_words(k)) / 16;  // words, 16 waves
   // buffer words a wave: 8 a row of 15 entries
   const int64_t rows = (per_wave - ((nbk + 3) & ~3) - NBS_S01 - 64) / 8;

@@ -278,3 +278,46 @@ def test_block_cyclic_cover(n, world, block):
     assert sorted(seen) == list(range(n))
     assert rows_padded(n, world, block) % (world * block) == 0
     assert rows_padded(n, world, block) >= n
+
+
+COLBLOCK_WORKER = r"""
+import os, sys, json
+for p in ("kernel-methods-for-genomics_amd", "oracle"):
+    sys.path.insert(0, os.path.join(os.environ["ROOT"], p))
+import numpy as np, torch, torch.distributed as dist
+import cref
+from kmgram import encode as E
+from kmgram.shard import rank_rows
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+n = 203
+codes, lens = E.synthetic(n, 101, seed=11)
+c0, c1 = rank_rows(n, w, r)
+# this rank's column block K[:, c0:c1] as kmg_gram_device_cols lays it out (every row, the
+# block's columns), restated from the oracle's rows (K symmetric)
+blk = cref.mismatch_raw(codes, lens, 9, 1, rows=(c0, c1)).T.copy()
+parts = [None] * w
+dist.all_gather_object(parts, (c0, c1, blk.tolist()))
+if r == 0:
+    K = np.hstack([np.array(p[2], dtype=np.int64).reshape(n, p[1] - p[0]) for p in parts])
+    ref = cref.mismatch_raw(codes, lens, 9, 1)
+    print(json.dumps({"equal": bool(np.array_equal(K, ref)),
+                      "cover": [p[:2] for p in parts]}))
+dist.destroy_process_group()
+"""
+
+
+def test_gloo_world2_column_blocks(tmp_path):
+    """The collective-free config-5 share as column blocks (bench.py run_colblock_dist): the
+    ranks' K[:, C_r] blocks, C_r = rank_rows(n, G, r), tile K exactly."""
+    pytest.importorskip("torch")
+    script = tmp_path / "c.py"
+    script.write_text(COLBLOCK_WORKER)
+    env = dict(os.environ, ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["equal"] and d["cover"] == [[0, 101], [101, 203]]
