@@ -212,22 +212,43 @@ __global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_e
     for (int b = 0; b < 2; ++b) acc[a][b] = (v16i){};
 
   const int fr = lane & 31, fh = lane >> 5;
+  // one k-stage: DT_BK / 32 steps of 8 MFMAs; the fragments of step s + 1 are read from LDS
+  // while step s multiplies (two fragment sets: without them every 4 MFMAs waited for the
+  // reads issued just before, and the MFMA pipes stood ~70 % idle)
   auto mfma_stage = [&](const uint8_t *sA) {
     const uint8_t *sB = sA + DT_BM * DT_BK;
-#pragma unroll
-    for (int s = 0; s < DT_BK / 32; ++s) {
+    constexpr int NSTEP = DT_BK / 32;
+    v4i a[2][4], b[2][2];
+    auto frag = [&](int s, int set) {
       const int c16 = 2 * s + fh;
-      v4i a[4], b[2];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) a[x] = *(const v4i *)(sA + swz<DT_BK>(wm * 128 + x * 32 + fr, c16));
+      for (int x = 0; x < 4; ++x) a[set][x] = *(const v4i *)(sA + swz<DT_BK>(wm * 128 + x * 32 + fr, c16));
 #pragma unroll
-      for (int y = 0; y < 2; ++y) b[y] = *(const v4i *)(sB + swz<DT_BK>(wn * 64 + y * 32 + fr, c16));
+      for (int y = 0; y < 2; ++y) b[set][y] = *(const v4i *)(sB + swz<DT_BK>(wn * 64 + y * 32 + fr, c16));
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      if (s + 1 < NSTEP) frag(s + 1, (s + 1) & 1);
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[x], b[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s & 1][x], b[s & 1][y], acc[x][y], 0, 0, 0);
     }
+    // schedule: step 0's 6 reads, then each step's 8 MFMAs with the next step's 6 reads
+    // interleaved one by one (masks: 0x100 LDS read, 0x008 MFMA)
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int s = 0; s + 1 < NSTEP; ++s) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
   };
   {
     // LDS-DMA staging (global_load_lds_dwordx4): one wave-instruction fills 1 KB of the
