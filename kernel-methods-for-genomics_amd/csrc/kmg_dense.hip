@@ -337,36 +337,46 @@ __global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_e
     for (int y = 0; y < 2; ++y) {
       const int64_t gr0 = rbase + wm * 128 + x * 32, gc0 = cbase + wn * 64 + y * 32;
       if (gr0 >= rend || gc0 >= n) continue;  // wave-uniform
-      const int64_t gc = gc0 + fr;
-      const double dc = (norm && gc < n) ? o.dsq[gc] : 1.0;
+      // the raw counts into the LDS sub-tile (exact in T: counts < 2^24)
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int r = (g & 3) + 8 * (g >> 2) + 4 * fh;
-        const int64_t gr = gr0 + r;
-        const int v = acc[x][y][g];
-        T val;
-        if constexpr (DT == KMG_I32) {
-          val = v;
-        } else {
-          double d = (double)v;
-          if (norm) d = (gr == gc) ? 1.0 : (gr < rend && gc < n ? d / (o.dsq[gr] * dc) : 0.0);
-          val = (T)d;
-        }
-        tile[r * PITCH + ecol(r, fr)] = val;
+        tile[r * PITCH + ecol(r, fr)] = (T)acc[x][y][g];
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile is in LDS
       __builtin_amdgcn_wave_barrier();
-      // rows of the sub-tile: 32 rows x (32 / V) chunks of 16 B
+      // rows of the sub-tile: 32 rows x (32 / V) chunks of 16 B; normalize_K here, V
+      // columns of one row a lane, the division unconditional (no branch around it: the
+      // per-element branches of the bounded form were ~2x the epilogue's VALU), one
+      // iteration at a time (16 divisions in flight spilled)
       constexpr int CPR = 32 / V;
+      const int c4l = (lane % CPR) * V;  // the lane's columns: the same in every iteration
+      double dcv[V];
 #pragma unroll
+      for (int q = 0; q < V; ++q) dcv[q] = norm ? o.dsq[min(gc0 + c4l + q, n - 1)] : 1.0;
+#pragma unroll 2
       for (int it = 0; it < (32 * CPR) / 64; ++it) {
         const int ch = lane + 64 * it;
-        const int r = ch / CPR, c4 = (ch - r * CPR) * V;
+        const int r = ch / CPR, c4 = c4l;
         const int64_t gr = gr0 + r, gc = gc0 + c4;
         if (gr >= rend) continue;
         T v[V];
 #pragma unroll
         for (int q = 0; q < V; ++q) v[q] = tile[r * PITCH + ecol(r, c4) + q];
+        if constexpr (DT != KMG_I32) {
+          if (norm) {
+            const double dr = o.dsq[gr];
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+              const double qv = (double)v[q] / (dr * dcv[q]);
+              v[q] = (T)((gr == gc + q) ? 1.0 : qv);
+            }
+            if (mirror) {  // the mirror below reads the normalised values
+#pragma unroll
+              for (int q = 0; q < V; ++q) tile[r * PITCH + ecol(r, c4) + q] = v[q];
+            }
+          }
+        }
         T *dst = (T *)o.out + (gr - row0) * o.ld + gc;
         if (vec_ok && gc + V <= n) {
           store16(dst, v);
@@ -377,6 +387,8 @@ __global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_e
         }
       }
       if (mirror) {  // K[gc][gr] = K[gr][gc]: output row c of the sub-tile is column c
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the normalised rows are in LDS
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int it = 0; it < (32 * CPR) / 64; ++it) {
           const int ch = lane + 64 * it;
