@@ -111,8 +111,6 @@ struct Tuning {
                             // was removed in round 5: measured slower than the lists at k = 9)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
                             // (0 auto)
-  int nb_wgcu = 2;          // KMG_NB_WGCU: neighbourhood-list Gram workgroups a CU the chunk's
-                            // LDS accumulator is sized for (2: chunks <= ~20000; 1: <= ~40000)
   int nb_unroll = 0;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8;
                             // 0 auto: 8, or 4 for an upper-block-triangle build or packed
                             // lists -- profiles/r04x2_nb_unroll_ab.jsonl; column block N=200000
@@ -146,8 +144,6 @@ struct Tuning {
   int dense_bk = 128;       // KMG_DENSE_BK: dense Gram k-stage bytes, 64 or 128 (128: half the
                             // barriers; MM k=7 N=20000 3.38 -> 3.13 ms, k=6 0.92 -> 0.87,
                             // SP k=5 0.38 -> 0.367; profiles/r02ay_dense_bk_ab.jsonl)
-  int dense_stages = 2;     // KMG_DENSE_STAGES: LDS ring stages of the dense Gram's k loop (2, or
-                            // with 64-byte stages 3 / 4: more DMA in flight)
   int dense_half = -1;      // KMG_DENSE_HALF: dense Gram tiles over two 4-wave workgroups (BK
                             // 64), -1: when dp <= 1024 (SP k=5 N=20000 0.41 -> 0.39 ms; at
                             // dp >= 4096 BK 128 wins; profiles/r02bj_dense_epilogue_ab.jsonl)
@@ -179,7 +175,6 @@ void read_tuning(Tuning &t) {
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_pack_reads = env_or("KMG_NB_PACK_READS", d.nb_pack_reads);
   t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
-  t.nb_wgcu = env_or("KMG_NB_WGCU", d.nb_wgcu) == 1 ? 1 : 2;
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
@@ -187,7 +182,6 @@ void read_tuning(Tuning &t) {
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   t.dense_half = env_or("KMG_DENSE_HALF", d.dense_half);
-  t.dense_stages = env_or("KMG_DENSE_STAGES", d.dense_stages);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -563,12 +557,13 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
 // 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
 // mirror.  Largest chunk: the int32 LDS accumulator beside the row tables, and where
 // segment 2 packs, the sorted fill's LDS buffer (nb_sorted_max_chunk: ~24900 at k = 9).
-int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted,
-             int wgcu) {
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted) {
   // two workgroups a CU (their table builds, epilogues and streams overlap; one a CU measured
   // 22 % slower at N=20000, profiles/r05g_*): the accumulator, 16 dummy columns and the row
   // table in 80 KB (1024 threads) or 40 KB (512)
-  const int64_t lds_words = (threads == 512 ? 40 : 80) * (wgcu == 1 ? 2 : 1) * 1024 / 4;
+  // (sizing for one workgroup a CU, chunks up to ~40000, measured slower for the config-5
+  // slab too: Gram 26.0 -> 30.5 ms, profiles/r05v.jsonl)
+  const int64_t lds_words = (threads == 512 ? 40 : 80) * 1024 / 4;
   int64_t max_chunk = (lds_words - 16 - 4 * (int64_t)pmax - 2 - ldp) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
   const int smax = sorted ? nb_sorted_max_chunk(k, pmax) : 0;
@@ -746,8 +741,7 @@ int gram_dense(kmg_ctx *c, int k, int m, int window, const uint8_t *d_codes,
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
     return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
                              c->tune.dense_bk,
-                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0,
-                             c->tune.dense_stages);
+                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0);
   });
 }
 
@@ -794,8 +788,7 @@ int gram_gappy_intended(kmg_ctx *c, int k, int g, int window, const uint8_t *d_c
     if (dense_tile_order(c, n, r0, r1, dp, &order) != KMG_OK) return hipErrorInvalidValue;
     return launch_gram_dense(c->feat.as<int8_t>(), dp, n, r0, r1, order, oq, c->stream,
                              c->tune.dense_bk,
-                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0,
-                             c->tune.dense_stages);
+                             c->tune.dense_half < 0 ? dp <= 1024 : c->tune.dense_half != 0);
   });
 }
 
@@ -1119,13 +1112,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           int64_t rows_read = 0;
           for (const RowRange &r : ranges) rows_read += r.row1 - r.row0;
           const int ch = nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
-                                  true, c->tune.nb_wgcu);
+                                  true);
           const int64_t nch = (ncols + ch - 1) / ch;
           const double f = (tri_esz > 0 && nch > 1) ? (double)(nch + 1) / (2.0 * nch) : 1.0;
           sorted = (double)rows_read * g.pmax / (double)pow4(k) * f >= (double)c->tune.nb_pack_reads;
         }
         choose_chunks(gc, nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
-                                   sorted, c->tune.nb_wgcu));
+                                   sorted));
         g.chunk = gc.chunk;
         g.nchunks = gc.nchunks;
         o.tri = tri_esz > 0 && g.nchunks > 1;

@@ -122,18 +122,12 @@ constexpr int DT_BM = 256;
 constexpr int DT_EPI = 8 * 1024;                  // LDS bytes per wave for the epilogue (32 x 32 x 8 B)
 // BK = bytes of F per stage: 64 (32 KB of A + B per stage) or 128 (64 KB, half the
 // barriers per k; dp >= 1024)
-// NS = stages in the LDS ring (NS - 1 in flight while one is multiplied)
-template <int BK, bool HALF = false, int NS = 2>
+// (a 3- / 4-stage ring of 64-byte stages measured no faster: the k loop is not bound by the
+// DMA latency, profiles/r05aa_dense.jsonl)
+template <int BK, bool HALF = false>
 constexpr int dt_lds() {
   constexpr int nw = HALF ? 4 : 8, stage = (DT_BM + (HALF ? DT_BM / 2 : DT_BM)) * BK;
-  return nw * DT_EPI > NS * stage ? nw * DT_EPI : NS * stage;
-}
-
-// s_waitcnt vmcnt(V) (V < 16), expcnt / lgkmcnt left alone
-template <int V>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(V >= 0 && V < 16, "vmcnt immediate");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | V);
+  return nw * DT_EPI > 2 * stage ? nw * DT_EPI : 2 * stage;
 }
 
 // 16-byte chunk c16 of row `row` in a stage: XOR-swizzled so the fragment reads of 16
@@ -162,7 +156,7 @@ __device__ __forceinline__ void store16(T *p, const T (&v)[16 / sizeof(T)]) {
   __builtin_nontemporal_store(x, (v4i_t *)p);
 }
 
-template <int DT, bool SYM, int DT_BK, bool HALF, int NS>
+template <int DT, bool SYM, int DT_BK, bool HALF>
 __global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_eu(HALF ? 2 : 1, 2))) void gram_dense_kernel(const int8_t *__restrict__ F, int dp,
                                                             int64_t n, int64_t row0, int64_t rows,
                                                             int tiles_m, int tiles_n, int64_t ntiles,
@@ -281,37 +275,17 @@ __global__ __launch_bounds__(HALF ? 256 : 512) __attribute__((amdgpu_waves_per_e
                                          16, 0, 0);
     };
     const int nst = dp / DT_BK;
-    if constexpr (NS == 2) {
-      issue(lds, 0);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA has landed
-      __syncthreads();
-      for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        const bool more = st + 1 < nst;
-        if (more) issue(lds + (buf ^ 1) * DT_STAGE, (st + 1) * DT_BK);  // read in stage st-1
-        mfma_stage(lds + buf * DT_STAGE);
-        if (more) {
-          __builtin_amdgcn_s_waitcnt(0x0F70);
-          __syncthreads();
-        }
-      }
-    } else {
-      // a ring of NS stages, NS - 1 of them in flight: stage st's DMA was issued NS - 1
-      // stages earlier, so the fabric latency hides behind NS - 1 stages of MFMA work (one
-      // stage in flight left the MFMA pipes ~24 % busy at MM k=6, N=9000)
-      constexpr int LPS = NIA + NIB;  // DMA instructions a wave issues per stage
-#pragma unroll
-      for (int q = 0; q < NS - 1; ++q)
-        if (q < nst) issue(lds + q * DT_STAGE, q * DT_BK);
-      for (int st = 0; st < nst; ++st) {
-        // this wave's DMA of stage st has landed once at most the later stages' are left
-        const int ahead = min(NS - 2, nst - 1 - st);
-        if (ahead >= 2) wait_vmcnt<(2 * LPS < 16 ? 2 * LPS : 15)>();
-        else if (ahead == 1) wait_vmcnt<LPS>();
-        else wait_vmcnt<0>();
-        __syncthreads();  // every wave's DMA of stage st; every wave done with stage st - 1
-        if (st + NS - 1 < nst) issue(lds + ((st + NS - 1) % NS) * DT_STAGE, (st + NS - 1) * DT_BK);
-        mfma_stage(lds + (st % NS) * DT_STAGE);
+    issue(lds, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA has landed
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      const int buf = st & 1;
+      const bool more = st + 1 < nst;
+      if (more) issue(lds + (buf ^ 1) * DT_STAGE, (st + 1) * DT_BK);  // read in stage st-1
+      mfma_stage(lds + buf * DT_STAGE);
+      if (more) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
       }
     }
   }
@@ -541,12 +515,10 @@ hipError_t launch_gappy_features(const uint8_t *codes, int64_t ldc, int64_t n, i
 
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
                              const uint32_t *order, const OutSpec &o, hipStream_t s, int bk,
-                             bool half, int stages) {
+                             bool half) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || n <= 0) return hipSuccess;
   if (bk != 128 || (dp & 127) || half) bk = 64;
-  if (bk == 128) stages = 2;  // (3 stages of 64 KB exceed the LDS)
-  stages = half ? (stages >= 3 ? 3 : 2) : (stages >= 4 ? 4 : stages == 3 ? 3 : 2);
   if (dp & 63) return hipErrorInvalidValue;
   const bool sym = row0 == 0 && rows == n;
   const int tiles_m = (int)((rows + DT_BM - 1) / DT_BM);
@@ -554,24 +526,14 @@ hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, i
   const int64_t total = sym ? (int64_t)tiles_n * (tiles_n + 1) / 2 : (int64_t)tiles_m * tiles_n;
   if (total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)(((half ? 2 * total : total) + 7) & ~7LL);
-#define KMG_DENSE_GO(DTV, SY, BKV, HV, NSV)                                                     \
-  hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, BKV, HV, NSV>), dim3(grid), dim3(HV ? 256 : 512), \
-                     (dt_lds<BKV, HV, NSV>()), s, F, dp, n, row0, rows, tiles_m, tiles_n, total,  \
-                     order, o)
+#define KMG_DENSE_GO(DTV, SY, BKV, HV)                                                          \
+  hipLaunchKernelGGL((gram_dense_kernel<DTV, SY, BKV, HV>), dim3(grid), dim3(HV ? 256 : 512),      \
+                     (dt_lds<BKV, HV>()), s, F, dp, n, row0, rows, tiles_m, tiles_n, total, order, o)
 #define KMG_DENSE(DTV, SY)                                                      \
   do {                                                                          \
-    if (half) {                                                                 \
-      if (stages == 3) KMG_DENSE_GO(DTV, SY, 64, true, 3);                      \
-      else KMG_DENSE_GO(DTV, SY, 64, true, 2);                                  \
-    } else if (bk == 128) {                                                     \
-      KMG_DENSE_GO(DTV, SY, 128, false, 2);                                     \
-    } else if (stages == 4) {                                                   \
-      KMG_DENSE_GO(DTV, SY, 64, false, 4);                                      \
-    } else if (stages == 3) {                                                   \
-      KMG_DENSE_GO(DTV, SY, 64, false, 3);                                      \
-    } else {                                                                    \
-      KMG_DENSE_GO(DTV, SY, 64, false, 2);                                      \
-    }                                                                           \
+    if (half) KMG_DENSE_GO(DTV, SY, 64, true);                                  \
+    else if (bk == 128) KMG_DENSE_GO(DTV, SY, 128, false);                      \
+    else KMG_DENSE_GO(DTV, SY, 64, false);                                      \
   } while (0)
   switch (o.dtype) {
     case KMG_I32:

@@ -338,7 +338,7 @@ hipError_t launch_dense_features(const uint8_t *codes, const int32_t *lens, int6
                                  int8_t *F, double *diagv, double *dsq, hipStream_t s);
 hipError_t launch_gram_dense(const int8_t *F, int dp, int64_t n, int64_t row0, int64_t row1,
                              const uint32_t *order, const OutSpec &o, hipStream_t s, int bk = 64,
-                             bool half = false, int stages = 2);
+                             bool half = false);
 
 // kernel-combination consumers (kmg_combine.hip): K = device array of p matrix pointers
 #define KMG_COMBINE_PMAX 12
