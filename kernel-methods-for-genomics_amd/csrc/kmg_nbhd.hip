@@ -30,14 +30,18 @@
 //   nb_count_kernel   per (c, u): n0, n1, n2 from the exact index (1 + 3k + 9k(k-1)/2
 //                     lookups of its bin offsets, L2-resident) -> 16-bit pieces and segment ends
 //   launch_scan       list starts (in pieces; < 2^32: checked by the host)
-//   list fills        (launch_nb_fill picks one)
-//     nb_fill_sorted_kernel   default where segment 2 packs: one workgroup per 16 k-mers
-//                     sharing a (k-2)-letter prefix, one wave a list: segments 0 / 1 copied
-//                     into the table, segment 2 counting-sorted by column >> 6 in a per-wave
-//                     LDS buffer, then packed 15 entries a lane
-//     nb_fill_grouped_kernel  16-bit lists (k >= 10): the same groups, lane-per-run copies
-//     nb_fill_pieces_kernel   16-bit lists past 8.5 occurrences a k-mer and chunk: the
-//                     ranges as an LDS image (16-byte loads), each list assembled 16 B a lane
+//   list fills        (launch_nb_fill picks one; all take one workgroup per 16 k-mers sharing
+//                     a (k-2)-letter prefix, the group's range offsets loaded once, one wave a list)
+//     nb_fill_sorted_kernel   packed segment 2, where a list is read often enough to repay
+//                     the sort (the host's reads rule): runs staged in a per-wave LDS buffer,
+//                     segments 0 / 1 stored with 16-byte stores, segment 2 counting-sorted by
+//                     column >> 6, then packed 15 entries a lane
+//     nb_fill_staged_kernel   16-bit lists (the default elsewhere): the whole list staged in
+//                     LDS, stored with 16-byte stores
+//     nb_fill_grouped_kernel  lane-per-run copies straight from the index (forced, and the
+//                     other fills' fallback for lists past their LDS buffers)
+//     nb_fill_pieces_kernel   16-bit lists past 8.5 occurrences a k-mer and chunk where the
+//                     staged fill's buffer is too small: the ranges as an LDS image
 //   gram_nb_kernel   per (row i, chunk c): row windows -> (list start, pieces, segment
 //                     ends) in LDS, prefix sums over the row's 16-bit and packed pieces, then
 //                     every wave streams an equal share of each, 16 bytes a lane, adding the
@@ -46,7 +50,8 @@
 //
 // Roofline: the lists are read from HBM once per (row, chunk): N=20000 ~270 KB a row (packed;
 // 466 KB as 16-bit lists) against the 160 KB float64 K row; the bound is HBM (list reads +
-// K writes) beside the LDS adds (one ds_add per entry).
+// K writes) beside the LDS adds (one ds_add per entry).  Column blocks (kmg_gram_device_cols)
+// build the lists over a block's sequences and stream them for every row.
 #include "kmg_rowacc.h"
 
 namespace kmg {
