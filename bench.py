@@ -909,10 +909,19 @@ def _compact_record(rec):
 
 
 def _compact_configs(extra):
+    """The configs' times for the stdout tail: no workload text (bench_details.json has it),
+    the stages that carry the time, the plan's shape."""
     out = {}
     for k, v in extra.items():
         if k.startswith("config") and isinstance(v, dict):
-            out[k] = _compact_record(v)
+            rec = {kk: _r(v[kk]) for kk in ("ms_per_step", "spot_check", "gram_hbm_frac") if kk in v}
+            st = v.get("stages_ms") or {}
+            rec["stages_ms"] = {kk: _r(st[kk], 3) for kk in ("nbfill", "diag", "gram", "mirror")
+                                if kk in st}
+            pl = v.get("plan") or {}
+            if pl:
+                rec["plan"] = {kk: pl.get(kk) for kk in ("formulation", "nchunks", "packed") if kk in pl}
+            out[k] = rec
     if isinstance(extra.get("run_py_kernels_n9000"), dict):
         out["run_py_kernels_n9000_total_ms"] = _r(extra["run_py_kernels_n9000"].get("total_ms"))
     return out
