@@ -119,6 +119,8 @@ struct Tuning {
                             // list is read >= nb_pack_reads times and nb_sorted_cap allows;
                             // else staged 16-bit lists), 1 sorted, 2 grouped lane-per-run,
                             // 3 piece-assembled, 4 staged (launch_nb_fill)
+  int nb_fill_threads = 512;  // KMG_NB_FILL_THREADS: staged fill workgroup, 512 (two a CU where
+                              // a list fits their buffers) or 1024
   int nb_pack_reads = 16;   // KMG_NB_PACK_READS: reads a list must get for the packed segment 2
                             // (its sort costs ~1 ms more at N=20000, k=9; each read of the
                             // list saves ~0.9 of its 16-bit segment-2 bytes)
@@ -174,6 +176,7 @@ void read_tuning(Tuning &t) {
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_pack_reads = env_or("KMG_NB_PACK_READS", d.nb_pack_reads);
+  t.nb_fill_threads = env_or("KMG_NB_FILL_THREADS", d.nb_fill_threads);
   t.nb_unroll = env_or("KMG_NB_UNROLL", d.nb_unroll);
   if (t.nb_threads != 512 && t.nb_threads != 1024) t.nb_threads = 0;
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
@@ -1160,7 +1163,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
                                               c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                               c->nb_use.as<uint2>(), c->nb_lines.as<uint16_t>(),
                                               c->stream,
-                                              c->tune.nb_fill != 0 ? c->tune.nb_fill : sorted ? 0 : 5);
+                                              c->tune.nb_fill != 0 ? c->tune.nb_fill : sorted ? 0 : 5,
+                                              c->tune.nb_fill_threads);
           if (e == hipErrorInvalidValue && c->tune.nb_fill == 1)
             return fail(KMG_EUNSUPPORTED, "KMG_NB_FILL=1: no sorted fill at k=%d, chunk %d", k, g.chunk);
           KMG_HIP(e);

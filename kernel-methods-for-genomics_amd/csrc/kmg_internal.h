@@ -255,7 +255,7 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 // buffer, else the piece-assembled fill past 8.5 occurrences a k-mer and chunk, else grouped)
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint2 *nbuse,
-                          uint16_t *table, hipStream_t s, int form = 0);
+                          uint16_t *table, hipStream_t s, int form = 0, int fill_threads = 512);
 hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const uint32_t *nboff,
                                     const uint2 *nbseg, const uint2 *nbuse, const uint4 *table,
                                     int64_t row0, int64_t row1, int w0, int w1, int w2,

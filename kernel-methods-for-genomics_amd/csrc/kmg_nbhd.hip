@@ -691,12 +691,12 @@ __global__ __launch_bounds__(1024) void nb_fill_sorted_kernel(
 // Writes that a lane does not need go to its own trash word (no exec-mask branching).  The
 // runs of iteration i + 1 are loaded before iteration i's writes.  Lists past the buffer take
 // the lane-per-run copies.
-template <int K>
-__global__ __launch_bounds__(1024) void nb_fill_staged_kernel(
+template <int K, int NT>
+__global__ __launch_bounds__(NT) void nb_fill_staged_kernel(
     int64_t ngroups, const uint32_t *__restrict__ xoff, const uint16_t *__restrict__ xent,
     const uint32_t *__restrict__ nboff, const uint2 *__restrict__ nbseg, uint2 *__restrict__ nbuse,
     uint16_t *__restrict__ table, uint32_t pad_col, int cap16) {
-  constexpr int S = 2, SW = 16, NT = 1024, NW = NT / 64;
+  constexpr int S = 2, SW = 16, NW = NT / 64;
   constexpr int kp = K - S;
   constexpr int mr = 1 + 3 * kp + 9 * kp * (kp - 1) / 2;  // prefix ranges
   constexpr int nbn = 1 + 3 * K + 9 * K * (K - 1) / 2;
@@ -1314,7 +1314,7 @@ hipError_t launch_nb_count(const IndexGeom &g, const uint32_t *xoff, uint32_t *h
 
 hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16_t *xent,
                           const uint32_t *nboff, const uint2 *nbseg, uint2 *nbuse,
-                          uint16_t *table, hipStream_t s, int form) {
+                          uint16_t *table, hipStream_t s, int form, int fill_threads) {
   const int64_t nbins = g.nbins();
   if (g.copies != 1 || g.k < 4 || g.k > 12) return hipErrorInvalidValue;
   const uint32_t pad_col = (uint32_t)(((g.chunk + 3) >> 2) << 2);
@@ -1345,16 +1345,25 @@ hipError_t launch_nb_fill(const IndexGeom &g, const uint32_t *xoff, const uint16
     // staged 16-bit fill: the whole list in a per-wave LDS buffer, 16-byte stores
     // (lists are sums of ~350 runs: their sizes stay within a few % of the mean; the rare
     // longer one takes the lane-per-run copies)
-    const int cap16 = ((160 * 1024 / 4 - nb_staged_table_words(g.k)) / 16 * 2) & ~7;
+    // 512-thread workgroups, two a CU, each with its own groups and barriers, where a list
+    // fits their smaller per-wave buffer (N=20000 fill 0.62 -> 0.60 ms, rank slab 5.50 ->
+    // 5.40, profiles/r05at_fill_threads.jsonl); else 1024
     const double mean_list = (double)(1 + 3 * g.k + 9 * g.k * (g.k - 1) / 2) * mean;
+    const int cap512 = ((80 * 1024 / 4 - nb_staged_table_words(g.k)) / 8 * 2) & ~7;
+    const bool w512 = fill_threads == 512 && cap512 >= 1.08 * mean_list + 192;
+    const int cap16 = w512 ? cap512 : ((160 * 1024 / 4 - nb_staged_table_words(g.k)) / 16 * 2) & ~7;
     if (cap16 >= 1.08 * mean_list + 192 && (((uintptr_t)xent) & 3u) == 0) {
-      const size_t lds = 4 * ((size_t)nb_staged_table_words(g.k) + 16 * (size_t)(cap16 / 2));
-      const int64_t blocks = std::min<int64_t>(ngroups, 256);
+      const size_t lds = 4 * ((size_t)nb_staged_table_words(g.k) + (w512 ? 8 : 16) * (size_t)(cap16 / 2));
+      const int64_t blocks = std::min<int64_t>(ngroups, w512 ? 512 : 256);
       switch (g.k) {
 #define KMG_NB_STAGED(KK)                                                                        \
   case KK:                                                                                       \
-    hipLaunchKernelGGL(nb_fill_staged_kernel<KK>, dim3((unsigned)blocks), dim3(1024), lds, s,    \
-                       ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16);         \
+    if (w512)                                                                                    \
+      hipLaunchKernelGGL((nb_fill_staged_kernel<KK, 512>), dim3((unsigned)blocks), dim3(512), lds, \
+                         s, ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16);    \
+    else                                                                                         \
+      hipLaunchKernelGGL((nb_fill_staged_kernel<KK, 1024>), dim3((unsigned)blocks), dim3(1024),  \
+                         lds, s, ngroups, xoff, xent, nboff, nbseg, nbuse, table, pad_col, cap16); \
     break;
         KMG_NB_STAGED(4) KMG_NB_STAGED(5) KMG_NB_STAGED(6) KMG_NB_STAGED(7) KMG_NB_STAGED(8)
         KMG_NB_STAGED(9) KMG_NB_STAGED(10) KMG_NB_STAGED(11) KMG_NB_STAGED(12)
