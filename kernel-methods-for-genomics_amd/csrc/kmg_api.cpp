@@ -138,7 +138,8 @@ struct Tuning {
   int idx_buckets = 0;      // KMG_IDX_BUCKETS: coarse buckets (0: 384 spectrum / 1024 mismatch)
   int idx_threads = 1024;   // KMG_IDX_THREADS
   int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
-  int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky
+  int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky (implies KMG_CHOL=0)
+  int chol = 1;             // KMG_CHOL: 1 blocked Cholesky + solves (chol_factor), 0 rocSOLVER potrf/potrs
   int sp_store = 0;         // KMG_SP_STORE: spectrum K stores, 0 auto, 1 non-temporal, 2 plain
   int sp_order = 1;         // KMG_SP_ORDER: spectrum grid, 0 row-major, 1 chunk-major (N=100000:
                             // Gram 6.66 -> 5.85 ms, interleaved A/B profiles/r02aq_sp_order_ab.jsonl)
@@ -168,6 +169,7 @@ void read_tuning(Tuning &t) {
   t.idx_threads = env_or("KMG_IDX_THREADS", d.idx_threads);
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
+  t.chol = env_or("KMG_CHOL", d.chol);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
   t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
   t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
@@ -215,6 +217,7 @@ struct kmg_ctx {
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
+  DevBuf sv_inv, sv_panel;         // blocked Cholesky: diagonal-block inverses, panel / sweep scratch
   rocblas_handle blas = nullptr;   // rocBLAS/rocSOLVER handle bound to `stream` (lazy)
   int masks_k = -1, masks_m = -1, nmask = 0;
   DevBuf h_codes, h_lens, h_out;  // host-path staging on the device
@@ -1458,7 +1461,7 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->h_lens, &c->h_out, &c->feat,    &c->masks,  &c->slots, &c->packed,
                     &c->pr_summary, &c->pr_rtot, &c->pr_rbase, &c->pr_cursor, &c->pr_lines,
                     &c->hcnt,  &c->hstart, &c->cmb_k, &c->cmb_ptrs, &c->cmb_vec,
-                    &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info,
+                    &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info, &c->sv_inv, &c->sv_panel,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
                     &c->gcoef, &c->feat32, &c->k32, &c->ft_cols,
                     &c->nb_seg, &c->nb_use, &c->nb_lines};
@@ -2333,6 +2336,62 @@ static int is_asymmetric(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, b
   return KMG_OK;
 }
 
+// Right-looking blocked Cholesky of the symmetric n x n B (column-major lower, ld n) in
+// place, 128-column blocks: the diagonal block and its inverse Y in one workgroup
+// (launch_chol_diag), the panel below it as one GEMM (L21 = A21 Y^T, into sv_panel, copied
+// back), the trailing triangle by one rank-128 update (rocBLAS syrk, A22 -= L21 L21^T).
+// rocSOLVER's potrf issues ~22 kernels a block at n = 9000 (trtri, copies, recursive GEMMs;
+// profiles/r05ba_*).  The inverses (Y and Y^T of every block) stay in sv_inv for chol_solve.
+// *info (device) ends 0 or the 1-based column of the first non-positive pivot; nothing is
+// read back here.
+static constexpr int CHOL_BLK = 128;
+static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
+  const int64_t nblk = (n + CHOL_BLK - 1) / CHOL_BLK;
+  KMG_TRY(c->sv_inv.ensure(sizeof(double) * 2 * CHOL_BLK * CHOL_BLK * (size_t)nblk));
+  KMG_TRY(c->sv_panel.ensure(sizeof(double) * CHOL_BLK * (size_t)n));
+  double *inv = c->sv_inv.as<double>(), *T = c->sv_panel.as<double>();
+  const double one = 1.0, mone = -1.0, zero = 0.0;
+  KMG_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), c->stream));
+  for (int64_t b = 0; b < nblk; ++b) {
+    const int64_t j0 = b * CHOL_BLK;
+    const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
+    double *Ajj = B + j0 + j0 * n, *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
+    KMG_HIP(launch_chol_diag(Ajj, n, jb, (int)j0, (int *)info, Y, Y + CHOL_BLK * CHOL_BLK, c->stream));
+    const rocblas_int m = (rocblas_int)(n - j0 - jb);
+    if (m == 0) break;
+    double *A21 = Ajj + jb;
+    KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb, jb, &one,
+                           A21, (rocblas_int)n, Y, CHOL_BLK, &zero, T, m));
+    KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, m, jb, &mone, T, m, &one,
+                           A21 + (size_t)jb * n, (rocblas_int)n));
+    KMG_HIP(hipMemcpy2DAsync(A21, sizeof(double) * n, T, sizeof(double) * m, sizeof(double) * m, jb,
+                             hipMemcpyDeviceToDevice, c->stream));
+  }
+  return KMG_OK;
+}
+
+// x = (L L^T)^-1 b in place for chol_factor's L and inverses: a forward sweep into sv_panel
+// then a backward sweep back into b, one launch_tri_sweep a block each (rocSOLVER's potrs
+// runs two rocBLAS trsv at ~2.3 ms each at n = 9000, latency-bound;
+// profiles/r05z_downstream_kernel_stats.csv).
+static int chol_solve(kmg_ctx *c, const double *L, int64_t n, double *b) {
+  const int64_t nblk = (n + CHOL_BLK - 1) / CHOL_BLK;
+  const double *inv = c->sv_inv.as<double>();
+  double *y = c->sv_panel.as<double>();
+  for (int64_t k = 0; k < nblk; ++k) {  // L y = b (b's trailing rows updated in place)
+    const int64_t j0 = k * CHOL_BLK;
+    const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
+    KMG_HIP(launch_tri_sweep(L, n, inv + 2 * CHOL_BLK * CHOL_BLK * k, j0, jb, 0, b, y, c->stream));
+  }
+  for (int64_t k = nblk - 1; k >= 0; --k) {  // L^T x = y (y's leading rows updated in place)
+    const int64_t j0 = k * CHOL_BLK;
+    const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
+    KMG_HIP(launch_tri_sweep(L, n, inv + 2 * CHOL_BLK * CHOL_BLK * k + CHOL_BLK * CHOL_BLK, j0, jb, 1, y,
+                             b, c->stream));
+  }
+  return KMG_OK;
+}
+
 // Build the system into sv_mat (build()), factorise, solve in place into rhs.
 // B = diag(s) K diag(s) + shift I is symmetric when K is, so its row-major image is its
 // own column-major image and rocSOLVER's column-major routines apply unchanged; an
@@ -2357,13 +2416,20 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs, bool as
   }
   // B is symmetric: either triangle is the matrix (KMG_POTRF_UPPER selects rocSOLVER's
   // upper-triangle variant)
+  const bool own = c->tune.chol && !c->tune.potrf_upper;
   const rocblas_fill fill = c->tune.potrf_upper ? rocblas_fill_upper : rocblas_fill_lower;
-  KMG_BLAS(rocsolver_dpotrf(c->blas, fill, ni, B, ni, info));
+  if (own)
+    KMG_TRY(chol_factor(c, B, n, info));
+  else
+    KMG_BLAS(rocsolver_dpotrf(c->blas, fill, ni, B, ni, info));
   KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
   KMG_HIP(hipStreamSynchronize(c->stream));
   if (hinfo == 0) {
     c->last_factor = KMG_FACTOR_CHOLESKY;
-    KMG_BLAS(rocsolver_dpotrs(c->blas, fill, ni, 1, B, ni, rhs, ni));
+    if (own)
+      KMG_TRY(chol_solve(c, B, n, rhs));
+    else
+      KMG_BLAS(rocsolver_dpotrs(c->blas, fill, ni, 1, B, ni, rhs, ni));
     return KMG_OK;
   }
   c->last_factor = KMG_FACTOR_LU_INDEFINITE;
@@ -2477,7 +2543,11 @@ static int svm_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     if (gap <= tol * std::max(1.0, std::fabs(h[2])) && h[1] <= tol) break;
     // M = YKY + diag(D), factorised once, solved for the predictor and the corrector
     KMG_HIP(launch_shift_scale(d_K, ld, d_y, 0.0, D, n, B, n, c->stream));
-    KMG_BLAS(rocsolver_dpotrf(c->blas, rocblas_fill_lower, ni, B, ni, info));
+    const bool own = c->tune.chol != 0;
+    if (own)
+      KMG_TRY(chol_factor(c, B, n, info));
+    else
+      KMG_BLAS(rocsolver_dpotrf(c->blas, rocblas_fill_lower, ni, B, ni, info));
     rocblas_int hinfo = 0;
     KMG_HIP(hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, c->stream));
     KMG_HIP(hipStreamSynchronize(c->stream));
@@ -2493,6 +2563,8 @@ static int svm_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     auto solve = [&]() -> int {
       if (lu)
         KMG_BLAS(rocsolver_dgetrs(c->blas, rocblas_operation_transpose, ni, 1, B, ni, ipiv, rhs, ni));
+      else if (own)
+        KMG_TRY(chol_solve(c, B, n, rhs));
       else
         KMG_BLAS(rocsolver_dpotrs(c->blas, rocblas_fill_lower, ni, 1, B, ni, rhs, ni));
       return KMG_OK;

@@ -358,6 +358,14 @@ hipError_t launch_alignf(const double *const *K, int p, const double *y, int64_t
 hipError_t launch_shift_scale(const double *K, int64_t ldk, const double *s, double shift,
                               const double *dvec, int64_t n, double *B, int64_t ldb,
                               hipStream_t st);
+// blocked Cholesky (kmg_solve.hip): one diagonal block (nb <= 128) factorised in place
+// (column-major lower) plus its inverse Y and Y^T (ld 128); a non-positive pivot sets *info
+// (1-based column j0 + j + 1); returns at once if *info != 0
+hipError_t launch_chol_diag(double *A, int64_t lda, int nb, int j0, int *info, double *Y, double *YT,
+                            hipStream_t st);
+// one block step of the substitution sweeps (forward: M = Y, back: M = Y^T)
+hipError_t launch_tri_sweep(const double *L, int64_t n, const double *M, int64_t j0, int jb, int back,
+                            double *src, double *dst, hipStream_t st);
 // *flag |= 1 when K is not exactly symmetric (flag must be zeroed before)
 hipError_t launch_asymmetry(const double *K, int64_t ld, int64_t n, int *flag, hipStream_t st);
 // KLR IRLS step: s = sqrt(sig(m) sig(-m)), rhs = s * (m + y / sig(-y m))

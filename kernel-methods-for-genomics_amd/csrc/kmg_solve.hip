@@ -274,6 +274,315 @@ __global__ __launch_bounds__(256) void asym_kernel(const double *__restrict__ K,
   if (__any(diff) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// ------------------------------------------------------------------ blocked Cholesky
+// The diagonal blocks (nb <= CHOL_NB) of the right-looking blocked Cholesky (kmg_api.cpp
+// chol_factor).  chol_diag_kernel factorises one block with one 1024-thread workgroup, the
+// block held in registers 2-D block-cyclic: thread t owns rows (t & 31) + 32 i and columns
+// (t >> 5) + 32 j, so the shrinking trailing triangle stays spread over all threads.  A step
+// publishes columns j, j+1 through LDS (double-buffered: one barrier a step) and every owner
+// of a trailing element subtracts their rank-2 term; the columns are scaled by 1/sqrt of
+// their pivots at the end.  The step loop is latency-bound (the chain of 128 pivots); a version blocked by
+// 32-column panels with the pivot chain in one wave measured slower (314 vs 193 us a block
+// with the inverse; profiles/r05be_*), since one wave hides none of the LDS and fp64 latency.
+// A pivot <= 0 (or NaN) sets *info = j0 + j + 1 and leaves the block: the caller rebuilds and
+// falls back to LU, and every later block returns at once.
+constexpr int CHOL_NB = 128;
+constexpr int CHOL_SWEEP_ROWS = 128;       // rows of b a tri_sweep workgroup updates
+constexpr int CHOL_RT = 32;                // rows (and columns) of the thread grid
+constexpr int CHOL_S = CHOL_NB / CHOL_RT;  // owned rows / columns a thread
+
+// 1/d to within an ulp or so: v_rcp_f64 and two Newton steps (a division's fix-up
+// sequence is ~3x the instructions, on every wave of the step loop)
+__device__ __forceinline__ double chol_recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+}
+
+__global__ __launch_bounds__(1024) void chol_diag_kernel(double *__restrict__ A, int64_t lda, int nb,
+                                                         int j0, int *__restrict__ info) {
+  __shared__ double cb[2][2][CHOL_NB];  // [step parity][column j / j+1]
+  if (*info != 0) return;               // an earlier block failed
+  const int r0 = (int)threadIdx.x & (CHOL_RT - 1), c0 = (int)threadIdx.x / CHOL_RT;
+  // Slots (ri, ci) with ri < ci lie above the diagonal (r < 32 ri + 32 <= c): never held.
+  // Slots with ri >= ci may still hold r < c or r >= nb: they are updated like the rest
+  // (their values are never stored), so the step loop carries no per-element masks; the
+  // column multipliers are zeroed instead where a column must not change, and slot columns
+  // that are finished are skipped by a wave-uniform branch.  Each step retires two columns
+  // j, j+1 behind one barrier: both are published as they stand after step j-1, and every
+  // thread applies column j to the entries of column j+1 it needs itself.
+  double a[CHOL_S][CHOL_S], pv[CHOL_S];
+  for (int t = threadIdx.x; t < 4 * CHOL_NB; t += blockDim.x) (&cb[0][0][0])[t] = 0.0;
+#pragma unroll
+  for (int ri = 0; ri < CHOL_S; ++ri)
+#pragma unroll
+    for (int ci = 0; ci <= ri; ++ci) {
+      const int r = r0 + CHOL_RT * ri, c = c0 + CHOL_RT * ci;
+      a[ri][ci] = (r < nb && c < nb && r >= c) ? A[r + (int64_t)c * lda] : 0.0;
+    }
+#pragma unroll
+  for (int ci = 0; ci < CHOL_S; ++ci) pv[ci] = 1.0;
+  __syncthreads();
+  for (int j = 0; j < nb; j += 2) {
+    double *b0 = cb[(j >> 1) & 1][0], *b1 = cb[(j >> 1) & 1][1];
+    const int j1 = j + 1;
+    const bool two = j1 < nb;
+    const int jq = j / CHOL_RT, jq1 = j1 / CHOL_RT;
+    if (c0 == (j & (CHOL_RT - 1))) {
+#pragma unroll
+      for (int ci = 0; ci < CHOL_S; ++ci)
+        if (ci == jq) {
+#pragma unroll
+          for (int ri = ci; ri < CHOL_S; ++ri) {
+            const int r = r0 + CHOL_RT * ri;
+            if (r >= j && r < nb) b0[r] = a[ri][ci];
+          }
+        }
+    }
+    if (two && c0 == (j1 & (CHOL_RT - 1))) {
+#pragma unroll
+      for (int ci = 0; ci < CHOL_S; ++ci)
+        if (ci == jq1) {
+#pragma unroll
+          for (int ri = ci; ri < CHOL_S; ++ri) {
+            const int r = r0 + CHOL_RT * ri;
+            if (r >= j1 && r < nb) b1[r] = a[ri][ci];
+          }
+        }
+    }
+    __syncthreads();
+    // every LDS read of the step at once (clamped, unconditional): one latency, not five
+    const int jc1 = min(j1, nb - 1);
+    const double d0 = b0[j], a10 = b0[jc1], a11 = b1[jc1];
+    double rw0[CHOL_S], rw1[CHOL_S], cl0[CHOL_S], cl1[CHOL_S];
+#pragma unroll
+    for (int q = 0; q < CHOL_S; ++q) {
+      const int r = min(r0 + CHOL_RT * q, nb - 1), c = min(c0 + CHOL_RT * q, nb - 1);
+      rw0[q] = b0[r];
+      rw1[q] = b1[r];
+      cl0[q] = b0[c];
+      cl1[q] = b1[c];
+    }
+    // (no branch between the reads and their use: a failed pivot is acted on after the
+    // update, whose values are then discarded)
+    const double rd0 = chol_recip(d0);
+    const double l10 = two ? a10 * rd0 : 0.0;  // a_{j+1,j} / a_jj
+    const double d1 = two ? __builtin_fma(-a10, l10, a11) : 1.0;
+    const double rd1 = chol_recip(d1);
+    // row factors: u0 = a_rj, u1 = a_r,j+1 after column j (rows below j only matter)
+    double u0[CHOL_S], u1[CHOL_S];
+#pragma unroll
+    for (int ri = 0; ri < CHOL_S; ++ri) {
+      u0[ri] = rw0[ri];
+      u1[ri] = __builtin_fma(-rw0[ri], l10, rw1[ri]);
+    }
+    if (c0 == (j1 & (CHOL_RT - 1))) {  // column j+1 itself, after column j
+#pragma unroll
+      for (int ci = 0; ci < CHOL_S; ++ci)
+        if (ci == jq1) {
+#pragma unroll
+          for (int ri = ci; ri < CHOL_S; ++ri) a[ri][ci] = u1[ri];
+        }
+    }
+#pragma unroll
+    for (int ci = 0; ci < CHOL_S; ++ci) {
+      if (CHOL_RT * ci + CHOL_RT - 1 <= j1) continue;  // slot columns all <= j+1: finished
+      const bool live = c0 + CHOL_RT * ci > j1;
+      const double lc0 = live ? cl0[ci] * rd0 : 0.0;
+      const double lc1 = live ? __builtin_fma(-cl0[ci], l10, cl1[ci]) * rd1 : 0.0;
+#pragma unroll
+      for (int ri = ci; ri < CHOL_S; ++ri)
+        a[ri][ci] = __builtin_fma(-u1[ri], lc1, __builtin_fma(-u0[ri], lc0, a[ri][ci]));
+    }
+    if (!(d0 > 0.0) || !(d1 > 0.0)) {  // not positive definite (or NaN): the same in every thread
+      if (threadIdx.x == 0) *info = j0 + (d0 > 0.0 ? j1 : j) + 1;
+      return;
+    }
+#pragma unroll
+    for (int ci = 0; ci < CHOL_S; ++ci) {
+      if (ci == jq && c0 == (j & (CHOL_RT - 1))) pv[ci] = d0;
+      if (two && ci == jq1 && c0 == (j1 & (CHOL_RT - 1))) pv[ci] = d1;
+    }
+    if (!two) break;
+  }
+  // L_rc = a_rc / sqrt(a_cc), L_cc = sqrt(a_cc)
+#pragma unroll
+  for (int ci = 0; ci < CHOL_S; ++ci) {
+    const int c = c0 + CHOL_RT * ci;
+    const double sd = __builtin_sqrt(pv[ci]), rs = 1.0 / sd;
+#pragma unroll
+    for (int ri = ci; ri < CHOL_S; ++ri) {
+      const int r = r0 + CHOL_RT * ri;
+      if (r < nb && c < nb && r >= c) A[r + (int64_t)c * lda] = r == c ? sd : a[ri][ci] * rs;
+    }
+  }
+}
+
+// LDS written by some lanes of the wave, read by others next (a wave's LDS ops run in order)
+__device__ __forceinline__ void chol_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Y = L^-1 for one factorised diagonal block, one column of Y a workgroup: the block's
+// columns are independent triangular solves L y = e_c, so the 128 pivot chains run side by
+// side on 128 CUs instead of one after another.  The workgroup's 16 waves stage columns
+// c.. of L in LDS (all loads in flight at once), then wave 0 alone runs the chain: lane l
+// holds rows l and l + 64; step k takes y_k from its owner lane (readlane) and every row
+// r > k subtracts L_rk y_k.  Writes Y and Y^T (128 x 128, ld CHOL_NB,
+// zero above the diagonal and past nb).
+__global__ __launch_bounds__(1024) void chol_inv_kernel(const double *__restrict__ L, int64_t lda, int nb,
+                                                        const int *__restrict__ info, double *__restrict__ Y,
+                                                        double *__restrict__ YT) {
+  extern __shared__ __align__(16) double ls[];  // [CHOL_NB][CHOL_NB + 1], columns >= c only
+  if (*info != 0) return;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  constexpr int LD = CHOL_NB + 1;
+  if (c >= nb) {  // zero column (block past nb)
+    if (tid < 64) {
+      Y[lane + c * CHOL_NB] = Y[lane + 64 + c * CHOL_NB] = 0.0;
+      YT[c + lane * CHOL_NB] = YT[c + (lane + 64) * CHOL_NB] = 0.0;
+    }
+    return;
+  }
+  double *dinv = ls + CHOL_NB * LD;  // 1 / L_kk
+  {  // stage columns c .. nb-1 with every load in flight at once (16 a thread)
+    const int row = tid & (CHOL_NB - 1), k0 = c + (tid >> 7);
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = L[min(row, nb - 1) + (int64_t)min(k0 + 8 * u, nb - 1) * lda];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (row < nb && k0 + 8 * u < nb) ls[row + (k0 + 8 * u) * LD] = v[u];
+  }
+  __syncthreads();
+  if (tid >= 64) return;
+  if (lane >= c && lane < nb) dinv[lane] = 1.0 / ls[lane + lane * LD];
+  if (lane + 64 >= c && lane + 64 < nb) dinv[lane + 64] = 1.0 / ls[lane + 64 + (lane + 64) * LD];
+  chol_wave_sync();
+  double b0 = lane == c ? 1.0 : 0.0, b1 = lane + 64 == c ? 1.0 : 0.0;
+  for (int k = c; k < nb; ++k) {
+    const double yk = (k < 64 ? readlane_f64(b0, k) : readlane_f64(b1, k - 64)) * dinv[k];
+    if (lane == (k & 63)) {
+      if (k < 64)
+        b0 = yk;
+      else
+        b1 = yk;
+    }
+    if (lane > k && lane < nb) b0 = __builtin_fma(-ls[lane + k * LD], yk, b0);
+    if (lane + 64 > k && lane + 64 < nb) b1 = __builtin_fma(-ls[lane + 64 + k * LD], yk, b1);
+  }
+  const double y0 = (lane >= c && lane < nb) ? b0 : 0.0;
+  const double y1 = (lane + 64 >= c && lane + 64 < nb) ? b1 : 0.0;
+  Y[lane + c * CHOL_NB] = y0;
+  Y[lane + 64 + c * CHOL_NB] = y1;
+  YT[c + lane * CHOL_NB] = y0;
+  YT[c + (lane + 64) * CHOL_NB] = y1;
+}
+
+hipError_t launch_chol_diag(double *A, int64_t lda, int nb, int j0, int *info, double *Y, double *YT,
+                            hipStream_t st) {
+  if (nb <= 0 || nb > CHOL_NB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(1024), 0, st, A, lda, nb, j0, info);
+  const size_t lds = sizeof(double) * (CHOL_NB * (CHOL_NB + 1) + CHOL_NB);
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(CHOL_NB), dim3(1024), lds, st, (const double *)A, lda, nb,
+                     (const int *)info, Y, YT);
+  return hipGetLastError();
+}
+
+// One block step of the substitution sweeps of chol_solve, for the factor L (column-major,
+// ld n) and the block's inverse M (Y for the forward sweep, Y^T for the backward one;
+// nb x nb, ld CHOL_NB): x = M src[j0 : j0+jb] (every workgroup, from L2), workgroup 0 stores
+// x at dst[j0 : j0+jb], and each workgroup subtracts the block's contribution from 128 rows
+// of src: forward  src[r] -= sum_c L[r, j0+c] x_c for r >= j0 + jb (lanes down a column,
+// coalesced; eight thread groups split c); backward src[r] -= sum_c L[j0+c, r] x_c for
+// r < j0 (8 lanes a row, 16 contiguous c each).  Every load of a phase is issued before its
+// first use: the kernel is latency-bound (~9 MB of L at n = 9000).  src[j0 : j0+jb] is only
+// read here and dst is another vector: no workgroup waits on another.
+__global__ __launch_bounds__(1024) void tri_sweep_kernel(const double *__restrict__ L, int64_t n,
+                                                         const double *__restrict__ M, int64_t j0, int jb,
+                                                         int back, double *__restrict__ src,
+                                                         double *__restrict__ dst) {
+  __shared__ double bs[CHOL_NB], xs[CHOL_NB], ps[8][CHOL_NB];
+  const int tid = threadIdx.x;
+  // this workgroup's share of L first: it does not depend on x, so its latency overlaps
+  // the x = M b phase.  Forward: thread (row rl, octant cq) holds L[r, j0 + 16 cq ..];
+  // backward: 8 lanes a row, lane (lane & 7) holds L[j0 + 16 (lane & 7) .., r].
+  double v[16];
+  const int rl = tid & (CHOL_SWEEP_ROWS - 1), cq = tid / CHOL_SWEEP_ROWS;
+  const int lane = tid & 63, seg = (lane & 7) * 16;
+  const int64_t rf = j0 + jb + (int64_t)blockIdx.x * CHOL_SWEEP_ROWS + rl;
+  const int64_t rb = (int64_t)blockIdx.x * CHOL_SWEEP_ROWS + (tid >> 3);
+  if (!back) {
+    const double *col = L + min(rf, n - 1) + j0 * n;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = col[(int64_t)min(cq * 16 + u, jb - 1) * n];
+  } else {
+    const double *row = L + j0 + (j0 > 0 ? min(rb, j0 - 1) : 0) * n;  // L[j0 + c, r]
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = row[min(seg + u, jb - 1)];
+  }
+  if (tid < CHOL_NB) bs[tid] = tid < jb ? src[j0 + tid] : 0.0;
+  __syncthreads();
+  {
+    const int i = tid & (CHOL_NB - 1), q = tid >> 7;
+    double m[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) m[u] = M[i + (q * 16 + u) * CHOL_NB];  // zero past jb
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += m[u] * bs[q * 16 + u];
+    ps[q][i] = acc;
+  }
+  __syncthreads();
+  if (tid < CHOL_NB) {
+    double x = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x += ps[q][tid];
+    xs[tid] = x;  // zero past jb (M is)
+    if (blockIdx.x == 0 && tid < jb) dst[j0 + tid] = x;
+  }
+  __syncthreads();
+  if (!back) {
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += v[u] * xs[cq * 16 + u];  // xs[c >= jb] = 0
+    ps[cq][rl] = acc;  // (ps reused: every read of it is behind the barrier above)
+    __syncthreads();
+    if (tid < CHOL_SWEEP_ROWS && rf < n) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += ps[q][tid];
+      src[rf] -= t;
+    }
+  } else {
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += v[u] * xs[seg + u];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (rb < j0 && (lane & 7) == 0) src[rb] -= acc;
+  }
+}
+
+hipError_t launch_tri_sweep(const double *L, int64_t n, const double *M, int64_t j0, int jb, int back,
+                            double *src, double *dst, hipStream_t st) {
+  if (jb <= 0 || jb > CHOL_NB || j0 < 0 || j0 + jb > n) return hipErrorInvalidValue;
+  const int64_t rows = back ? j0 : n - j0 - jb;
+  const int64_t g = std::max<int64_t>(1, (rows + CHOL_SWEEP_ROWS - 1) / CHOL_SWEEP_ROWS);
+  hipLaunchKernelGGL(tri_sweep_kernel, dim3((unsigned)g), dim3(1024), 0, st, L, n, M, j0, jb, back, src, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_asymmetry(const double *K, int64_t ld, int64_t n, int *flag, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t nt = (n + 31) / 32;

@@ -199,3 +199,43 @@ def test_factorisation_branches_reported(ctx):
     B = rng.standard_normal((n, n))
     ctx.krr_solve((B + B.T) / 2, y, 0.0)
     assert ctx.last_factorisation() == "lu_indefinite"
+
+
+@pytest.mark.parametrize("chol", ["1", "0"])
+@pytest.mark.parametrize("n", [127, 128, 129, 256, 385])
+def test_krr_block_edges_both_factorisations(ctx, tune, chol, n):
+    """The blocked Cholesky (KMG_CHOL=1: LDS diagonal blocks of 128, inverse-block GEMM
+    panels, one-launch-a-block substitution sweeps) and rocSOLVER potrf/potrs (KMG_CHOL=0)
+    at sizes on and around the 128-column block edges."""
+    tune(KMG_CHOL=chol)
+    K = _psd(n, max(1, n // 3), 7 * n)
+    y = np.where(np.random.default_rng(n + 3).random(n) > 0.5, 1.0, -1.0)
+    got = ctx.krr_solve(K, y, 0.02)
+    assert ctx.last_factorisation() == "cholesky"
+    np.testing.assert_allclose(got, cpu_ref.krr_alpha(K, y, 0.02), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("chol", ["1", "0"])
+def test_indefinite_pivot_in_later_block_falls_back(ctx, tune, chol):
+    """A pivot that fails in the third diagonal block (column ~300) of the blocked path:
+    every later block returns at once, the system is rebuilt and LU agrees with inv()."""
+    tune(KMG_CHOL=chol)
+    n = 400
+    K = _psd(n, n, 5)
+    K[300, 300] = -5.0  # symmetric, not positive definite
+    y = np.random.default_rng(6).standard_normal(n)
+    got = ctx.krr_solve(K, y, 0.0)
+    assert ctx.last_factorisation() == "lu_indefinite"
+    np.testing.assert_allclose(got, cpu_ref.krr_alpha(K, y, 0.0), rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.parametrize("chol", ["1", "0"])
+def test_svm_both_factorisations(ctx, tune, chol):
+    tune(KMG_CHOL=chol)
+    n, C = 700, 1.0
+    K = _psd(n, n // 4, 99)
+    y = np.where(np.random.default_rng(98).random(n) > 0.5, 1.0, -1.0)
+    a, steps, obj = ctx.svm_fit(K, y, C)
+    ra, rsteps, robj = cpu_ref.svm_dual(K, y, C)
+    assert obj == pytest.approx(robj, rel=1e-9, abs=1e-12)
+    np.testing.assert_allclose(a, ra, atol=1e-5 * C, rtol=0)
