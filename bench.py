@@ -695,7 +695,7 @@ def downstream(ctx, asym=True):
                 "ms": ms, "alg_flops": fl, "achieved_TFLOPs": fl / (ms / 1e3) / 1e12,
                 "fp64_frac": fl / (ms / 1e3) / FP64_PEAK, "source": "KRR.py:33",
                 "factorisation": ctx.last_factorisation(),
-                "note": "symmetry check + Cholesky (rocSOLVER dpotrf) + dpotrs of K + lbda n I"}
+                "note": "symmetry check + blocked Cholesky (kmg_solve.hip, rocBLAS GEMM / syrk updates) + substitution sweeps of K + lbda n I"}
         # the same solve on the ulp-asymmetric K / d_i / d_j: LU (rocSOLVER dgetrf, launch-bound
         # per column), what any user-normalised K not symmetrised costs (asym=False: skipped,
         # tools/trace_downstream.py's trace of the symmetric legs)

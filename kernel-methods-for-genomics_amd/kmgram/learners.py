@@ -5,7 +5,7 @@ Mirrors of the reference's KRR (KRR.py:4-66), KLR (KLR.py:4-110) and C_SVM
 ``score(pred, y)`` contract on pandas frames with ``Id`` and ``Bound`` columns, same fitted
 attributes.  The n x n system that the reference inverts with ``np.linalg.inv`` (KRR.py:33,
 KLR.py:53-54) is factorised on the MI355X by libkmgram (``kmg_krr_solve`` /
-``kmg_klr_fit``: rocSOLVER Cholesky with an LU fallback), and C_SVM's cvxopt QP
+``kmg_klr_fit``: the in-tree blocked Cholesky, rocSOLVER LU as the fallback), and C_SVM's cvxopt QP
 (SVM.py:78-89; cvxopt is not installed here) is solved by a device interior-point method
 (``kmg_svm_fit``).  The O(n_sv^2) bookkeeping around the solve (support-vector selection,
 intercept, decision values) stays on the host as vectorised numpy.  No CPU fallback for

@@ -1,5 +1,6 @@
-"""GPU parity of the dense learners on K (kmg_krr_solve / kmg_klr_fit: rocSOLVER Cholesky,
-LU fallback, HIP IRLS kernels in csrc/kmg_solve.hip) through the drop-in KRR.py / KLR.py.
+"""GPU parity of the dense learners on K (kmg_krr_solve / kmg_klr_fit: the blocked Cholesky
+of csrc/kmg_solve.hip -- or rocSOLVER potrf with KMG_CHOL=0 --, rocSOLVER LU fallback, HIP IRLS
+kernels) through the drop-in KRR.py / KLR.py.
 
 Pinned by golden vectors from the unmodified reference KRR.py / KLR.py
 (tests/golden/make_learner_golden.py).  The reference inverts with np.linalg.inv; the device
