@@ -241,6 +241,8 @@ struct kmg_ctx {
   hipStream_t unpack_stream = nullptr;          // upper triangle over RCCL: unpack of round t
   hipEvent_t ev_gath[2] = {nullptr, nullptr};   // overlaps the all-gather of round t + 1
   int last_wire_bytes = 0;                      // slab element bytes of the last blocks call
+  hipStream_t chol_stream = nullptr;            // blocked Cholesky: next diagonal block, ahead
+  hipEvent_t ev_chol[2] = {nullptr, nullptr};   // [0] its panel updated, [1] its factor done
   int nranks = 1, rank = 0;
 };
 
@@ -1475,6 +1477,9 @@ int kmg_destroy(kmg_ctx *c) {
   for (hipEvent_t e : c->ev_tri)
     if (e) (void)hipEventDestroy(e);
   if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
+  if (c->chol_stream) (void)hipStreamDestroy(c->chol_stream);
+  for (hipEvent_t e : c->ev_chol)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_slab)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_out)
@@ -2337,36 +2342,61 @@ static int is_asymmetric(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, b
 }
 
 // Right-looking blocked Cholesky of the symmetric n x n B (column-major lower, ld n) in
-// place, 128-column blocks: the diagonal block and its inverse Y in one workgroup
-// (launch_chol_diag), the panel below it as one GEMM (L21 = A21 Y^T, into sv_panel, copied
-// back), the trailing triangle by one rank-128 update (rocBLAS syrk, A22 -= L21 L21^T).
-// rocSOLVER's potrf issues ~22 kernels a block at n = 9000 (trtri, copies, recursive GEMMs;
-// profiles/r05ba_*).  The inverses (Y and Y^T of every block) stay in sv_inv for chol_solve.
-// *info (device) ends 0 or the 1-based column of the first non-positive pivot; nothing is
-// read back here.
+// place, 128-column blocks: the diagonal block and its inverse Y (launch_chol_diag: one
+// workgroup, then 128 one-column workgroups), the panel below it as one GEMM (L21 = A21 Y^T,
+// into sv_panel, copied back), the trailing triangle by rank-128 updates.  Look-ahead: the
+// next block column is updated first (one GEMM), the next diagonal block is factorised on a
+// second stream while the rest of the trailing triangle takes its dsyrk here, so the
+// latency-bound diagonal work hides behind the MFMA-bound update.  rocSOLVER's potrf issues
+// ~22 kernels a block at n = 9000 (trtri, copies, recursive GEMMs; profiles/r05ba_*).
+// The inverses (Y and Y^T of every block) stay in sv_inv for chol_solve.  *info (device)
+// ends 0 or the 1-based column of the first non-positive pivot; nothing is read back here.
 static constexpr int CHOL_BLK = 128;
 static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
   const int64_t nblk = (n + CHOL_BLK - 1) / CHOL_BLK;
   KMG_TRY(c->sv_inv.ensure(sizeof(double) * 2 * CHOL_BLK * CHOL_BLK * (size_t)nblk));
   KMG_TRY(c->sv_panel.ensure(sizeof(double) * CHOL_BLK * (size_t)n));
+  if (!c->chol_stream) KMG_HIP(hipStreamCreateWithFlags(&c->chol_stream, hipStreamNonBlocking));
+  for (hipEvent_t &e : c->ev_chol)
+    if (!e) KMG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   double *inv = c->sv_inv.as<double>(), *T = c->sv_panel.as<double>();
   const double one = 1.0, mone = -1.0, zero = 0.0;
+  const rocblas_int ld = (rocblas_int)n;
+  auto diag = [&](int64_t b, hipStream_t st) -> int {
+    const int64_t j0 = b * CHOL_BLK;
+    const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
+    double *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
+    KMG_HIP(launch_chol_diag(B + j0 + j0 * n, n, jb, (int)j0, (int *)info, Y, Y + CHOL_BLK * CHOL_BLK, st));
+    return KMG_OK;
+  };
   KMG_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), c->stream));
+  KMG_TRY(diag(0, c->stream));
   for (int64_t b = 0; b < nblk; ++b) {
     const int64_t j0 = b * CHOL_BLK;
     const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
-    double *Ajj = B + j0 + j0 * n, *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
-    KMG_HIP(launch_chol_diag(Ajj, n, jb, (int)j0, (int *)info, Y, Y + CHOL_BLK * CHOL_BLK, c->stream));
     const rocblas_int m = (rocblas_int)(n - j0 - jb);
     if (m == 0) break;
-    double *A21 = Ajj + jb;
+    if (b > 0) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // block b factorised
+    double *Ajj = B + j0 + j0 * n, *A21 = Ajj + jb, *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
     KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb, jb, &one,
-                           A21, (rocblas_int)n, Y, CHOL_BLK, &zero, T, m));
-    KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, m, jb, &mone, T, m, &one,
-                           A21 + (size_t)jb * n, (rocblas_int)n));
+                           A21, ld, Y, CHOL_BLK, &zero, T, m));
     KMG_HIP(hipMemcpy2DAsync(A21, sizeof(double) * n, T, sizeof(double) * m, sizeof(double) * m, jb,
                              hipMemcpyDeviceToDevice, c->stream));
+    // the next block column (its m x jb2 panel, the diagonal block's upper part included:
+    // never read), then its diagonal block on the side stream
+    const rocblas_int jb2 = std::min<rocblas_int>(CHOL_BLK, m);
+    double *A22 = A21 + (size_t)jb * n;
+    KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb2, jb, &mone,
+                           T, m, T, m, &one, A22, ld));
+    KMG_HIP(hipEventRecord(c->ev_chol[0], c->stream));
+    KMG_HIP(hipStreamWaitEvent(c->chol_stream, c->ev_chol[0], 0));
+    KMG_TRY(diag(b + 1, c->chol_stream));
+    KMG_HIP(hipEventRecord(c->ev_chol[1], c->chol_stream));
+    if (m > jb2)  // the rest of the trailing triangle
+      KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, m - jb2, jb, &mone, T + jb2,
+                             m, &one, A22 + jb2 + (size_t)jb2 * n, ld));
   }
+  if (nblk > 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // the last block
   return KMG_OK;
 }
 
