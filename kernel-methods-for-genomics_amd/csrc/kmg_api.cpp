@@ -140,6 +140,9 @@ struct Tuning {
   int poison = 0;           // KMG_POISON: fill the output with 0xA5 first (testing)
   int potrf_upper = 0;      // KMG_POTRF_UPPER: rocSOLVER upper-triangle Cholesky (implies KMG_CHOL=0)
   int chol = 1;             // KMG_CHOL: 1 blocked Cholesky + solves (chol_factor), 0 rocSOLVER potrf/potrs
+  int chol_panels = 4;      // KMG_CHOL_PANELS: trailing update as this many GEMM column panels (0:
+                            // one dsyrk).  KRR n=9000 19.3-19.5 -> 18.3 ms at 4 (2: 19.0, 3: 18.4,
+                            // 6: 18.4, 8: 18.5; profiles/r05bo_chol_panels.json)
   int sp_store = 0;         // KMG_SP_STORE: spectrum K stores, 0 auto, 1 non-temporal, 2 plain
   int sp_order = 1;         // KMG_SP_ORDER: spectrum grid, 0 row-major, 1 chunk-major (N=100000:
                             // Gram 6.66 -> 5.85 ms, interleaved A/B profiles/r02aq_sp_order_ab.jsonl)
@@ -170,6 +173,7 @@ void read_tuning(Tuning &t) {
   t.poison = env_or("KMG_POISON", d.poison);
   t.potrf_upper = env_or("KMG_POTRF_UPPER", d.potrf_upper);
   t.chol = env_or("KMG_CHOL", d.chol);
+  t.chol_panels = env_or("KMG_CHOL_PANELS", d.chol_panels);
   t.mm_form = env_or("KMG_MM_FORM", d.mm_form);
   t.esc_cap = env_or("KMG_ESC_CAP", d.esc_cap);
   t.mm_tri = env_or("KMG_MM_TRI", d.mm_tri);
@@ -2344,7 +2348,8 @@ static int is_asymmetric(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, b
 // Right-looking blocked Cholesky of the symmetric n x n B (column-major lower, ld n) in
 // place, 128-column blocks: the diagonal block and its inverse Y (launch_chol_diag: one
 // workgroup, then 128 one-column workgroups), the panel below it as one GEMM (L21 = A21 Y^T,
-// into sv_panel, copied back), the trailing triangle by rank-128 updates.  Look-ahead: the
+// into sv_panel, copied back), the trailing triangle by rank-128 updates (a few GEMMs over
+// its lower trapezoid: rocBLAS dsyrk recurses into many small ones).  Look-ahead: the
 // next block column is updated first (one GEMM), the next diagonal block is factorised on a
 // second stream while the rest of the trailing triangle takes its dsyrk here, so the
 // latency-bound diagonal work hides behind the MFMA-bound update.  rocSOLVER's potrf issues
@@ -2392,9 +2397,22 @@ static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
     KMG_HIP(hipStreamWaitEvent(c->chol_stream, c->ev_chol[0], 0));
     KMG_TRY(diag(b + 1, c->chol_stream));
     KMG_HIP(hipEventRecord(c->ev_chol[1], c->chol_stream));
-    if (m > jb2)  // the rest of the trailing triangle
-      KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, m - jb2, jb, &mone, T + jb2,
-                             m, &one, A22 + jb2 + (size_t)jb2 * n, ld));
+    if (m > jb2) {  // the rest of the trailing triangle
+      const rocblas_int mr = m - jb2;
+      double *Ar = A22 + jb2 + (size_t)jb2 * n;
+      const int np = c->tune.chol_panels;
+      if (np <= 0 || mr < 1024) {
+        KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, mr, jb, &mone, T + jb2, m,
+                               &one, Ar, ld));
+      } else {  // lower trapezoid as np column panels, one GEMM each (square tops: upper never read)
+        const rocblas_int w = (mr + np - 1) / np;
+        for (rocblas_int p0 = 0; p0 < mr; p0 += w) {
+          const rocblas_int pw = std::min(w, mr - p0);
+          KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, mr - p0, pw, jb,
+                                 &mone, T + jb2 + p0, m, T + jb2 + p0, m, &one, Ar + p0 + (size_t)p0 * n, ld));
+        }
+      }
+    }
   }
   if (nblk > 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // the last block
   return KMG_OK;
