@@ -226,8 +226,9 @@ int kmg_alignf_device(kmg_ctx *ctx, const double *const *d_K, int32_t p, const d
 
 /*
  * Dense learners on a Gram matrix.  K: n x n float64, row stride ld.
- * The system is factorised on the device (rocSOLVER Cholesky, LU with partial pivoting if
- * it is not positive definite); KMG_ESINGULAR where np.linalg.inv raises LinAlgError.
+ * The system is factorised on the device (blocked Cholesky of kmg_solve.hip -- rocSOLVER
+ * potrf with KMG_CHOL=0 --, rocSOLVER LU with partial pivoting if it is not positive
+ * definite); KMG_ESINGULAR where np.linalg.inv raises LinAlgError.
  */
 /* KRR.fit (KRR.py:33): alpha = inv(K + lambda * n * I) . y */
 int kmg_krr_solve(kmg_ctx *ctx, const double *K, int64_t ld, int64_t n, const double *y,
