@@ -2376,43 +2376,50 @@ static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
   };
   KMG_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), c->stream));
   KMG_TRY(diag(0, c->stream));
-  for (int64_t b = 0; b < nblk; ++b) {
-    const int64_t j0 = b * CHOL_BLK;
-    const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
-    const rocblas_int m = (rocblas_int)(n - j0 - jb);
-    if (m == 0) break;
-    if (b > 0) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // block b factorised
-    double *Ajj = B + j0 + j0 * n, *A21 = Ajj + jb, *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
-    KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb, jb, &one,
-                           A21, ld, Y, CHOL_BLK, &zero, T, m));
-    KMG_HIP(hipMemcpy2DAsync(A21, sizeof(double) * n, T, sizeof(double) * m, sizeof(double) * m, jb,
-                             hipMemcpyDeviceToDevice, c->stream));
-    // the next block column (its m x jb2 panel, the diagonal block's upper part included:
-    // never read), then its diagonal block on the side stream
-    const rocblas_int jb2 = std::min<rocblas_int>(CHOL_BLK, m);
-    double *A22 = A21 + (size_t)jb * n;
-    KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb2, jb, &mone,
-                           T, m, T, m, &one, A22, ld));
-    KMG_HIP(hipEventRecord(c->ev_chol[0], c->stream));
-    KMG_HIP(hipStreamWaitEvent(c->chol_stream, c->ev_chol[0], 0));
-    KMG_TRY(diag(b + 1, c->chol_stream));
-    KMG_HIP(hipEventRecord(c->ev_chol[1], c->chol_stream));
-    if (m > jb2) {  // the rest of the trailing triangle
-      const rocblas_int mr = m - jb2;
-      double *Ar = A22 + jb2 + (size_t)jb2 * n;
-      const int np = c->tune.chol_panels;
-      if (np <= 0 || mr < 1024) {
-        KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, mr, jb, &mone, T + jb2, m,
-                               &one, Ar, ld));
-      } else {  // lower trapezoid as np column panels, one GEMM each (square tops: upper never read)
-        const rocblas_int w = (mr + np - 1) / np;
-        for (rocblas_int p0 = 0; p0 < mr; p0 += w) {
-          const rocblas_int pw = std::min(w, mr - p0);
-          KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, mr - p0, pw, jb,
-                                 &mone, T + jb2 + p0, m, T + jb2 + p0, m, &one, Ar + p0 + (size_t)p0 * n, ld));
+  auto blocks = [&]() -> int {
+    for (int64_t b = 0; b < nblk; ++b) {
+      const int64_t j0 = b * CHOL_BLK;
+      const int jb = (int)std::min<int64_t>(CHOL_BLK, n - j0);
+      const rocblas_int m = (rocblas_int)(n - j0 - jb);
+      if (m == 0) break;
+      if (b > 0) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // block b factorised
+      double *Ajj = B + j0 + j0 * n, *A21 = Ajj + jb, *Y = inv + 2 * CHOL_BLK * CHOL_BLK * b;
+      KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb, jb, &one,
+                             A21, ld, Y, CHOL_BLK, &zero, T, m));
+      KMG_HIP(hipMemcpy2DAsync(A21, sizeof(double) * n, T, sizeof(double) * m, sizeof(double) * m, jb,
+                               hipMemcpyDeviceToDevice, c->stream));
+      // the next block column (its m x jb2 panel, the diagonal block's upper part included:
+      // never read), then its diagonal block on the side stream
+      const rocblas_int jb2 = std::min<rocblas_int>(CHOL_BLK, m);
+      double *A22 = A21 + (size_t)jb * n;
+      KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, m, jb2, jb, &mone,
+                             T, m, T, m, &one, A22, ld));
+      KMG_HIP(hipEventRecord(c->ev_chol[0], c->stream));
+      KMG_HIP(hipStreamWaitEvent(c->chol_stream, c->ev_chol[0], 0));
+      KMG_TRY(diag(b + 1, c->chol_stream));
+      KMG_HIP(hipEventRecord(c->ev_chol[1], c->chol_stream));
+      if (m > jb2) {  // the rest of the trailing triangle
+        const rocblas_int mr = m - jb2;
+        double *Ar = A22 + jb2 + (size_t)jb2 * n;
+        const int np = c->tune.chol_panels;
+        if (np <= 0 || mr < 1024) {
+          KMG_BLAS(rocblas_dsyrk(c->blas, rocblas_fill_lower, rocblas_operation_none, mr, jb, &mone, T + jb2, m,
+                                 &one, Ar, ld));
+        } else {  // lower trapezoid as np column panels, one GEMM each (square tops: upper never read)
+          const rocblas_int w = (mr + np - 1) / np;
+          for (rocblas_int p0 = 0; p0 < mr; p0 += w) {
+            const rocblas_int pw = std::min(w, mr - p0);
+            KMG_BLAS(rocblas_dgemm(c->blas, rocblas_operation_none, rocblas_operation_transpose, mr - p0, pw, jb,
+                                   &mone, T + jb2 + p0, m, T + jb2 + p0, m, &one, Ar + p0 + (size_t)p0 * n, ld));
+          }
         }
       }
     }
+    return KMG_OK;
+  };
+  if (const int rc = blocks()) {  // (an error mid-way: no side-stream work outlives the call)
+    (void)hipStreamSynchronize(c->chol_stream);
+    return rc;
   }
   if (nblk > 1) KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_chol[1], 0));  // the last block
   return KMG_OK;
