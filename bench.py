@@ -8,8 +8,11 @@ codes already in HBM when the timed region starts); posting-list formulation (DE
 on the configs[3] "count-vector GEMM" wording).  A "step" is one full-K build (SURVEY §8d t_build):
 2-bit packing + posting-index build + Gram kernel (G > 1: this GPU's rows of it).
 
-Multi-GPU (`python -m torch.distributed.run --nproc-per-node G bench.py --gpus G`): one
-process per GPU.  The rows of K are independent, so the headline shards them
+Multi-GPU: one process per GPU.  `python bench.py --gpus G` starts the G rank processes
+itself (launch_ranks: rank r on device r, rendezvous on 127.0.0.1, rank 0's JSON line
+relayed, non-zero exit if any rank fails); under `python -m torch.distributed.run
+--nproc-per-node G bench.py --gpus G` the launcher's environment is used as is, and a
+WORLD_SIZE different from --gpus is an error.  The rows of K are independent, so the headline shards them
 with no data-path collective and scales STRONGLY at the north-star's named N = 100000:
 every GPU builds the replicated index and computes its 1/G share of the rows x all N
 columns, packed in its own buffer; `value` = N^2 / max-over-ranks step time.  The
@@ -55,6 +58,79 @@ STAGES = ("count", "scan", "place", "fine", "pack", "lists", "nbfill", "slots", 
           "gram", "mirror", "gather")
 
 
+def rank_env(base, world, rank, port, addr="127.0.0.1"):
+    """The environment of rank `rank` of a `world`-rank job started by launch_ranks: the
+    variables torch.distributed.run sets (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT; one node, so the local rank is the rank and picks the GPU),
+    plus KMG_BENCH_LAUNCHED so a child never launches again."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+               LOCAL_WORLD_SIZE=str(world), GROUP_RANK="0", MASTER_ADDR=addr,
+               MASTER_PORT=str(port), KMG_BENCH_LAUNCHED="1")
+    return env
+
+
+def free_port(addr="127.0.0.1"):
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((addr, 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(world, argv, poll_s=0.5):
+    """`bench.py --gpus G` started without a launcher (WORLD_SIZE unset): start G rank
+    processes of this script (one per GPU, rank r on device r) and relay rank 0's JSON line.
+    Runs before this process loads libkmgram or makes any HIP call; the children are
+    started as new processes (never an exec of this one).  If a rank fails, the others are
+    terminated (their own PIDs) and the exit status is non-zero.  Returns the exit status."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT") or free_port())
+    addr = os.environ.get("MASTER_ADDR") or "127.0.0.1"
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen(cmd, env=rank_env(os.environ, world, r, port, addr),
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"launch_ranks: rank {r} exited with status {c}; stopping the others",
+                      file=sys.stderr)
+                status = c if c > 0 else 128 - c
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out = procs[0].stdout.read().decode(errors="replace")
+    procs[0].stdout.close()
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    if status == 0:
+        if not lines:
+            print("launch_ranks: rank 0 printed no JSON line", file=sys.stderr)
+            return 1
+        rec = json.loads(lines[-1])
+        if rec.get("n_gpus") != world:
+            print(f"launch_ranks: rank 0 reports n_gpus={rec.get('n_gpus')}, not {world}",
+                  file=sys.stderr)
+            return 1
+        print(lines[-1], flush=True)
+    return status
+
+
 class Dist:
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,6 +156,14 @@ class Dist:
 
     def all_true(self, v):
         return self.max(0.0 if v else 1.0) == 0.0
+
+    def gather(self, v):
+        """[v of rank 0, v of rank 1, ...] on every rank."""
+        if self.world == 1:
+            return [v]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, v)
+        return out
 
     def bcast_bytes(self, b):
         if self.world == 1:
@@ -963,6 +1047,16 @@ def main():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the config 4 / 5, host-path, run.py and downstream lines")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    # `--gpus G` alone (no launcher environment): this process starts the G ranks itself,
+    # before anything here touches the GPU, and relays rank 0's line
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world} (launched with a different "
+                 "number of ranks)")
     global GATHER_MODE
     GATHER_MODE = args.gather_mode
     # stdout carries exactly one JSON line: everything else written to fd 1 (gloo's
@@ -972,8 +1066,27 @@ def main():
     os.dup2(2, 1)
 
     dist = Dist()
-    if dist.world != args.gpus and dist.rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
+    if os.environ.get("KMG_BENCH_DRYRUN") == "1":
+        # launcher plumbing only (tests/test_distributed_cpu.py): the rank layout of the
+        # headline and one barrier / max-over-ranks round, no library, no GPU
+        # (KMG_BENCH_FAIL_RANK=r: rank r exits with status 3, the launcher's failure path)
+        if os.environ.get("KMG_BENCH_FAIL_RANK") == str(dist.rank):
+            sys.exit(3)
+        n = args.n
+        rows = sum(b - a for a, b in block_cyclic_ranges(n, dist.world, dist.rank,
+                                                          (-(-n // dist.world) + 7) // 8 * 8))
+        dist.barrier()
+        slowest = dist.max(float(dist.rank))
+        per_rank = dist.gather(rows)
+        if dist.rank == 0:
+            print(json.dumps({"metric": METRIC, "dryrun": True, "n_gpus": dist.world,
+                              "rank": dist.rank, "rows_this_rank": rows,
+                              "rows_per_rank": per_rank, "max_over_ranks": slowest,
+                              "local_rank": dist.local,
+                              "launched": os.environ.get("KMG_BENCH_LAUNCHED") == "1"}),
+                  file=json_out, flush=True)
+        dist.close()
+        return
     n1 = args.n
     sp_seed = 4 if n1 == 100000 else 2
     # the CPU baseline runs FIRST, before this process makes any HIP call: its workers are
@@ -999,6 +1112,8 @@ def main():
     n = n1
     sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
                    sp_seed, args.steps, args.warmup, check_spectrum, gather=0)
+    sp["rows_per_rank"] = dist.gather(sp["rows_this_rank"])
+    sp["devices_per_rank"] = dist.gather(ctx.device)
     asm = None
     if rccl:
         asm = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n1,
@@ -1066,6 +1181,9 @@ def main():
                                "measured as `assembled`)" % n,
                    "N": n, "L": 101, "k": 8,
                    "rows_this_rank": sp["rows_this_rank"],
+                   "rows_per_rank": sp["rows_per_rank"],
+                   "devices_per_rank": sp["devices_per_rank"],
+                   "rccl": rccl,
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
         "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],

@@ -321,3 +321,64 @@ def test_gloo_world2_column_blocks(tmp_path):
     import json
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert d["equal"] and d["cover"] == [[0, 101], [101, 203]]
+
+
+def test_bench_rank_env_plumbing():
+    """bench.launch_ranks' per-rank environment: the variables torch.distributed.run sets
+    (one node: LOCAL_RANK = RANK picks the GPU), a shared rendezvous, the marker that stops
+    a child from launching again, and the caller's other variables passed through."""
+    import bench
+    base = {"KMG_BENCH_NO_RCCL": "1", "PATH": "/x"}
+    envs = [bench.rank_env(base, 3, r, 29512) for r in range(3)]
+    for r, e in enumerate(envs):
+        assert e["RANK"] == e["LOCAL_RANK"] == str(r)
+        assert e["WORLD_SIZE"] == e["LOCAL_WORLD_SIZE"] == "3"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29512"
+        assert e["KMG_BENCH_LAUNCHED"] == "1"
+        assert e["KMG_BENCH_NO_RCCL"] == "1" and e["PATH"] == "/x"
+    assert "RANK" not in base  # the parent's environment is not modified
+
+
+def _bench(args, env_extra, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_gpus_flag_starts_ranks(world):
+    """`python bench.py --gpus G` with no launcher environment starts G rank processes itself
+    (gloo rendezvous on 127.0.0.1), and rank 0's line reports n_gpus = G with every rank's
+    share of the headline rows (KMG_BENCH_DRYRUN: the plumbing only, no library / GPU)."""
+    pytest.importorskip("torch")
+    out = _bench(["--gpus", str(world), "--n", "100000"], {"KMG_BENCH_DRYRUN": "1"})
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1  # exactly one JSON line on stdout
+    import json
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["launched"] and d["rank"] == 0
+    assert d["max_over_ranks"] == world - 1
+    assert sum(d["rows_per_rank"]) == 100000 and len(d["rows_per_rank"]) == world
+    assert max(d["rows_per_rank"]) - min(d["rows_per_rank"]) <= 8
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    """A launcher environment whose WORLD_SIZE disagrees with --gpus is refused (it used to
+    be a warning, which let a G-GPU request run on fewer ranks)."""
+    out = _bench(["--gpus", "4"], {"KMG_BENCH_DRYRUN": "1", "WORLD_SIZE": "1", "RANK": "0"})
+    assert out.returncode != 0
+    assert "WORLD_SIZE=1" in out.stderr
+
+
+def test_bench_failing_rank_fails_the_launch():
+    """A rank that dies makes the launcher stop the others and exit non-zero, with no JSON
+    line on stdout."""
+    pytest.importorskip("torch")
+    out = _bench(["--gpus", "2", "--n", "100000"],
+                 {"KMG_BENCH_DRYRUN": "1", "KMG_BENCH_FAIL_RANK": "1"})
+    assert out.returncode != 0
+    assert not out.stdout.strip()
+    assert "rank 1 exited" in out.stderr
