@@ -41,7 +41,9 @@ enum {
   KMG_ENOMEM = 4,       /* device allocation failed */
   KMG_ERCCL = 5,        /* RCCL error */
   KMG_ENODEV = 6,       /* no HIP device visible */
-  KMG_ESINGULAR = 7     /* dense learner: the system matrix is singular (LinAlgError) */
+  KMG_ESINGULAR = 7,    /* dense learner: the system matrix is singular (LinAlgError) */
+  KMG_EINTERNAL = 8     /* an internal consistency check failed (KMG_CHECK=1: the neighbourhood
+                           lists' metadata after a fill); nothing past the check was launched */
 };
 
 /* kernel families (one per reference get_*_K) */
@@ -274,8 +276,13 @@ int kmg_svm_fit_device(kmg_ctx *ctx, const double *d_K, int64_t ld, int64_t n,
  * one-GPU rehearsal of the multi-rank assembly; no RCCL).  gather = 4: like 0 (no data-path
  * collective) with this rank's blocks packed: row t*block + y of d_out holds row
  * t*R + rank*block + y of K (d_out needs ceil(n / R) * block rows: a rank's share of a K
- * that no single GPU could hold).  gather = 1 or 2 with nranks > 1
- * needs kmg_comm_init with the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
+ * that no single GPU could hold).  gather = 5 (column blocks, mismatch (k, 1) with 4 <= k <= 12
+ * only, KMG_EUNSUPPORTED otherwise): one round, nranks * block >= n; rank r computes the column
+ * block K[:, C_r], C_r = [r*block, min(n, (r+1)*block)), with the neighbourhood lists built over
+ * its own |C_r| sequences (kmg_gram_device_cols), transposes it into K's rows C_r (K is
+ * symmetric) and the slabs are all-gathered in place over RCCL; d_out holds nranks * block rows.
+ * gather = 6: the gather = 5 layout with every rank's block computed on this GPU (no RCCL).
+ * gather = 1, 2 or 5 with nranks > 1 needs kmg_comm_init with the same nranks / rank.  Replaces the whole-matrix pair loops of get_spectrum_K /
  * get_mismatch_K (kernels.py:41-45, 211-215) split over GPUs.
  */
 int64_t kmg_rows_padded(int64_t n, int32_t nranks, int64_t block);

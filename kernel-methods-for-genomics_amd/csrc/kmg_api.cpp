@@ -153,6 +153,10 @@ struct Tuning {
   int dense_half = -1;      // KMG_DENSE_HALF: dense Gram tiles over two 4-wave workgroups (BK
                             // 64), -1: when dp <= 1024 (SP k=5 N=20000 0.41 -> 0.39 ms; at
                             // dp >= 4096 BK 128 wins; profiles/r02bj_dense_epilogue_ab.jsonl)
+  int check = 0;            // KMG_CHECK: 1 validate the neighbourhood lists' metadata after
+                            // every fill (nb_check_kernel; one host sync a build) and fail with
+                            // KMG_EINTERNAL before any Gram launch reads past a list; 2 the
+                            // same after overwriting every list's piece counts (tests only)
 };
 
 int env_or(const char *name, int dflt) {
@@ -191,6 +195,7 @@ void read_tuning(Tuning &t) {
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   t.dense_half = env_or("KMG_DENSE_HALF", d.dense_half);
+  t.check = env_or("KMG_CHECK", d.check);
   if (getenv("KMG_MM_CHUNK") == nullptr) t.mm_chunk = 0;  // 0: per-formulation default
 }
 
@@ -218,6 +223,8 @@ struct kmg_ctx {
   int32_t last_factor = 0;        // last KRR / KLR solve's factorisation (kmg_last_factorisation)
   DevBuf pr_summary, pr_rtot, pr_rbase, pr_cursor, pr_lines;  // pair (drop-two) table
   DevBuf nb_seg, nb_use, nb_lines;  // neighbourhood lists: segment ends, pieces in use, lists
+  DevBuf chk;                       // KMG_CHECK: validation flag + first offending list
+  DevBuf cb_scratch;                // column-block assembly: one rank's K[:, C_q] (n x block)
   Tuning tune;
   DevBuf cmb_k, cmb_ptrs, cmb_vec, cmb_out, cmb_tmp;  // combination consumers (host path)
   DevBuf sv_mat, sv_vec, sv_info;  // dense learners: factorised system, vectors, info/ipiv
@@ -248,6 +255,7 @@ struct kmg_ctx {
   hipStream_t chol_stream = nullptr;            // blocked Cholesky: next diagonal block, ahead
   hipEvent_t ev_chol[2] = {nullptr, nullptr};   // [0] its panel updated, [1] its factor done
   int nranks = 1, rank = 0;
+  int lds_max = 0;  // LDS bytes a workgroup may allocate on the device (kmg_create)
 };
 
 namespace {
@@ -1178,6 +1186,27 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
             return fail(KMG_EUNSUPPORTED, "KMG_NB_FILL=1: no sorted fill at k=%d, chunk %d", k, g.chunk);
           KMG_HIP(e);
         }
+        if (c->tune.check) {
+          // the Gram kernel reads table[start + rel] for rel below the list's nbuse counts
+          // without a bound: a fill that left them inconsistent is reported here, before any
+          // read past a list (round 5's r05ah fault)
+          KMG_TRY(c->chk.ensure(2 * sizeof(uint32_t)));
+          if (c->tune.check == 2)  // test hook: a fill that left every list's counts stale
+            KMG_HIP(hipMemsetD32Async((hipDeviceptr_t)c->nb_use.p, 0x7FFFFFFFu, 2 * (size_t)nbins,
+                                      c->stream));
+          KMG_HIP(hipMemsetD32Async((hipDeviceptr_t)c->chk.p, 0u, 1, c->stream));
+          KMG_HIP(hipMemsetD32Async((hipDeviceptr_t)(c->chk.as<uint32_t>() + 1), 0xFFFFFFFFu, 1, c->stream));
+          KMG_HIP(launch_nb_check(nbins, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
+                                  c->nb_use.as<uint2>(), (uint64_t)(bound + 8) / 8,
+                                  c->chk.as<uint32_t>(), c->stream));
+          uint32_t res[2] = {0u, 0u};
+          KMG_HIP(hipMemcpyAsync(res, c->chk.p, sizeof(res), hipMemcpyDeviceToHost, c->stream));
+          KMG_HIP(hipStreamSynchronize(c->stream));
+          if (res[0])
+            return fail(KMG_EINTERNAL, "KMG_CHECK: neighbourhood list %u (chunk %u, k-mer %u) has "
+                        "inconsistent metadata after the fill (KMG_NB_FILL=%d)", res[1],
+                        res[1] >> (2 * k), res[1] & (uint32_t)(pow4(k) - 1), c->tune.nb_fill);
+        }
         if (p->normalize || dt == KMG_U8) {  // (8-bit slabs: the unpack's K_ii)
           KMG_TRY(upload_wtab(c, w));
           KMG_TRY(diag_hamming(c, g, pkd));
@@ -1447,6 +1476,13 @@ int kmg_create(kmg_ctx **out, int device_id) {
   kmg_ctx *c = new kmg_ctx();
   c->device = device_id;
   read_tuning(c->tune);
+  // LDS a workgroup may take: the largest of what the runtime reports per block, per block
+  // opt-in and per CU (runtimes differ in which one carries gfx950's 160 KB)
+  for (hipDeviceAttribute_t a : {hipDeviceAttributeMaxSharedMemoryPerBlock, hipDeviceAttributeSharedMemPerBlockOptin,
+                                 hipDeviceAttributeMaxSharedMemoryPerMultiprocessor}) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, a, device_id) == hipSuccess) c->lds_max = std::max(c->lds_max, v);
+  }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -1470,7 +1506,7 @@ int kmg_destroy(kmg_ctx *c) {
                     &c->cmb_out, &c->cmb_tmp, &c->sv_mat, &c->sv_vec, &c->sv_info, &c->sv_inv, &c->sv_panel,
                     &c->tri_stage, &c->tri_scratch, &c->dense_tiles, &c->ovf, &c->slabs,
                     &c->gcoef, &c->feat32, &c->k32, &c->ft_cols,
-                    &c->nb_seg, &c->nb_use, &c->nb_lines};
+                    &c->nb_seg, &c->nb_use, &c->nb_lines, &c->chk, &c->cb_scratch};
   for (DevBuf *b : bufs) b->release();
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -1726,12 +1762,78 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      int32_t gather, int narrow_bits);
 }  // namespace
 
+namespace {
+// Column blocks (gather 5 / 6): rank q computes the column block K[:, C_q], C_q = [q * block,
+// min(n, (q + 1) * block)), with the neighbourhood lists built over its own |C_q| sequences
+// (kmg_gram_device_cols: every list read by all n rows, so they pack), transposes it into
+// K's rows C_q (the row slab: K is symmetric), and the slabs are all-gathered in place over
+// RCCL (gather 5; one equal-count ncclAllGather, d_out holds nranks * block rows).  gather 6
+// computes every rank's block on this GPU (the one-GPU rehearsal, no RCCL).  The transposes
+// are timed as "unpack", the all-gather as "gather".
+int gram_colblocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
+                        const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype,
+                        void *d_out, int64_t ld_out, int32_t nranks, int32_t rank, int64_t block,
+                        int32_t gather) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
+  if (block < 1 || (int64_t)nranks * block < n)
+    return fail(KMG_EINVAL, "column blocks: nranks * block = %lld rows must cover n = %lld",
+                (long long)nranks * (long long)block, (long long)n);
+  if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
+  if (out_dtype != KMG_I32 && out_dtype != KMG_F32 && out_dtype != KMG_F64)
+    return fail(KMG_EINVAL, "bad output dtype %d", out_dtype);
+  const bool rccl = gather == 5 && (nranks > 1 || (c->comm && c->nranks == 1));
+  if (rccl && (!c->comm || c->nranks != nranks || c->rank != rank))
+    return fail(KMG_EINVAL, "gather needs a communicator of %d ranks with this rank %d", nranks, rank);
+  KMG_HIP(hipSetDevice(c->device));
+  const size_t esz = dtype_size(out_dtype);
+  c->last_wire_bytes = (int)esz;
+  if (n == 0) return KMG_OK;
+  KMG_TRY(c->cb_scratch.ensure((size_t)n * (size_t)block * esz));
+  for (int32_t q = 0; q < nranks; ++q) {
+    if (gather != 6 && q != rank) continue;
+    const int64_t c0 = std::min(n, (int64_t)q * block), c1 = std::min(n, c0 + block), w = c1 - c0;
+    if (w <= 0) continue;
+    KMG_TRY(gram_device(c, p, d_codes, d_lens, (int)ldc, n, ldc, {RowRange{0, n, c->cb_scratch.p}},
+                        out_dtype, w, nullptr, c0, w));
+    StageTimer t(c, ST_UNPACK);
+    KMG_HIP(launch_transpose(c->cb_scratch.p, w, n, w, (char *)d_out + (size_t)c0 * ld_out * esz,
+                             ld_out, (int)esz, c->stream));
+  }
+  if (rccl) {  // in place: rank q's slab at rows q * block (send = recv + rank * count)
+    if (!c->comm_stream) KMG_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!c->ev_sync) KMG_HIP(hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+    KMG_HIP(hipEventRecord(c->ev_sync, c->stream));
+    KMG_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_sync, 0));
+    const size_t count = (size_t)block * (size_t)ld_out * esz;
+    hipEvent_t b = nullptr, e = nullptr;
+    if (c->timing) {
+      b = pool_event(c);
+      e = pool_event(c);
+      KMG_HIP(hipEventRecord(b, c->comm_stream));
+    }
+    ncclResult_t r = ncclAllGather((char *)d_out + (size_t)rank * count, d_out, count, ncclChar, c->comm,
+                                   c->comm_stream);
+    if (r != ncclSuccess) return fail(KMG_ERCCL, "ncclAllGather (column blocks): %s", ncclGetErrorString(r));
+    if (c->timing) {
+      KMG_HIP(hipEventRecord(e, c->comm_stream));
+      c->ev_log.push_back({ST_GATHER, {b, e}});
+    }
+    KMG_HIP(hipEventRecord(c->ev_sync, c->comm_stream));
+    KMG_HIP(hipStreamWaitEvent(c->stream, c->ev_sync, 0));
+  }
+  return KMG_OK;
+}
+}  // namespace
+
 int kmg_gram_blocks(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                     const int32_t *d_lens, int64_t n, int64_t ldc, int32_t out_dtype, void *d_out,
                     int64_t ld_out, int32_t nranks, int32_t rank, int64_t block, int32_t gather) {
   if (!c) return fail(KMG_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(c->mu);
   KMG_TRY(check_params(p, n, ldc, out_dtype));
+  if (gather == 5 || gather == 6)
+    return gram_colblocks_impl(c, p, d_codes, d_lens, n, ldc, out_dtype, d_out, ld_out, nranks,
+                               rank, block, gather);
   // round slabs as narrow as the counts allow: 8 bits, else 16, else the output dtype
   int r = KMG_RETRY_WIDE;
   for (int bits : {8, 16, 0}) {
@@ -1786,7 +1888,7 @@ int gram_blocks_impl(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes,
                      int32_t gather, int narrow_bits) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KMG_EINVAL, "bad rank %d of %d", rank, nranks);
   if (block < 1) return fail(KMG_EINVAL, "block < 1");
-  if (gather < 0 || gather > 4) return fail(KMG_EINVAL, "gather must be 0..4");
+  if (gather < 0 || gather > 4) return fail(KMG_EINVAL, "gather must be 0..6");
   const bool packed = gather == 4;  // this rank's blocks, packed (no collective)
   if (packed) gather = 0;
   if (n > 0 && (!d_out || ld_out < n)) return fail(KMG_EINVAL, "bad output");
@@ -2357,6 +2459,14 @@ static int is_asymmetric(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, b
 // The inverses (Y and Y^T of every block) stay in sv_inv for chol_solve.  *info (device)
 // ends 0 or the 1-based column of the first non-positive pivot; nothing is read back here.
 static constexpr int CHOL_BLK = 128;
+
+// The in-tree factorisation (KMG_CHOL=1, not KMG_POTRF_UPPER) where the device has the LDS
+// its diagonal-block inverse takes (gfx950's 160 KB); else rocSOLVER potrf / potrs.  One
+// rule for KRR, KLR and the C-SVM.
+static bool use_own_chol(const kmg_ctx *c) {
+  return c->tune.chol && !c->tune.potrf_upper && (size_t)c->lds_max >= chol_diag_lds_bytes();
+}
+
 static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
   const int64_t nblk = (n + CHOL_BLK - 1) / CHOL_BLK;
   KMG_TRY(c->sv_inv.ensure(sizeof(double) * 2 * CHOL_BLK * CHOL_BLK * (size_t)nblk));
@@ -2376,6 +2486,11 @@ static int chol_factor(kmg_ctx *c, double *B, int64_t n, rocblas_int *info) {
   };
   KMG_HIP(hipMemsetAsync(info, 0, sizeof(rocblas_int), c->stream));
   KMG_TRY(diag(0, c->stream));
+  // Nothing is read back while the blocks are enqueued: after a non-positive pivot the later
+  // diagonal / inverse launches return at once, but every panel GEMM and trailing update still
+  // runs on stale inverses (their result is discarded: the caller rebuilds the system for LU).
+  // An indefinite system therefore pays about one full factorisation before the LU fallback
+  // (once per IRLS / interior-point step that meets one) -- the price of no host sync here.
   auto blocks = [&]() -> int {
     for (int64_t b = 0; b < nblk; ++b) {
       const int64_t j0 = b * CHOL_BLK;
@@ -2471,7 +2586,7 @@ static int solve_system(kmg_ctx *c, Build build, int64_t n, double *rhs, bool as
   }
   // B is symmetric: either triangle is the matrix (KMG_POTRF_UPPER selects rocSOLVER's
   // upper-triangle variant)
-  const bool own = c->tune.chol && !c->tune.potrf_upper;
+  const bool own = use_own_chol(c);
   const rocblas_fill fill = c->tune.potrf_upper ? rocblas_fill_upper : rocblas_fill_lower;
   if (own)
     KMG_TRY(chol_factor(c, B, n, info));
@@ -2598,7 +2713,7 @@ static int svm_run(kmg_ctx *c, const double *d_K, int64_t ld, int64_t n, const d
     if (gap <= tol * std::max(1.0, std::fabs(h[2])) && h[1] <= tol) break;
     // M = YKY + diag(D), factorised once, solved for the predictor and the corrector
     KMG_HIP(launch_shift_scale(d_K, ld, d_y, 0.0, D, n, B, n, c->stream));
-    const bool own = c->tune.chol != 0;
+    const bool own = use_own_chol(c);
     if (own)
       KMG_TRY(chol_factor(c, B, n, info));
     else

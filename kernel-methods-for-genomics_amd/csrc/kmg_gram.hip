@@ -1186,6 +1186,63 @@ hipError_t launch_mirror_chunks(void *K, int64_t ld, int64_t n, int chunk, int e
   return hipGetLastError();
 }
 
+// Column-block assembly (kmg_gram_blocks gather 5 / 6): a rank's column block K[:, C] (n
+// rows x w columns) is, K being symmetric, its row slab K[C, :] stored column-major; this
+// copies it into the slab's rows of K.  One 64 x 64 tile a workgroup: read along the block's
+// rows, written along K's rows, 16 bytes a lane each way (as mirror_chunks_kernel).
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T *__restrict__ M, int64_t ldm,
+                                                        int64_t rows, int64_t w,
+                                                        T *__restrict__ K, int64_t ldk) {
+  constexpr int V = 16 / (int)sizeof(T), CPR = 64 / V;
+  __shared__ T tile[64][64 + 1];  // [i - i0][j - j0]
+  const int64_t j0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+  for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
+    const int r = c / CPR, q = (c - r * CPR) * V;
+    const int64_t i = i0 + r, j = j0 + q;
+    if (i >= rows || j >= w) continue;
+    const T *src = M + i * ldm + j;
+    if (j + V <= w && (((uintptr_t)src) & 15) == 0) {
+      const uint4 x = *(const uint4 *)src;
+      const T *v = (const T *)&x;
+#pragma unroll
+      for (int h = 0; h < V; ++h) tile[r][q + h] = v[h];
+    } else {
+      for (int h = 0; h < V && j + h < w; ++h) tile[r][q + h] = src[h];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 64 * CPR; c += blockDim.x) {
+    const int r = c / CPR, q = (c - r * CPR) * V;
+    const int64_t j = j0 + r, i = i0 + q;  // K row j, columns i ..
+    if (j >= w || i >= rows) continue;
+    T o[V];
+#pragma unroll
+    for (int h = 0; h < V; ++h) o[h] = tile[q + h][r];
+    T *dst = K + j * ldk + i;
+    if (i + V <= rows && (((uintptr_t)dst) & 15) == 0) {
+      *(uint4 *)dst = *(const uint4 *)o;
+    } else {
+      for (int h = 0; h < V && i + h < rows; ++h) dst[h] = o[h];
+    }
+  }
+}
+
+hipError_t launch_transpose(const void *M, int64_t ldm, int64_t rows, int64_t w, void *K,
+                            int64_t ldk, int esz, hipStream_t s) {
+  if (rows <= 0 || w <= 0) return hipSuccess;
+  if (esz != 8 && esz != 4) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((w + 63) / 64), (unsigned)((rows + 63) / 64));
+  if ((rows + 63) / 64 > 65535 || (w + 63) / 64 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+  if (esz == 8)
+    hipLaunchKernelGGL(transpose_kernel<uint64_t>, grid, dim3(256), 0, s, (const uint64_t *)M, ldm,
+                       rows, w, (uint64_t *)K, ldk);
+  else
+    hipLaunchKernelGGL(transpose_kernel<uint32_t>, grid, dim3(256), 0, s, (const uint32_t *)M, ldm,
+                       rows, w, (uint32_t *)K, ldk);
+  return hipGetLastError();
+}
+
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
                                 hipStream_t s, int store, int order) {

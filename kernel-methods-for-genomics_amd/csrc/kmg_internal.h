@@ -209,6 +209,11 @@ hipError_t launch_tri_unpack(const void *S, int64_t w, int64_t R, int64_t c0, in
 // formula, bit for bit)
 hipError_t launch_mirror_chunks(void *K, int64_t ld, int64_t n, int chunk, int esz,
                                 hipStream_t s);
+// column-block assembly (kmg_gram_blocks gather 5 / 6): K[j][i] = M[i][j] for the column block
+// M (rows x w, row stride ldm) into w rows of K (row stride ldk), 64 x 64 LDS tiles, 16 bytes
+// a lane both ways (esz = 4 or 8 bytes)
+hipError_t launch_transpose(const void *M, int64_t ldm, int64_t rows, int64_t w, void *K,
+                            int64_t ldk, int esz, hipStream_t s);
 hipError_t launch_tri_unpack16(const uint16_t *S, int64_t w, int64_t R, int64_t c0, int64_t n,
                                void *K, int64_t ld, int dt, int normalize, const double *diagv,
                                const double *dsq, hipStream_t s);
@@ -260,6 +265,11 @@ hipError_t launch_gram_mismatch1_nb(const IndexGeom &g, const Packed &pk, const 
                                     const uint2 *nbseg, const uint2 *nbuse, const uint4 *table,
                                     int64_t row0, int64_t row1, int w0, int w1, int w2,
                                     const OutSpec &o, hipStream_t s, int threads, int unroll = 8);
+// KMG_CHECK: validate the filled lists' metadata (nb_check_kernel); flag[0] bit 0 set on a
+// violation, flag[1] = min offending list (the caller zeroes flag[0] and sets flag[1] to ~0)
+hipError_t launch_nb_check(int64_t nbins, const uint32_t *nboff, const uint2 *nbseg,
+                           const uint2 *nbuse, uint64_t table_pieces, uint32_t *flag,
+                           hipStream_t s);
 // all-pairs Hamming formulation, any (k <= 16, m): K = sum_{a,b} w[ham(x_a, y_b)]
 hipError_t launch_gram_hamming(const IndexGeom &g, const uint32_t *kmers, int64_t row0,
                                int64_t row1, const int64_t *wtab, const OutSpec &o, hipStream_t s);
@@ -363,6 +373,8 @@ hipError_t launch_shift_scale(const double *K, int64_t ldk, const double *s, dou
 // (1-based column j0 + j + 1); returns at once if *info != 0
 hipError_t launch_chol_diag(double *A, int64_t lda, int nb, int j0, int *info, double *Y, double *YT,
                             hipStream_t st);
+// dynamic LDS of one launch_chol_diag workgroup (its inverse: ~133 KB, gfx950's 160 KB LDS)
+size_t chol_diag_lds_bytes();
 // one block step of the substitution sweeps (forward: M = Y, back: M = Y^T)
 hipError_t launch_tri_sweep(const double *L, int64_t n, const double *M, int64_t j0, int jb, int back,
                             double *src, double *dst, hipStream_t st);

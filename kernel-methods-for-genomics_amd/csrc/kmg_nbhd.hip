@@ -1252,7 +1252,39 @@ __global__ __launch_bounds__(1024) void gram_nb_kernel(IndexGeom g, Packed pk,
 }
 
 
+// KMG_CHECK=1: the list metadata gram_nb_kernel trusts without a bound, validated after every
+// fill.  For each list: start <= end <= the table's pieces; non-empty: segment ends s0 <= s1
+// <= n16 (segments 0 / 1 lie in the 16-bit part) and n16 + np <= the list's span (the packed
+// pieces end inside it; the sorted fill shrinks a list, never grows it).  A violation sets
+// bit 0 of *flag (a vector-memory atomic) and records the first offending list in flag[1].
+__global__ __launch_bounds__(256) void nb_check_kernel(int64_t nbins, const uint32_t *__restrict__ nboff,
+                                                       const uint2 *__restrict__ nbseg,
+                                                       const uint2 *__restrict__ nbuse,
+                                                       uint64_t table_pieces, uint32_t *flag) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbins) return;
+  const uint32_t st = nboff[b], en = nboff[b + 1];
+  bool bad = en < st || (uint64_t)en > table_pieces;
+  if (!bad && en != st) {
+    const uint2 sg = nbseg[b], us = nbuse[b];
+    bad = sg.x > sg.y || sg.y > us.x || (uint64_t)us.x + us.y > (uint64_t)(en - st);
+  }
+  if (bad) {
+    atomicOr(flag, 1u);
+    atomicMin(flag + 1, (uint32_t)min<int64_t>(b, 0xFFFFFFFFLL));
+  }
+}
+
 // ------------------------------------------------------------------ host side
+hipError_t launch_nb_check(int64_t nbins, const uint32_t *nboff, const uint2 *nbseg,
+                           const uint2 *nbuse, uint64_t table_pieces, uint32_t *flag,
+                           hipStream_t s) {
+  if (nbins <= 0) return hipSuccess;
+  hipLaunchKernelGGL(nb_check_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, nbins,
+                     nboff, nbseg, nbuse, table_pieces, flag);
+  return hipGetLastError();
+}
+
 int64_t nb_list_entries_bound(int k, int64_t occurrences, int64_t nbins) {
   // every occurrence sits in the lists of its 1 + 3k + 9k(k-1)/2 neighbours; a non-empty list
   // pads each of its three segments by at most 7 entries

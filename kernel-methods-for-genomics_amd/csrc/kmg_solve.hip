@@ -488,11 +488,13 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(const double *__restrict
   YT[c + (lane + 64) * CHOL_NB] = y1;
 }
 
+size_t chol_diag_lds_bytes() { return sizeof(double) * (CHOL_NB * (CHOL_NB + 1) + CHOL_NB); }
+
 hipError_t launch_chol_diag(double *A, int64_t lda, int nb, int j0, int *info, double *Y, double *YT,
                             hipStream_t st) {
   if (nb <= 0 || nb > CHOL_NB) return hipErrorInvalidValue;
   hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(1024), 0, st, A, lda, nb, j0, info);
-  const size_t lds = sizeof(double) * (CHOL_NB * (CHOL_NB + 1) + CHOL_NB);
+  const size_t lds = chol_diag_lds_bytes();
   hipLaunchKernelGGL(chol_inv_kernel, dim3(CHOL_NB), dim3(1024), lds, st, (const double *)A, lda, nb,
                      (const int *)info, Y, YT);
   return hipGetLastError();

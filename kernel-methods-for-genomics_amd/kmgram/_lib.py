@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KMGRAM_LIB") or os.path.join(os.path.dirname(_HERE), "libkmgram.so")
 
 (KMG_OK, KMG_EINVAL, KMG_EUNSUPPORTED, KMG_EHIP, KMG_ENOMEM, KMG_ERCCL, KMG_ENODEV,
- KMG_ESINGULAR) = range(8)
+ KMG_ESINGULAR, KMG_EINTERNAL) = range(9)
 KMG_SPECTRUM, KMG_MISMATCH, KMG_WD, KMG_WDS, KMG_SUBSTRING, KMG_LOCALALIGN, KMG_GAPPY = range(1, 8)
 KMG_I32, KMG_F32, KMG_F64 = 1, 2, 3
 KMG_LA_REFERENCE, KMG_LA_INTENDED = 0, 1
@@ -247,7 +247,10 @@ class Context:
         full rows all-gathered in place over RCCL per round; 2 upper-triangle round slabs
         all-gathered + local mirror; 3 the upper-triangle layout with every rank's blocks
         computed locally (one-GPU rehearsal, no RCCL); 4 this rank's blocks packed (row
-        t * block + y of d_out = K row t * nranks * block + rank * block + y)."""
+        t * block + y of d_out = K row t * nranks * block + rank * block + y); 5 column blocks:
+        this rank's K[:, rank * block : (rank + 1) * block] (lists over its own sequences),
+        transposed into those rows of d_out, all-gathered in place over RCCL (one round:
+        nranks * block >= n rows); 6 the same with every rank's block on this GPU (no RCCL)."""
         g = int(gather) if not isinstance(gather, bool) else (1 if gather else 0)
         check(self.lib.kmg_gram_blocks(self._h, ctypes.byref(params), d_codes, d_lens, n, ldc,
                                        out_dtype, d_out, ld, int(nranks), int(rank), int(block),

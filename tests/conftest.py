@@ -11,6 +11,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # every Gram output is pre-filled with garbage, so a kernel that silently does not run
 # cannot pass by leaving a previous (correct) result in a reused device buffer
 os.environ.setdefault("KMG_POISON", "1")
+# every neighbourhood-list fill is followed by the metadata check (KMG_EINTERNAL instead of a
+# Gram kernel reading past a list: DESIGN §7)
+os.environ.setdefault("KMG_CHECK", "1")
 for p in (PKG, ORACLE, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -23,12 +23,15 @@ def spectrum_row_sums(codes, k, rows=None):
     return T[sub].sum(axis=1)
 
 
-def mismatch1_row_sums(codes, k, window=101, rows=None):
+def mismatch1_row_sums(codes, k, window=101, rows=None, cols=None):
     """Raw mismatch (k, m=1) row sums: sum_j K_ij = <Phi_i, C> with C = sum_j Phi_j the
     column sums of the neighbour-count map, C(b) = sum_{v: ham(v, b) <= 1} T(v), and
-    Phi_i = sum_a 1[B_1(u_a)], so sum_j K_ij = sum_a sum_{b in B_1(u_a)} C(b)."""
+    Phi_i = sum_a 1[B_1(u_a)], so sum_j K_ij = sum_a sum_{b in B_1(u_a)} C(b).
+    cols = (c0, c1): the sums over the columns [c0, c1) only (T from those sequences), i.e.
+    the row sums of a column block K[:, c0:c1]."""
     km = kmers(codes, k, window)
-    T = np.bincount(km.ravel(), minlength=4 ** k).astype(np.int64)
+    tk = km if cols is None else km[cols[0]:cols[1]]
+    T = np.bincount(tk.ravel(), minlength=4 ** k).astype(np.int64)
     b = np.arange(4 ** k, dtype=np.int64)
     flips = [d << (2 * (k - 1 - p)) for p in range(k) for d in (1, 2, 3)]
     C = T.copy()

@@ -287,40 +287,49 @@ for p in ("kernel-methods-for-genomics_amd", "oracle"):
 import numpy as np, torch, torch.distributed as dist
 import cref
 from kmgram import encode as E
-from kmgram.shard import rank_rows
 dist.init_process_group("gloo")
 r, w = dist.get_rank(), dist.get_world_size()
 n = 203
+block = -(-n // w)
 codes, lens = E.synthetic(n, 101, seed=11)
-c0, c1 = rank_rows(n, w, r)
-# this rank's column block K[:, c0:c1] as kmg_gram_device_cols lays it out (every row, the
-# block's columns), restated from the oracle's rows (K symmetric)
+c0, c1 = min(n, r * block), min(n, (r + 1) * block)
+# this rank's column block K[:, c0:c1] (every row, the block's columns) as the library's
+# gram_device_cols lays it out -- restated from the oracle's rows (K symmetric)
 blk = cref.mismatch_raw(codes, lens, 9, 1, rows=(c0, c1)).T.copy()
-parts = [None] * w
-dist.all_gather_object(parts, (c0, c1, blk.tolist()))
+# kmg_gram_blocks gather = 5: transposed into K's rows c0..c1 (the padded buffer holds
+# w * block rows), then one equal-count in-place all-gather of the block-row slabs
+K = torch.full((w * block, n), -7, dtype=torch.int64)
+K[c0:c1] = torch.from_numpy(np.ascontiguousarray(blk.T))
+parts = list(K.split(block))
+dist.all_gather(parts, parts[r].clone())
+ok = bool(np.array_equal(K[:n].numpy(), cref.mismatch_raw(codes, lens, 9, 1)))
+flag = torch.tensor([1 if ok else 0])
+dist.all_reduce(flag, op=dist.ReduceOp.MIN)
 if r == 0:
-    K = np.hstack([np.array(p[2], dtype=np.int64).reshape(n, p[1] - p[0]) for p in parts])
-    ref = cref.mismatch_raw(codes, lens, 9, 1)
-    print(json.dumps({"equal": bool(np.array_equal(K, ref)),
-                      "cover": [p[:2] for p in parts]}))
+    print(json.dumps({"assembled_equal": int(flag.item()), "block": block}))
 dist.destroy_process_group()
 """
 
 
-def test_gloo_world2_column_blocks(tmp_path):
-    """The collective-free config-5 share as column blocks (bench.py run_colblock_dist): the
-    ranks' K[:, C_r] blocks, C_r = rank_rows(n, G, r), tile K exactly."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_column_block_assembly(tmp_path, world):
+    """The layout of the column-block assembly (kmg_gram_blocks gather = 5): each rank's
+    column block K[:, C_r] (restated from the oracle's rows -- the library's blocks are
+    checked on the GPU: test_gpu_colblock.py, test_gpu_multi.py
+    test_column_block_assembly_*), transposed into K's rows C_r and all-gathered in place
+    over gloo, is the 1-rank K on every rank, byte for byte."""
     pytest.importorskip("torch")
     script = tmp_path / "c.py"
     script.write_text(COLBLOCK_WORKER)
     env = dict(os.environ, ROOT=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), str(script)]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     import json
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
-    assert d["equal"] and d["cover"] == [[0, 101], [101, 203]]
+    assert d["assembled_equal"] == 1 and d["block"] == -(-203 // world)
 
 
 def test_bench_rank_env_plumbing():

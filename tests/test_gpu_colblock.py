@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import cref
+import invariants as I
 from kmgram import _lib as L
 from kmgram import encode as E
 from kmgram import params as P
@@ -91,3 +92,77 @@ def test_column_block_argument_checks(ctx):
         _col_block(ctx, P.make(L.KMG_MISMATCH, k=9, m=2, window=101), codes, lens, 0, 32, L.KMG_I32)
     with pytest.raises(L.KmgError):
         _col_block(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101), codes, lens, 40, 30, L.KMG_I32)
+
+
+def _row_sums_parallel(blk, pool):
+    parts = np.array_split(np.arange(blk.shape[0]), 8)
+    return np.concatenate(list(pool.map(lambda r: blk[r].sum(axis=1, dtype=np.int64), parts)))
+
+
+@pytest.mark.parametrize("c0", [0, 100000])
+def test_config5_column_block_n200000_full(ctx, c0):
+    """The block bench.py times for config 5's G=8 share (BENCH `configs.config5_*colblock*`):
+    N=200000, columns [c0, c0 + 25000), raw int32, the packed two-chunk plan asserted.  Every
+    row's sum over the block's columns exact (invariants.mismatch1_row_sums with the block's
+    column histogram), oracle rows on both sides of the block's chunk edge and at its ends,
+    and the block's own square part symmetric across the chunk edge (kernels.py:196-217)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n, k, w, piece = 200000, 9, 25000, 8000
+    c1 = c0 + w
+    codes, lens = E.synthetic(n, 101, seed=5)
+    params = P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(n * w * 4)
+    pool = ThreadPoolExecutor(8)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device_cols(params, d_codes, d_lens, n, codes.shape[1], c0, c1, L.KMG_I32, d_out, w)
+        ctx.synchronize()
+        plan = ctx.last_plan()
+        assert plan["formulation"] == "neighbourhood" and plan["packed"], plan
+        assert plan["nchunks"] == 2 and not plan["triangle"], plan
+        ch = plan["chunk"]
+        sums = I.mismatch1_row_sums(codes, k, cols=(c0, c1))
+        buf = np.empty((piece, w), dtype=np.int32)
+        for a in range(0, n, piece):
+            ctx.d2h(buf, ctypes.c_void_p(d_out.value + a * w * 4))
+            assert np.array_equal(_row_sums_parallel(buf, pool), sums[a:a + piece]), a
+        rows = sorted({0, n - 1, max(0, c0 - 1), c0, c0 + ch - 1, c0 + ch, c1 - 1, min(n - 1, c1)})
+        refs = list(pool.map(lambda r: cref.mismatch_raw(codes, lens, k, 1, rows=(r, r + 1))[0], rows))
+        row = np.empty(w, dtype=np.int32)
+        for r, ref in zip(rows, refs):
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * w * 4))
+            assert np.array_equal(row.astype(np.int64), ref[c0:c1]), r
+        # K[c0 + a, c0 + b] for a 256-square straddling the chunk edge: symmetric
+        e = ch - 128
+        sq = np.empty((256, w), dtype=np.int32)
+        ctx.d2h(sq, ctypes.c_void_p(d_out.value + (c0 + e) * w * 4))
+        S = sq[:, e:e + 256]
+        assert np.array_equal(S, S.T)
+    finally:
+        pool.shutdown()
+        for p in (d_out, d_codes, d_lens):
+            ctx.dfree(p)
+
+
+def test_column_block_packed_float64_n20000(ctx, tune):
+    """The packed lists (KMG_NB_FILL=1) on a float64 normalised column block at N=20000:
+    the raw int32 block, every row sum exact over the block's columns, then the normalised
+    block entry for entry = raw / (sqrt(K_ii) * sqrt(K_jj)) with the diagonal 1.0 --
+    normalize_K's expression (kernels.py:408-414) -- from the oracle's diagonal."""
+    n, k, c0, c1 = 20000, 9, 6000, 13500
+    w = c1 - c0
+    tune(KMG_NB_FILL="1")
+    codes, lens = E.synthetic(n, 101, seed=3)
+    raw = _col_block(ctx, P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0), codes, lens,
+                     c0, c1, L.KMG_I32)
+    assert ctx.last_plan()["packed"]
+    assert np.array_equal(raw.sum(axis=1, dtype=np.int64), I.mismatch1_row_sums(codes, k, cols=(c0, c1)))
+    Kn = _col_block(ctx, P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
+                    c0, c1, L.KMG_F64)
+    assert ctx.last_plan()["packed"]
+    d = np.sqrt(cref.mismatch_diag(codes, lens, k, 1).astype(np.float64))
+    ref = raw.astype(np.float64) / (d[:, None] * d[None, c0:c1])
+    ref[np.arange(c0, c1), np.arange(w)] = 1.0
+    assert np.array_equal(Kn, ref)

@@ -240,3 +240,48 @@ def test_svm_both_factorisations(ctx, tune, chol):
     ra, rsteps, robj = cpu_ref.svm_dual(K, y, C)
     assert obj == pytest.approx(robj, rel=1e-9, abs=1e-12)
     np.testing.assert_allclose(a, ra, atol=1e-5 * C, rtol=0)
+
+
+@pytest.mark.parametrize("panels", ["0", "3", "4"])
+@pytest.mark.parametrize("n", [1500, 2101])
+def test_krr_trailing_update_panels(ctx, tune, panels, n):
+    """The blocked Cholesky's trailing update as KMG_CHOL_PANELS GEMM column panels (taken
+    once the trailing triangle is >= 1024 rows: the n = 9000 production path) against one
+    dsyrk (0): ragged last panels (n = 2101: 1845 rows in 3 or 4 panels) and the panel
+    offsets, against numpy's inv (KRR.py:33)."""
+    tune(KMG_CHOL="1", KMG_CHOL_PANELS=panels)
+    K = _psd(n, n // 3, 11 * n)
+    y = np.where(np.random.default_rng(n + 9).random(n) > 0.5, 1.0, -1.0)
+    got = ctx.krr_solve(K, y, 0.02)
+    assert ctx.last_factorisation() == "cholesky"
+    np.testing.assert_allclose(got, cpu_ref.krr_alpha(K, y, 0.02), rtol=1e-9, atol=1e-12)
+
+
+def test_svm_panel_path_n1700(ctx, tune):
+    """One C-SVM fit (SVM.py:78-89) at a size whose factorisations take the GEMM-panel
+    trailing update (KMG_CHOL=1, default panels)."""
+    tune(KMG_CHOL="1", KMG_CHOL_PANELS=None)
+    n, C = 1700, 1.0
+    K = _psd(n, n // 4, 1701)
+    y = np.where(np.random.default_rng(1702).random(n) > 0.5, 1.0, -1.0)
+    a, steps, obj = ctx.svm_fit(K, y, C)
+    ra, rsteps, robj = cpu_ref.svm_dual(K, y, C)
+    assert steps < 100
+    assert obj == pytest.approx(robj, rel=1e-9, abs=1e-12)
+    np.testing.assert_allclose(a, ra, atol=1e-5 * C, rtol=0)
+
+
+def test_device_lds_allows_in_tree_cholesky():
+    """The in-tree factorisation needs ~133 KB of LDS a workgroup (chol_inv_kernel); the
+    library uses it only where the device reports that much (use_own_chol, else rocSOLVER).
+    On the MI355X it must be taken: the largest of the runtime's LDS attributes >= 133 KB."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    vals = []
+    # hipDeviceAttributeMaxSharedMemoryPerBlock, ...SharedMemPerBlockOptin,
+    # ...MaxSharedMemoryPerMultiprocessor (ROCm 7.2 hip_runtime_api.h enum values)
+    for attr in (74, 75, 10002):
+        v = ctypes.c_int(0)
+        if hip.hipDeviceGetAttribute(ctypes.byref(v), attr, 0) == 0:
+            vals.append(v.value)
+    assert max(vals) >= 8 * (128 * 129 + 128), vals

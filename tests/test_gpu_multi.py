@@ -288,3 +288,80 @@ def test_upper_triangle_slabs_other_formulations(ctx, params, dt, wire):
         ctx.dfree(d_lens)
     assert np.array_equal(got, full)
     assert ctx.blocks_wire() == wire
+
+
+# ---------------------------------------------------------------- column-block assembly
+def _colblock_assembly(ctx, data, params, dt, world, block, gather):
+    codes, lens, d_codes, d_lens = data
+    n, ldc = codes.shape
+    esz = np.dtype(L.DTYPES[dt]).itemsize
+    npad = world * block
+    d_out = ctx.dmalloc(npad * n * esz)
+    try:
+        ctx.memset(d_out, 0xA5, npad * n * esz)
+        ctx.gram_blocks(params, d_codes, d_lens, n, ldc, dt, d_out, n, world, 0, block, gather)
+        ctx.synchronize()
+        out = np.empty((n, n), dtype=L.DTYPES[dt])
+        ctx.d2h(out, d_out)
+        return out
+    finally:
+        ctx.dfree(d_out)
+
+
+@pytest.mark.parametrize("case", [1, 2])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_column_block_assembly_equals_full(ctx, data, case, world):
+    """gather = 6 (the one-GPU rehearsal of gather = 5): every rank's column block K[:, C_q]
+    (lists over its own sequences) computed, transposed into K's rows C_q: exactly the
+    single-call K (the buffer starts poisoned), the packed lists included."""
+    params, dt = CASES[case]
+    codes, lens = data[0], data[1]
+    n = codes.shape[0]
+    full = ctx.gram(params, codes, lens, dt)
+    block = -(-n // world)
+    got = _colblock_assembly(ctx, data, params, dt, world, block, 6)
+    assert np.array_equal(got, full)
+    assert ctx.last_plan()["formulation"] == "neighbourhood"
+
+
+def test_column_block_assembly_single_rank_comm(ctx, data):
+    """gather = 5 on a 1-rank RCCL communicator (the in-place all-gather after the transpose,
+    comm-stream ordering), and the argument checks: nranks * block must cover n, and a
+    communicator of another size is refused."""
+    params, dt = CASES[1]
+    codes, lens = data[0], data[1]
+    n = codes.shape[0]
+    full = ctx.gram(params, codes, lens, dt)
+    uid = L.Context.unique_id()
+    ctx.comm_init(uid, 1, 0)
+    try:
+        got = _colblock_assembly(ctx, data, params, dt, 1, n, 5)
+        assert np.array_equal(got, full)
+        with pytest.raises(L.KmgError):  # communicator size must match
+            _colblock_assembly(ctx, data, params, dt, 2, -(-n // 2), 5)
+    finally:
+        ctx.comm_destroy()
+    with pytest.raises(L.KmgError):  # 3 x 400 rows do not cover n = 1500
+        _colblock_assembly(ctx, data, params, dt, 3, 400, 6)
+    with pytest.raises(L.KmgUnsupported):  # column blocks are a mismatch (k, 1) path
+        _colblock_assembly(ctx, data, CASES[0][0], CASES[0][1], 2, 750, 6)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_column_block_assembly_n20000(ctx, world):
+    """BASELINE configs[2]'s K (N=20000, float64 normalised) assembled from column blocks
+    (gather = 6) equals the single-call K bit for bit."""
+    n = 20000
+    codes, lens = E.synthetic(n, 101, seed=3)
+    params = P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=1)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        full = ctx.gram(params, codes, lens, L.KMG_F64)
+        got = _colblock_assembly(ctx, (codes, lens, d_codes, d_lens), params, L.KMG_F64, world,
+                                 -(-n // world), 6)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    assert np.array_equal(got, full)
