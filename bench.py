@@ -265,13 +265,17 @@ def run_build(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, check_
             ctx.synchronize()
         # spot check: the first row of this rank's first block, plus (G > 1) a row computed
         # by the next rank and received through the all-gather
-        rows = [mine[0][0]]
+        rows = [mine[0][0], mine[0][1] - 1]
+        ch = (res.get("plan") or {}).get("chunk") or 0
+        if world == 1 and 0 < ch < n:  # a row at a column-chunk edge (its diagonal entry
+            rows += [ch - 1, ch]          # on either side of the edge)
         if gather:
             rows.append(block_cyclic_ranges(n, world, (rank + 1) % world, block)[0][0])
+        rows = sorted(set(rows))
         ok = True
         for r in rows:
             row = np.empty(n, dtype=L.DTYPES[out_dtype])
-            orow = 0 if packed else r  # (packed: the rank's first block starts at row 0)
+            orow = r - mine[0][0] if packed else r  # (packed: the rank's first block at row 0)
             ctx.d2h(row, ctypes.c_void_p(d_out.value + orow * n * esz))
             ok &= check_row(codes, lens, r, row)
         res["spot_check_rows"] = rows
@@ -302,8 +306,9 @@ def check_mismatch_raw(codes, lens, r, row):
 
 
 def write_ceiling(ctx, d_out, nbytes, reps=10):
-    """Measured HBM write ceiling on this box: hipMemsetAsync over the same K buffer
-    (context stream, HIP events) -> GB/s.  Reported beside the 8 TB/s spec peak."""
+    """hipMemsetAsync over the same K buffer (context stream, HIP events) -> GB/s: the
+    runtime fill's rate on this box, reported as `memset_GBps` beside the 8 TB/s spec peak
+    (not a ceiling: the spectrum Gram kernel's 16-byte row stores run above it)."""
     ctx.memset(d_out, 0, nbytes)
     ctx.synchronize()
     ctx.set_timing(True)
@@ -542,6 +547,69 @@ def run_colblock_dist(ctx, dist, params, out_dtype, n, seed, steps, warmup, orac
             "pairs_per_s": n * n / (ms / 1e3), "plan": plan, "spot_check": ok}
 
 
+def run_colblock_assembly(ctx, dist, params, out_dtype, n, seed, steps, warmup, oracle_row,
+                          world=None):
+    """Config 5 assembled from column blocks (kmg_gram_blocks gather 5): each rank
+    its column block K[:, C_r] (lists over its own n/G sequences, packed), transposed into
+    its row slab, then one in-place RCCL all-gather -- K on every GPU.  world (with
+    dist.world == 1): the one-GPU rehearsal (gather 6) of a `world`-rank job, every rank's
+    block computed here: its Gram / transpose stage times are what the projection uses.
+    Timed like run_build: barrier + synchronise on both sides, max over ranks."""
+    rehearsal = world is not None
+    world = world if rehearsal else dist.world
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    block = -(-n // world)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(world * block * n * esz)
+    gather = 6 if rehearsal else 5
+    try:
+        def step():
+            ctx.gram_blocks(params, d_codes, d_lens, n, ldc, out_dtype, d_out, n, world,
+                            0 if rehearsal else dist.rank, block, gather)
+
+        for _ in range(warmup):
+            step()
+        ctx.synchronize()
+        ctx.set_timing(2)
+        ctx.timing_reset()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.synchronize()
+        dist.barrier()
+        t = dist.max(time.perf_counter() - t0) / steps
+        stages = stage_means(ctx)
+        unpack_tot, unpack_cnt = ctx.stage_stats("unpack")
+        ctx.set_timing(False)
+        plan = ctx.last_plan()
+        # spot rows: the first row of rank 0's and of the last rank's slab, and the last row
+        # (each received through the all-gather on every other rank)
+        rows = sorted({0, (world - 1) * block, n - 1})
+        ok = True
+        for r in rows:
+            row = np.empty(n, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * n * esz))
+            ref = oracle_row(codes, lens, r)
+            ok &= bool(np.array_equal(row.astype(ref.dtype), ref))
+        ok = dist.all_true(ok)
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    out = {"N": n, "world": world, "block": block, "gather_mode": gather, "steps": steps,
+           "ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages,
+           "transpose_ms_per_step": unpack_tot / steps, "transposes_per_step": unpack_cnt / steps,
+           "plan": plan, "spot_check_rows": rows, "spot_check": ok}
+    if rehearsal:
+        out["per_rank_ms_model"] = t * 1e3 / world
+    return out
+
+
 def extras(ctx, cpu_rates, steps4):
     """BASELINE configs[3] and [4], the drop-in host path, run.py's kernels, downstream."""
     import cref
@@ -578,6 +646,15 @@ def extras(ctx, cpu_rates, steps4):
     c5cr["workload"] = ("config-5 raw int32 K's 1/8 share as a column block (the G=8 share of the "
                         "config5 full_1gpu build, collective-free)")
     out["config5_mismatch_k9_n200000_colblock_raw_int32"] = c5cr
+    # the G = 8 column-block assembly rehearsed on this GPU: all 8 ranks' blocks + transposes
+    # into one 160 GB K (no RCCL); the all-gather is modelled in projection()
+    c5ca = run_colblock_assembly(ctx, Dist(), P.make(L.KMG_MISMATCH, k=9, m=1, window=101,
+                                                     normalize=0), L.KMG_I32, n5, 5, 1, 1, mmr,
+                                 world=8)
+    c5ca["workload"] = ("config-5 raw int32 K from 8 column blocks, each transposed into its row "
+                        "slab (kmg_gram_blocks gather 6: the G=8 column-block assembly without "
+                        "its all-gather, every rank on this GPU)")
+    out["config5_mismatch_k9_n200000_colblock_assembly_rehearsal_g8"] = c5ca
     c5f = run_slab(ctx, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
                    n5, 5, 0, n5, 1, 1, (0, n5 - 1), mmr)
     c5f["workload"] = ("BASELINE configs[4] on ONE GPU: the full 200000 x 200000 raw int32 K "
@@ -965,6 +1042,20 @@ def projection(sp, n, extra):
                 cb["ms_per_step"]
             out["config5_mismatch_k9_n200000_raw_int32"]["8"]["collective_free_measured_speedup"] = \
                 c5["ms_per_step"] / cb["ms_per_step"]
+        ca = (extra or {}).get("config5_mismatch_k9_n200000_colblock_assembly_rehearsal_g8")
+        if cb and ca:
+            # K on every GPU from column blocks (gather 5): one rank's block (measured) + its
+            # transpose (the rehearsal's mean) + the in-place all-gather of int32 row slabs,
+            # (G - 1) / G x 4 N^2 bytes into every GPU over its 7 links, in sequence (one round)
+            tr = ca["transpose_ms_per_step"] / max(1.0, ca["transposes_per_step"])
+            recv = 7.0 / 8.0 * 4.0 * n5 * n5 / XGMI_IN_PEAK * 1e3
+            tot = cb["ms_per_step"] + tr + recv
+            out["config5_mismatch_k9_n200000_raw_int32"]["8"]["colblock_assembled"] = {
+                "block_ms_measured": cb["ms_per_step"], "transpose_ms_measured": tr,
+                "receive_ms_model": recv, "ms_model": tot,
+                "speedup_model": c5["ms_per_step"] / tot,
+                "note": "int32 row slabs: 4x the bytes of the uint8 upper-triangle round slabs "
+                        "the row-block path sends (every_gpu above), so receive-bound further out"}
     return out
 
 
@@ -1029,6 +1120,9 @@ def _projection_summary(proj):
             if "collective_free_measured_speedup" in g8:
                 out[k.split("_")[0]]["collective_free_measured_share"] = _r(
                     g8["collective_free_measured_speedup"], 3)
+            if "colblock_assembled" in g8:
+                out[k.split("_")[0]]["colblock_assembled"] = _r(
+                    g8["colblock_assembled"]["speedup_model"], 3)
     return out
 
 
@@ -1135,6 +1229,13 @@ def main():
         c5 = run_build(ctx, dist, "mismatch_k9_m1_raw",
                        P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0), L.KMG_I32,
                        200000, 5, 2, 1, check_mismatch_raw)
+    c5ca = None
+    if rccl and not args.no_extra:
+        # config 5 assembled from column blocks (gather 5): K on every GPU, int32 all-gather
+        import cref
+        c5ca = run_colblock_assembly(ctx, dist, P.make(L.KMG_MISMATCH, k=9, m=1, window=101, normalize=0),
+                                     L.KMG_I32, 200000, 5, 2, 1,
+                                     lambda c, l, r: cref.mismatch_raw(c, l, 9, 1, rows=(r, r + 1))[0])
     c5cb = None
     if dist.world > 1 and not args.no_extra:
         # config 5 collective-free at G > 1: each GPU its column block of the raw int32 K
@@ -1161,9 +1262,11 @@ def main():
             "kernel": "kmg::gram_sp_kernel<true,1,%s>" % ("true" if n > 24576 else "false"),
             "kernel_ms": st["gram"],
             "alg_bytes_per_launch": alg_bytes,
-            "measured_write_ceiling_GBps": sp.get("write_ceiling_GBps"),
-            "frac_of_measured_ceiling": (achieved / 1e9 / sp["write_ceiling_GBps"]
-                                         if sp.get("write_ceiling_GBps") else None)}
+            # hipMemsetAsync over the same K buffer in the same run: a reference rate, not a
+            # ceiling (the Gram kernel's own stores run faster than it)
+            "memset_GBps": sp.get("write_ceiling_GBps"),
+            "ratio_to_memset": (achieved / 1e9 / sp["write_ceiling_GBps"]
+                                if sp.get("write_ceiling_GBps") else None)}
 
     line = {
         "metric": METRIC, "value": sp["pairs_per_s"], "unit": "Gram pairs/s",
@@ -1232,6 +1335,12 @@ def main():
             **{k: c5[k] for k in ("ms_per_step", "pairs_per_s", "stages_ms", "block_rows",
                                   "rounds", "spot_check", "collective_free")},
             "gather_roofline": gather_roofline(c5, dist.world, 4)}
+    if c5ca:
+        line["config5_colblock_assembled"] = {
+            "workload": "BASELINE configs[4]: mismatch (9,1), N=200000, raw int32 K on every GPU "
+                        "from G column blocks, each transposed into its row slab, one in-place "
+                        "RCCL all-gather (kmg_gram_blocks gather 5)",
+            "scaling": "strong", **c5ca}
     if c5cb:
         line["config5_colblock_collective_free"] = {
             "workload": "BASELINE configs[4]: mismatch (9,1), N=200000, raw int32 K as G column "
