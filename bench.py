@@ -183,7 +183,7 @@ def stage_means(ctx):
         tot, cnt = ctx.stage_stats(st)
         if cnt:
             out[st] = round(tot / cnt, 5)
-            if st in ("gram", "gather"):
+            if st in ("gram", "gather", "mirror"):
                 out[st + "_launches"] = cnt
                 out[st + "_total"] = round(tot, 5)
     return out
@@ -481,6 +481,8 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         wall = time.perf_counter() - t0
         ctx.set_timing(False)
         stages = stage_means(ctx)
+        if "mirror_total" in stages:  # (the mirror runs as one launch per row chunk)
+            stages["mirror_per_build"] = round(stages["mirror_total"] / steps, 5)
         plan = ctx.last_plan()
         ok = True
         for r in spot_rows:
@@ -1032,7 +1034,8 @@ def projection(sp, n, extra):
         nch = -(-n5 // ch5)
         g_rows = s5["gram"] * (2.0 * nch) / (nch + 1) if s5.get("mirror") else s5["gram"]
         out["config5_mismatch_k9_n200000_raw_int32"] = {
-            "one_gpu": {"gram_ms": s5["gram"], "mirror_ms": s5.get("mirror"),
+            "one_gpu": {"gram_ms": s5["gram"],
+                        "mirror_ms": s5.get("mirror_per_build", s5.get("mirror")),
                         "full_rows_gram_ms_model": g_rows},
             **{str(g): v for g, v in scaling_projection(
                 n5, c5["ms_per_step"], t5_index, g_rows, fill, 4, 1, chunk=ch5).items()}}
@@ -1097,6 +1100,8 @@ def _compact_configs(extra):
             st = v.get("stages_ms") or {}
             rec["stages_ms"] = {kk: _r(st[kk], 3) for kk in ("nbfill", "diag", "gram", "mirror")
                                 if kk in st}
+            if "mirror_per_build" in st:  # (one mirror launch per row chunk)
+                rec["stages_ms"]["mirror"] = _r(st["mirror_per_build"], 3)
             pl = v.get("plan") or {}
             if pl:
                 rec["plan"] = {kk: pl.get(kk) for kk in ("formulation", "nchunks", "packed") if kk in pl}
@@ -1196,9 +1201,23 @@ def main():
     # KMG_BENCH_NO_RCCL=1: the collective-free lines only (a rehearsal of the G > 1 headline
     # with several ranks on one GPU, where RCCL refuses duplicate devices)
     rccl = dist.world > 1 and os.environ.get("KMG_BENCH_NO_RCCL") != "1"
+    rccl_error = None
     if rccl:
-        uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
-        ctx.comm_init(uid, dist.world, dist.rank)
+        # the communicator is the only RCCL step every G > 1 line needs; if it cannot be
+        # built on every rank, the collective-free lines (the headline) still run
+        comm_ok = False
+        try:
+            uid = dist.bcast_bytes(L.Context.unique_id() if dist.rank == 0 else None)
+            ctx.comm_init(uid, dist.world, dist.rank)
+            comm_ok = True
+        except L.KmgError as e:
+            rccl_error = repr(e)
+            print(f"rank {dist.rank}: RCCL communicator failed: {e}", file=sys.stderr)
+        if not dist.all_true(comm_ok):
+            if comm_ok:
+                ctx.comm_destroy()
+            rccl = False
+            rccl_error = rccl_error or "another rank's ncclCommInitRank failed"
     # headline at every G: the named N = n1 (strong scaling), rows sharded over the ranks
     # with no data-path collective (the rows of K are independent: SURVEY §8e); at G > 1
     # the north-star's final RCCL all-gather (K assembled on every GPU) is `assembled` and
@@ -1286,7 +1305,7 @@ def main():
                    "rows_this_rank": sp["rows_this_rank"],
                    "rows_per_rank": sp["rows_per_rank"],
                    "devices_per_rank": sp["devices_per_rank"],
-                   "rccl": rccl,
+                   "rccl": rccl, "rccl_error": rccl_error,
                    "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
         "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],

@@ -271,19 +271,21 @@ hipEvent_t pool_event(kmg_ctx *c) {
 
 struct StageTimer {
   kmg_ctx *c;
+  hipStream_t st;
   hipEvent_t end = nullptr;
-  StageTimer(kmg_ctx *c_, int i) : c(c_) {
+  // events on stream s (default: the context stream)
+  StageTimer(kmg_ctx *c_, int i, hipStream_t s = nullptr) : c(c_), st(s ? s : c_->stream) {
     if (c->timing == 1 ||
         (c->timing == 2 && (i == ST_GRAM || i == ST_GATHER || i == ST_MEMSET || i == ST_UNPACK ||
                             i == ST_MIRROR))) {
       hipEvent_t b = pool_event(c);
       end = pool_event(c);
-      (void)hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, st);
       c->ev_log.push_back({i, {b, end}});
     }
   }
   ~StageTimer() {
-    if (end) (void)hipEventRecord(end, c->stream);
+    if (end) (void)hipEventRecord(end, st);
   }
 };
 
@@ -860,6 +862,10 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
   c->cur_n = n;
   const bool colblk = ncols >= 0;
   if (!colblk) ncols = n;
+  // column blocks: only the posting-list paths below index a block's sequences (checked
+  // there); every other kernel writes whole rows, which a block's ld_out cannot hold
+  if (colblk && p->kind != KMG_SPECTRUM && p->kind != KMG_MISMATCH)
+    return fail(KMG_EUNSUPPORTED, "column blocks: spectrum / mismatch only");
   if (cseq0 < 0 || cseq0 + ncols > n) return fail(KMG_EINVAL, "bad column range");
   for (const RowRange &r : ranges)
     if (r.row0 < 0 || r.row1 > n || r.row0 > r.row1) return fail(KMG_EINVAL, "bad row range");
@@ -909,6 +915,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       if (k > 16) {
         // k-mers past 32 bits: the generic per-pair kernels (kmg_generic.hip)
         c->plan[0] = KMG_PLAN_GENERIC;
+        if (colblk) return fail(KMG_EUNSUPPORTED, "column blocks: k = %d past the posting-list paths", k);
         if (narrow) return fail(KMG_EINVAL, "internal: 8/16-bit slabs need a posting-list formulation");
         if (dt == KMG_I32 && p->normalize)
           return fail(KMG_EINVAL, "normalised output needs a floating dtype");
@@ -978,11 +985,14 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       }
       const bool exact = !mm || p->m == 0;           // spectrum-shaped: only ham 0 counts
       SmPath path = sm_path(c->tune, p, g.pmax, n);
-      if (colblk) {  // column blocks: the neighbourhood lists over the block's sequences
-        if (!(mm && p->m == 1 && k >= 4 && k <= 12) || (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64) ||
-            after || ranges.size() != 1 || ranges[0].col_lo != 0)
-          return fail(KMG_EUNSUPPORTED, "column blocks: mismatch (k, 1) with 4 <= k <= 12 only");
-        path = SM_NB;
+      if (colblk) {  // column blocks: the lists / postings over the block's sequences
+        const bool cb_mm = mm && p->m == 1 && k >= 4 && k <= 12;
+        const bool cb_sp = !mm && path == SM_POSTING;
+        if (!(cb_mm || cb_sp) || (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64) || after ||
+            ranges.size() != 1 || ranges[0].col_lo != 0)
+          return fail(KMG_EUNSUPPORTED, "column blocks: mismatch (k, 1) with 4 <= k <= 12, or the "
+                      "spectrum posting-list path (6 <= k <= 16), only");
+        if (cb_mm) path = SM_NB;
       }
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
       const bool use_nb = path == SM_NB;
@@ -1217,28 +1227,47 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           }
         }
         o.col_seq0 = cseq0;
-        KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
+        auto nb_launch = [&](int64_t r0, int64_t r1, const OutSpec &oq) {
           return launch_gram_mismatch1_nb(gc, pkd, c->pr_rbase.as<uint32_t>(), c->nb_seg.as<uint2>(),
                                           c->nb_use.as<uint2>(), c->nb_lines.as<uint4>(), r0, r1,
                                           (int)w[0], (int)w[1], (int)w[2], oq, c->stream, nbt,
                                           c->tune.nb_unroll ? c->tune.nb_unroll
                                                             : (o.tri || c->plan[5] ? 4 : 8));
-        }, true));
+        };
+        KMG_TRY(each_range(c, ranges, o, after, nb_launch, true));
         return mirror();
       }
+      // gi: the geometry of the columns (the index and the chunking); g keeps all n rows (the
+      // diagonal).  A spectrum column block indexes only its own ncols sequences.
+      IndexGeom gi = g;
       if (exact) {
         g.copies = 1;
         g.nkeys = (uint32_t)pow4(k);
-        choose_chunks(g, std::min(65536, c->tune.sp_chunk));
+        gi = g;
+        gi.n = ncols;
+        choose_chunks(gi, std::min(65536, c->tune.sp_chunk));
+        g.chunk = gi.chunk;
+        g.nchunks = gi.nchunks;
       } else {
         g.copies = k;
         g.rot = 1;
         g.nkeys = (uint32_t)pow4(k);
         choose_chunks(g, slot_chunk(n, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz));
         o.tri = use_slots && tri_esz > 0 && g.nchunks > 1;
+        gi = g;
       }
       note_plan(1024);
-      KMG_TRY(build_index(c, g, pkd, d_codes, d_lens, ldc));
+      if (!colblk) {
+        KMG_TRY(build_index(c, gi, pkd, d_codes, d_lens, ldc));
+      } else {  // every row's record, then the index over the block's (already packed) ones
+        {
+          StageTimer t(c, ST_PACK);
+          KMG_HIP(launch_pack(d_codes, d_lens, n, ldc, g.window, c->packed.as<uint32_t>(), c->stream));
+        }
+        const Packed pkc{pkd.w + cseq0 * pkd.ldp, pkd.ldp, pkd.cw};
+        KMG_TRY(build_index(c, gi, pkc));
+        o.col_seq0 = cseq0;
+      }
       if (use_slots) {
         KMG_TRY(c->slots.ensure((size_t)(g.nbins() >> 2) * KMG_SLOT_BYTES));
         StageTimer t(c, ST_SLOTS);
@@ -1255,7 +1284,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         }
       }
       KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
-        return exact ? launch_gram_spectrum(g, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
+        return exact ? launch_gram_spectrum(gi, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                             r0, r1, oq, c->stream, c->tune.sp_store,
                                             c->tune.sp_order)
                      : launch_gram_mismatch1_slots(g, pkd, c->slots.as<uint4>(),

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
         const uint2 w = *(const uint2 *)&acc[q];
         v0 = w.x; v1 = w.y;
       }
-      const int64_t c0 = col0 + q;
+      const int64_t c0 = o.col_seq0 + col0 + q;  // the column's sequence (column blocks)
       const bool two = q + 1 < cw;
       double r0 = (double)v0, r1 = (double)v1;
       if (norm) {  // normalize_K: K[i,j] / (sqrt(K[i,i]) * sqrt(K[j,j])), diagonal := 1

@@ -86,8 +86,12 @@ def test_column_block_is_row_slab_transposed_n20000(ctx):
 
 def test_column_block_argument_checks(ctx):
     codes, lens = E.synthetic(64, 101, seed=5)
+    with pytest.raises(L.KmgUnsupported):  # k > 16: the generic per-pair kernels
+        _col_block(ctx, P.make(L.KMG_SPECTRUM, k=20), codes, lens, 0, 32, L.KMG_I32)
+    with pytest.raises(L.KmgUnsupported):  # whole-row kernels (a block's ld cannot hold a row)
+        _col_block(ctx, P.make(L.KMG_WD, d=5), codes, lens, 0, 32, L.KMG_F64)
     with pytest.raises(L.KmgUnsupported):
-        _col_block(ctx, P.make(L.KMG_SPECTRUM, k=8), codes, lens, 0, 32, L.KMG_I32)
+        _col_block(ctx, P.make(L.KMG_MISMATCH, k=20, m=1, window=101), codes, lens, 0, 32, L.KMG_I32)
     with pytest.raises(L.KmgUnsupported):
         _col_block(ctx, P.make(L.KMG_MISMATCH, k=9, m=2, window=101), codes, lens, 0, 32, L.KMG_I32)
     with pytest.raises(L.KmgError):
@@ -166,3 +170,35 @@ def test_column_block_packed_float64_n20000(ctx, tune):
     ref = raw.astype(np.float64) / (d[:, None] * d[None, c0:c1])
     ref[np.arange(c0, c1), np.arange(w)] = 1.0
     assert np.array_equal(Kn, ref)
+
+
+@pytest.mark.parametrize("k", [6, 8, 12])
+def test_spectrum_column_blocks_vs_full(ctx, k):
+    """Spectrum column blocks (get_spectrum_K, kernels.py:28-47): the posting index over the
+    block's sequences only, every row; int32 raw and float64 normalised blocks equal the
+    columns of the single-call K bit for bit (ragged rows: lengths 60..101)."""
+    codes, lens = E.synthetic(900, 101, seed=300 + k)
+    lens[::7] = 60 + (np.arange(len(lens[::7])) % 41)
+    full = ctx.gram(P.make(L.KMG_SPECTRUM, k=k), codes, lens, L.KMG_I32)
+    fulln = ctx.gram(P.make(L.KMG_SPECTRUM, k=k, normalize=1), codes, lens, L.KMG_F64)
+    for col0, col1 in ((0, 900), (0, 113), (400, 777), (899, 900)):
+        K = _col_block(ctx, P.make(L.KMG_SPECTRUM, k=k), codes, lens, col0, col1, L.KMG_I32)
+        assert ctx.last_plan()["formulation"] == "posting"
+        assert np.array_equal(K, full[:, col0:col1]), (col0, col1)
+        Kn = _col_block(ctx, P.make(L.KMG_SPECTRUM, k=k, normalize=1), codes, lens, col0, col1,
+                        L.KMG_F64)
+        assert np.array_equal(Kn, fulln[:, col0:col1]), (col0, col1)
+
+
+def test_spectrum_column_block_n100000(ctx):
+    """The G = 8 share of the headline (BASELINE configs[3]) as a column block: K[:, 37500:
+    50000] of all 100000 rows, every row sum exact over the block's columns (sum_u phi_i(u)
+    T_block(u)) and oracle rows."""
+    n, k, c0, c1 = 100000, 8, 37500, 50000
+    codes, lens = E.synthetic(n, 101, seed=4)
+    K = _col_block(ctx, P.make(L.KMG_SPECTRUM, k=k), codes, lens, c0, c1, L.KMG_I32)
+    km = I.kmers(codes, k)
+    T = np.bincount(km[c0:c1].ravel(), minlength=4 ** k)
+    assert np.array_equal(K.sum(axis=1, dtype=np.int64), T[km].sum(axis=1))
+    for r in (0, c0, c1 - 1, n - 1):
+        assert np.array_equal(K[r].astype(np.int64), cref.spectrum(codes, lens, k, rows=(r, r + 1))[0, c0:c1]), r
