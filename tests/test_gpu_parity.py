@@ -566,3 +566,47 @@ def test_rccl_allgather_single_rank(ctx):
         ctx.comm_destroy()
         for p_ in (d_out, d_codes, d_lens):
             ctx.dfree(p_)
+
+
+def test_spectrum_column_chunks(ctx, tune):
+    """Spectrum over several column chunks (the config-4 layout at a small N): full K (int32
+    and float64 normalised), a row slab and block-cyclic rows of three ranks (several ranges
+    per call) equal the oracle (get_spectrum_K, kernels.py:28-47; normalize_K,
+    kernels.py:398-415), ragged rows included."""
+    import ctypes
+    codes, lens = E.synthetic(1300, 101, seed=77)
+    lens[::5] = 40 + (np.arange(len(lens[::5])) % 62)
+    tune(KMG_SP_CHUNK="304")
+    ref = cref.spectrum(codes, lens, 8)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    assert ctx.last_plan()["nchunks"] > 1
+    assert np.array_equal(K.astype(np.int64), ref)
+    Kn = ctx.gram(P.make(L.KMG_SPECTRUM, k=8, normalize=1), codes, lens, L.KMG_F64)
+    d = np.sqrt(np.diag(ref).astype(np.float64))
+    refn = ref.astype(np.float64) / (d[:, None] * d[None, :])
+    np.fill_diagonal(refn, 1.0)
+    assert np.array_equal(Kn, refn)
+    n, ldc = codes.shape
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(n * n * 4)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.memset(d_out, 0xA5, n * n * 4)
+        ctx.gram_device(P.make(L.KMG_SPECTRUM, k=8), d_codes, d_lens, n, ldc, 100, 900, L.KMG_I32,
+                        d_out, n)
+        ctx.synchronize()
+        rows = np.empty((800, n), dtype=np.int32)
+        ctx.d2h(rows, d_out)
+        assert np.array_equal(rows.astype(np.int64), ref[100:900])
+        ctx.memset(d_out, 0xA5, n * n * 4)
+        for r in range(3):
+            ctx.gram_blocks(P.make(L.KMG_SPECTRUM, k=8), d_codes, d_lens, n, ldc, L.KMG_I32, d_out,
+                            n, 3, r, 100, 0)
+        ctx.synchronize()
+        full = np.empty((n, n), dtype=np.int32)
+        ctx.d2h(full, d_out)
+        assert np.array_equal(full.astype(np.int64), ref)
+    finally:
+        for p_ in (d_out, d_codes, d_lens):
+            ctx.dfree(p_)
