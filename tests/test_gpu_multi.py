@@ -308,12 +308,12 @@ def _colblock_assembly(ctx, data, params, dt, world, block, gather):
         ctx.dfree(d_out)
 
 
-@pytest.mark.parametrize("case", [1, 2])
+@pytest.mark.parametrize("case", [0, 1, 2])
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_column_block_assembly_equals_full(ctx, data, case, world):
     """gather = 6 (the one-GPU rehearsal of gather = 5): every rank's column block K[:, C_q]
-    (lists over its own sequences) computed, transposed into K's rows C_q: exactly the
-    single-call K (the buffer starts poisoned), the packed lists included."""
+    (lists / postings over its own sequences) computed, transposed into K's rows C_q:
+    exactly the single-call K (the buffer starts poisoned), spectrum and mismatch."""
     params, dt = CASES[case]
     codes, lens = data[0], data[1]
     n = codes.shape[0]
@@ -321,7 +321,7 @@ def test_column_block_assembly_equals_full(ctx, data, case, world):
     block = -(-n // world)
     got = _colblock_assembly(ctx, data, params, dt, world, block, 6)
     assert np.array_equal(got, full)
-    assert ctx.last_plan()["formulation"] == "neighbourhood"
+    assert ctx.last_plan()["formulation"] == ("posting" if case == 0 else "neighbourhood")
 
 
 def test_column_block_assembly_single_rank_comm(ctx, data):
@@ -343,8 +343,8 @@ def test_column_block_assembly_single_rank_comm(ctx, data):
         ctx.comm_destroy()
     with pytest.raises(L.KmgError):  # 3 x 400 rows do not cover n = 1500
         _colblock_assembly(ctx, data, params, dt, 3, 400, 6)
-    with pytest.raises(L.KmgUnsupported):  # column blocks are a mismatch (k, 1) path
-        _colblock_assembly(ctx, data, CASES[0][0], CASES[0][1], 2, 750, 6)
+    with pytest.raises(L.KmgUnsupported):  # column blocks: the posting-list paths only
+        _colblock_assembly(ctx, data, CASES[3][0], CASES[3][1], 2, 750, 6)
 
 
 @pytest.mark.parametrize("world", [2, 8])
