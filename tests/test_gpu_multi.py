@@ -365,3 +365,22 @@ def test_column_block_assembly_n20000(ctx, world):
         ctx.dfree(d_codes)
         ctx.dfree(d_lens)
     assert np.array_equal(got, full)
+
+
+@pytest.mark.parametrize("n,world", [(1, 1), (3, 8), (17, 4)])
+def test_column_block_assembly_tiny(ctx, n, world):
+    """Column-block assembly at sizes where some ranks hold no column (n < world) and a
+    single row: still the one-call K, spectrum and mismatch."""
+    codes, lens = E.synthetic(n, 101, seed=90 + n)
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        for params, dt in (CASES[0], CASES[1]):
+            full = ctx.gram(params, codes, lens, dt)
+            got = _colblock_assembly(ctx, (codes, lens, d_codes, d_lens), params, dt, world,
+                                     -(-n // world), 6)
+            assert np.array_equal(got, full), (n, world)
+    finally:
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
