@@ -134,7 +134,7 @@ int kmg_gram_device(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,
  * of kernels.py:211-215 split by columns), with the neighbourhood lists built over the
  * block's sequences only -- each list read by all n rows.  Mismatch (k, 1), 4 <= k <= 12
  * (get_mismatch_K, kernels.py:196-217), and the spectrum posting-list path (get_spectrum_K,
- * kernels.py:28-47, 6 <= k <= 16: the posting index over the block's sequences only); other
+ * kernels.py:28-47, 6 <= k <= 12: the posting index over the block's sequences only); other
  * kernels return KMG_EUNSUPPORTED.  Runs on the context stream; returns without synchronising.
  */
 int kmg_gram_device_cols(kmg_ctx *ctx, const kmg_params *p, const uint8_t *d_codes,

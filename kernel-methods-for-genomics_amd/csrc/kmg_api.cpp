@@ -991,7 +991,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         if (!(cb_mm || cb_sp) || (dt != KMG_I32 && dt != KMG_F32 && dt != KMG_F64) || after ||
             ranges.size() != 1 || ranges[0].col_lo != 0)
           return fail(KMG_EUNSUPPORTED, "column blocks: mismatch (k, 1) with 4 <= k <= 12, or the "
-                      "spectrum posting-list path (6 <= k <= 16), only");
+                      "spectrum posting-list path (6 <= k <= 12), only");
         if (cb_mm) path = SM_NB;
       }
       const bool use_pairs = path == SM_PAIRS, use_slots = path == SM_SLOTS;
