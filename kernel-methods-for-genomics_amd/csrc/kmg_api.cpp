@@ -146,6 +146,10 @@ struct Tuning {
   int sp_store = 0;         // KMG_SP_STORE: spectrum K stores, 0 auto, 1 non-temporal, 2 plain
   int sp_order = 1;         // KMG_SP_ORDER: spectrum grid, 0 row-major, 1 chunk-major (N=100000:
                             // Gram 6.66 -> 5.85 ms, interleaved A/B profiles/r02aq_sp_order_ab.jsonl)
+  int sp_rows = 0;          // KMG_SP_ROWS: spectrum rows per workgroup, 1, 2 or 4 (full-width
+                            // dtypes), 0 auto: 2 for a single-chunk launch (column block 12500
+                            // wide: Gram 1.18 -> 0.88 ms; full K and row shares neutral,
+                            // profiles/r06j_rows*_ab.jsonl), else 1
   int dense_sb = 0;         // KMG_DENSE_SB: dense Gram super-block edge in tiles (0: by F panel size)
   int dense_bk = 128;       // KMG_DENSE_BK: dense Gram k-stage bytes, 64 or 128 (128: half the
                             // barriers; MM k=7 N=20000 3.38 -> 3.13 ms, k=6 0.92 -> 0.87,
@@ -192,6 +196,7 @@ void read_tuning(Tuning &t) {
   t.la_lpp = env_or("KMG_LA_LPP", d.la_lpp);
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
+  t.sp_rows = env_or("KMG_SP_ROWS", d.sp_rows);
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   t.dense_half = env_or("KMG_DENSE_HALF", d.dense_half);
@@ -1286,7 +1291,7 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
       KMG_TRY(each_range(c, ranges, o, after, [&](int64_t r0, int64_t r1, const OutSpec &oq) {
         return exact ? launch_gram_spectrum(gi, pkd, c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                             r0, r1, oq, c->stream, c->tune.sp_store,
-                                            c->tune.sp_order)
+                                            c->tune.sp_order, c->tune.sp_rows)
                      : launch_gram_mismatch1_slots(g, pkd, c->slots.as<uint4>(),
                                                    c->off.as<uint32_t>(), c->ent.as<uint16_t>(),
                                                    r0, r1, (int)w[0], (int)w[1], (int)w[2], oq,

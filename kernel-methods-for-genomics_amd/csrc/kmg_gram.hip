@@ -50,26 +50,39 @@ __device__ __forceinline__ uint32_t drop_letter_g(uint32_t code, int p, int k) {
 // the row (int32 / float32: 4 columns a lane; float64: 2), so every line is written whole.
 // NT: non-temporal stores (measured faster for multi-chunk and float64 K; plain stores
 // faster for a single-chunk int32 K, profiles/r02t_sp_store.jsonl).
-template <bool PACK16, int DT, bool NT>
+// ROWS > 1 (KMG_SP_ROWS; full-width dtypes only): one workgroup owns ROWS consecutive rows of
+// the chunk, their accumulators side by side in LDS, the windows of all its rows over its lane
+// groups, so the per-workgroup costs (accumulator clear, descriptors, barriers) are shared.
+template <bool PACK16, int DT, bool NT, int ROWS>
 __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
                                                        const uint32_t *__restrict__ off,
                                                        const uint16_t *__restrict__ ent,
-                                                       int64_t row0, int64_t cm_rows, OutSpec o) {
-  extern __shared__ __align__(16) uint32_t acc[];
-  // cm_rows > 0: chunk-major grid (all rows of chunk 0 first, so the lists in flight all
+                                                       int64_t row0, int64_t rows,
+                                                       int chunk_major, OutSpec o) {
+  extern __shared__ __align__(16) uint32_t acc_all[];
+  // chunk_major: chunk-major grid (all rows of chunk 0 first, so the lists in flight all
   // belong to one chunk's slice of the index: 3.7 MB at N=100000 instead of all 18.6 MB,
   // which the XCD's L2 keeps despite the K stores streaming through it; FETCH_SIZE 4.5 ->
   // 0.96 GB per launch, config 4 Gram 6.66 -> 5.85 ms = 6.8 TB/s), else row-major
-  const int64_t il = cm_rows > 0 ? (int64_t)blockIdx.x % cm_rows : blockIdx.x / g.nchunks;
-  const int64_t i = row0 + il;
-  const int c = cm_rows > 0 ? (int)((int64_t)blockIdx.x / cm_rows) : (int)(blockIdx.x - il * g.nchunks);
+  const int64_t groups = (rows + ROWS - 1) / ROWS;  // row groups of the launch
+  const int64_t gl = chunk_major ? (int64_t)blockIdx.x % groups : blockIdx.x / g.nchunks;
+  const int c = chunk_major ? (int)((int64_t)blockIdx.x / groups) : (int)(blockIdx.x - gl * g.nchunks);
+  const int64_t il0 = gl * ROWS;
+  const int nr = (int)min((int64_t)ROWS, rows - il0);  // rows of this workgroup
   const int64_t col0 = (int64_t)c * g.chunk;
   const int cw = (int)min((int64_t)g.chunk, g.n - col0);
   if (col0 + cw <= o.col_lo) return;  // the whole chunk lies below the written columns
   const int words = PACK16 ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
-  const uint32_t *__restrict__ srec = pk.w + i * pk.ldp;
   const uint32_t *__restrict__ o_c = off + (size_t)c * g.nkeys;
   const uint4 *__restrict__ e4 = (const uint4 *)ent;
+  const int nwr = nr * g.pmax;  // windows of the workgroup's rows
+  // lanes per window: a power of two, >= 2, so that the windows of the rows fill the block
+  int lpw = 2;
+  while (lpw < 16 && (lpw << 1) * ROWS * g.pmax <= (int)blockDim.x) lpw <<= 1;
+  const int sub = threadIdx.x & (lpw - 1);
+  const int nwin = blockDim.x / lpw;
+  int a = threadIdx.x / lpw;
+  uint32_t *acc = acc_all;  // the accumulator of window a's row
   auto add = [&](uint32_t j0) {
     if (PACK16)
       atomicAdd(&acc[j0 >> 1], 1u << ((j0 & 1) << 4));
@@ -85,27 +98,26 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
       if (rel < len) add((w[h >> 1] >> ((h & 1) * 16)) & 0xFFFFu);
     }
   };
-  // lanes per window: a power of two, >= 2, so that the windows of a row fill the block
-  int lpw = 2;
-  while (lpw < 16 && (lpw << 1) * g.pmax <= (int)blockDim.x) lpw <<= 1;
-  const int sub = threadIdx.x & (lpw - 1);
-  const int nwin = blockDim.x / lpw;
-  int a = threadIdx.x / lpw;
-  uint32_t beg = 0, len = 0;
-  if (a < g.pmax) {
-    const uint32_t u = pk_window(srec, pk.cw, a, g.k);
+  auto window = [&](int aw, uint32_t &b, uint32_t &l) {  // window aw: list + accumulator
+    const int r = ROWS == 1 ? 0 : aw / g.pmax;
+    const int aa = aw - r * g.pmax;
+    acc = acc_all + r * words;
+    l = 0;
+    const uint32_t u = pk_window(pk.w + (row0 + il0 + r) * pk.ldp, pk.cw, aa, g.k);
     if (u != KMG_INVALID) {
-      beg = o_c[u];
-      len = o_c[u + 1] - beg;
+      b = o_c[u];
+      l = o_c[u + 1] - b;
     }
-  }
+  };
+  uint32_t beg = 0, len = 0;
+  if (a < nwr) window(a, beg, len);
   uint32_t q0 = beg >> 3;
   uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0;
   // only pieces that hold entries of the list are read
   if (len && 8u * (q0 + sub) < beg + len) p0 = e4[q0 + sub];
   if (len && 8u * (q0 + sub + lpw) < beg + len) p1 = e4[q0 + sub + lpw];
-  uint4 *acc4 = (uint4 *)acc;
-  for (int w = threadIdx.x; w < (words >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
+  uint4 *acc4 = (uint4 *)acc_all;
+  for (int w = threadIdx.x; w < ((ROWS * words) >> 2); w += blockDim.x) acc4[w] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   for (;;) {
     if (len) {
@@ -114,13 +126,8 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
       for (uint32_t q = q0 + 2 * lpw + sub; 8u * q < beg + len; q += lpw) piece(e4[q], q, beg, len);
     }
     a += nwin;
-    if (a >= g.pmax) break;  // more windows than lane groups (long sequences)
-    len = 0;
-    const uint32_t u = pk_window(srec, pk.cw, a, g.k);
-    if (u != KMG_INVALID) {
-      beg = o_c[u];
-      len = o_c[u + 1] - beg;
-    }
+    if (a >= nwr) break;  // more windows than lane groups (long sequences)
+    window(a, beg, len);
     q0 = beg >> 3;
     if (len && 8u * (q0 + sub) < beg + len) p0 = e4[q0 + sub];
     if (len && 8u * (q0 + sub + lpw) < beg + len) p1 = e4[q0 + sub + lpw];
@@ -129,6 +136,9 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
 
   const bool norm = o.normalize && o.diagv[0] != 1.0;
   const int qs = (int)max((int64_t)0, o.col_lo - col0);  // a multiple of 8 (host check)
+  for (int r = 0; r < nr; ++r) {
+  acc = acc_all + r * words;
+  const int64_t il = il0 + r, i = row0 + il;
   if constexpr (DT == KMG_U8) {
     // raw off-diagonal counts as uint8, diagonal column stored as 0 (see emit_row), 16
     // columns = 16 B per lane and step from the packed 16-bit counters
@@ -233,6 +243,7 @@ __global__ __launch_bounds__(1024) void gram_sp_kernel(IndexGeom g, Packed pk,
       emit4<DT, NT>(o, il, i, col0 + q, min(4, cw - q), v0, v1, v2, v3, norm);
     }
   }
+  }  // rows of the workgroup
 }
 
 // ------------------------------------------------------------------ mismatch m=1
@@ -1245,7 +1256,7 @@ hipError_t launch_transpose(const void *M, int64_t ldm, int64_t rows, int64_t w,
 
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
-                                hipStream_t s, int store, int order) {
+                                hipStream_t s, int store, int order, int rows_per) {
   const int64_t rows = row1 - row0;
   if (rows <= 0 || g.n == 0) return hipSuccess;
   if (o.tri) return hipErrorInvalidValue;  // (the spectrum grid has its own row orders)
@@ -1253,29 +1264,43 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   if (nblk * 1024 >= (1LL << 32)) return hipErrorInvalidValue;  // AQL grid size is 32-bit
   const bool pack = g.pmax <= 255;
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
-  const size_t lds = (size_t)words * 4;
-  const dim3 grid((unsigned)nblk);
+  // rows a workgroup (KMG_SP_ROWS 0 auto, 2 or 4): full-width dtypes, all accumulators in LDS
+  if (rows_per == 0) rows_per = g.nchunks == 1 ? 2 : 1;  // auto (kmg_api.cpp Tuning::sp_rows)
+  int rpw = (rows_per == 2 || rows_per == 4) && o.dtype != KMG_U16 && o.dtype != KMG_U8 ? rows_per : 1;
+  while (rpw > 1 && (size_t)rpw * words * 4 > 160 * 1024) rpw >>= 1;
+  const size_t lds = (size_t)words * 4 * rpw;
+  const int64_t nb = rpw > 1 ? ((rows + rpw - 1) / rpw) * g.nchunks : nblk;
+  const dim3 grid((unsigned)nb);
   // store policy: 0 auto (plain for a single-chunk int32 K, else non-temporal), 1 NT, 2 plain
   const bool nt = store == 1 || (store == 0 && !(o.dtype == KMG_I32 && g.nchunks == 1));
-  const int64_t cmr = (order == 1 && g.nchunks > 1) ? rows : 0;
+  const int cmj = (order == 1 && g.nchunks > 1) ? 1 : 0;
   if (o.dtype == KMG_U16 || o.dtype == KMG_U8) {  // raw round slab (kmg_gram_blocks)
     if (!pack) return hipErrorInvalidValue;
     if (o.dtype == KMG_U16)
-      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U16, false>), grid, dim3(1024), lds, s, g, pk,
-                         off, ent, row0, cmr, o);
+      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U16, false, 1>), grid, dim3(1024), lds, s, g, pk,
+                         off, ent, row0, rows, cmj, o);
     else
-      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U8, false>), grid, dim3(1024), lds, s, g, pk,
-                         off, ent, row0, cmr, o);
+      hipLaunchKernelGGL((gram_sp_kernel<true, KMG_U8, false, 1>), grid, dim3(1024), lds, s, g, pk,
+                         off, ent, row0, rows, cmj, o);
     return hipGetLastError();
   }
-#define KMG_SP(PK, NTV)                                                                       \
-  KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<PK, D, NTV>), grid, dim3(1024), \
-                                              lds, s, g, pk, off, ent, row0, cmr, o))
-  if (pack) {
-    if (nt) { KMG_SP(true, true); } else { KMG_SP(true, false); }
-  } else {
-    if (nt) { KMG_SP(false, true); } else { KMG_SP(false, false); }
+#define KMG_SP(PK, NTV, R)                                                                        \
+  KMG_DISPATCH_DT(o.dtype, hipLaunchKernelGGL((gram_sp_kernel<PK, D, NTV, R>), grid, dim3(1024),  \
+                                              lds, s, g, pk, off, ent, row0, rows, cmj, o))
+#define KMG_SP_R(R)                                                                    \
+  if (pack) {                                                                          \
+    if (nt) { KMG_SP(true, true, R); } else { KMG_SP(true, false, R); }                \
+  } else {                                                                             \
+    if (nt) { KMG_SP(false, true, R); } else { KMG_SP(false, false, R); }              \
   }
+  if (rpw == 4) {
+    KMG_SP_R(4)
+  } else if (rpw == 2) {
+    KMG_SP_R(2)
+  } else {
+    KMG_SP_R(1)
+  }
+#undef KMG_SP_R
 #undef KMG_SP
   return hipGetLastError();
 }

@@ -228,7 +228,7 @@ hipError_t launch_tri_patch8(const uint4 *esc, const uint32_t *counts, int nsets
                              const double *diagv, const double *dsq, hipStream_t s);
 hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint32_t *off,
                                 const uint16_t *ent, int64_t row0, int64_t row1, const OutSpec &o,
-                                hipStream_t s, int store = 0, int order = 0);
+                                hipStream_t s, int store = 0, int order = 0, int rows_per = 0);
 // mismatch (k,1), 8 <= k <= 12, on the slot layout (one line per list)
 hipError_t launch_gram_mismatch1_slots(const IndexGeom &g, const Packed &pk, const uint4 *slots,
                                        const uint32_t *off, const uint16_t *ent, int64_t row0,
