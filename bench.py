@@ -12,10 +12,14 @@ Multi-GPU: one process per GPU.  `python bench.py --gpus G` starts the G rank pr
 itself (launch_ranks: rank r on device r, rendezvous on 127.0.0.1, rank 0's JSON line
 relayed, non-zero exit if any rank fails); under `python -m torch.distributed.run
 --nproc-per-node G bench.py --gpus G` the launcher's environment is used as is, and a
-WORLD_SIZE different from --gpus is an error.  The rows of K are independent, so the headline shards them
-with no data-path collective and scales STRONGLY at the north-star's named N = 100000:
-every GPU builds the replicated index and computes its 1/G share of the rows x all N
-columns, packed in its own buffer; `value` = N^2 / max-over-ranks step time.  The
+WORLD_SIZE different from --gpus is an error.  The rows of K are independent and K is
+symmetric, so the headline shards K with no data-path collective and scales
+STRONGLY at the north-star's named N = 100000: every GPU computes its 1/G share -- at
+G = 2 its rows x all N columns (the replicated index), at G >= 4 all N rows x its columns
+as one column chunk (the index over its own sequences; share_mode: the faster shape
+there, the other one reported as `other_share`) -- in its own buffer; `value` = N^2 /
+max-over-ranks step time.  At G = 1 the G = 2 / 4 / 8 shares are also timed on the one GPU
+(`shares_measured`: a collective-free rank's time is the job's).  The
 north-star's final RCCL all-gather is measured beside it at the same N (`assembled`:
 upper-triangle uint8 round slabs all-gathered in place over RCCL/xGMI on a second stream
 while the next round is computed, every GPU unpacking / mirroring them into the whole K),
@@ -448,7 +452,7 @@ def reference_model_s(kind, n):
 
 # ----------------------------------------------------------------------- N = 1 extras
 def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, oracle_row,
-             cols=None):
+             cols=None, timing=True):
     """One workload on rows [r0, r1) x all n columns, device-resident, one launch set;
     cols = (c0, c1): instead the column block K[:, c0:c1] of every row (kmg_gram_device_cols;
     the same pairs as rows [c0, c1) x all n, K being symmetric), spot rows checked on it."""
@@ -472,7 +476,7 @@ def run_slab(ctx, params, out_dtype, n, seed, r0, r1, steps, warmup, spot_rows, 
         for _ in range(warmup):
             step()
         ctx.synchronize()
-        ctx.set_timing(True)
+        ctx.set_timing(timing)  # (2: events around the Gram launches only)
         ctx.timing_reset()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -547,6 +551,122 @@ def run_colblock_dist(ctx, dist, params, out_dtype, n, seed, steps, warmup, orac
     ms = t / steps * 1e3
     return {"N": n, "cols_this_rank": w, "steps": steps, "ms_per_step": ms,
             "pairs_per_s": n * n / (ms / 1e3), "plan": plan, "spot_check": ok}
+
+
+# widest spectrum share taken as a column block: the library makes a block this wide or
+# narrower one column chunk (kmg_api.cpp Tuning::sp_cb_chunk), the fastest share shape
+# measured at G >= 4 (N=100000: G=4 1.73 vs 1.81-1.85 ms, G=8 0.95-0.97 vs 1.02-1.06 ms as
+# row shares; at G=2 the 50000-row share is faster; profiles/r06k_*)
+SP_COLSHARE_MAX = 32768
+
+
+def share_mode(n, world):
+    """The headline's per-rank share at G ranks: "cols" (K[:, C_r], one column chunk) when
+    the rank's columns fit one chunk, else "rows" (K[R_r, :])."""
+    return "cols" if world > 1 and -(-n // world) <= SP_COLSHARE_MAX else "rows"
+
+
+def run_colshare(ctx, dist, name, params, out_dtype, n, seed, steps, warmup, oracle_row,
+                 world=None, rank=None):
+    """Timed column-block shares (kmg_gram_device_cols): rank r computes K[:, C_r] of all n
+    rows, C_r = rank_rows(n, G, r) -- by symmetry the row share K[C_r, :], column-major.
+    world / rank given: that rank's share of a G-rank job timed on this one GPU (the
+    collective-free build has no exchange, so its per-rank time is the job's).  Timed like
+    run_build: HIP events around the Gram launch, barrier + synchronise on both sides, the
+    max over ranks; spot rows against the oracle (first, last, the block's own diagonal)."""
+    codes, lens = E.synthetic(n, 101, seed=seed)
+    ldc = codes.shape[1]
+    esz = np.dtype(L.DTYPES[out_dtype]).itemsize
+    world = dist.world if world is None else world
+    rank = dist.rank if rank is None else rank
+    c0, c1 = rank_rows(n, world, rank)
+    w = c1 - c0
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    ctx.h2d(d_codes, codes)
+    ctx.h2d(d_lens, lens)
+    d_out = ctx.dmalloc(max(1, n * w * esz))
+    res = {"name": name, "N": n, "share": "cols", "world": world, "rank": rank,
+           "cols_this_rank": w, "col_range": [c0, c1]}
+    try:
+        def step():
+            ctx.gram_device_cols(params, d_codes, d_lens, n, ldc, c0, c1, out_dtype, d_out, w)
+
+        for _ in range(warmup):
+            step()
+        ctx.synchronize()
+        ctx.set_timing(2)
+        ctx.timing_reset()
+        dist.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.synchronize()
+        dist.barrier()
+        t = dist.max(time.perf_counter() - t0) / steps
+        kern = stage_means(ctx)
+        ctx.set_timing(True)
+        ctx.timing_reset()
+        for _ in range(min(steps, 5)):
+            step()
+        ctx.synchronize()
+        stages = stage_means(ctx)
+        ctx.set_timing(False)
+        stages.update(kern)
+        res.update({"ms_per_step": t * 1e3, "pairs_per_s": n * n / t, "stages_ms": stages,
+                    "plan": ctx.last_plan()})
+        rows = sorted({0, n - 1, c0, c1 - 1})
+        ok = True
+        for r in rows:
+            row = np.empty(w, dtype=L.DTYPES[out_dtype])
+            ctx.d2h(row, ctypes.c_void_p(d_out.value + r * w * esz))
+            ref = oracle_row(codes, lens, r)[c0:c1]
+            ok &= bool(np.array_equal(row.astype(ref.dtype), ref))
+        res["spot_check_rows"] = rows
+        res["spot_check"] = dist.all_true(ok)
+    finally:
+        ctx.dfree(d_out)
+        ctx.dfree(d_codes)
+        ctx.dfree(d_lens)
+    return res
+
+
+def measured_shares(ctx, dist, n, seed, steps, warmup, full_ms):
+    """The headline's G = 2 / 4 / 8 per-rank shares timed on this one GPU (rank 0's, in the
+    shape share_mode picks): the collective-free G-rank build exchanges nothing, so a rank's
+    time is the job's, and full / share is its strong-scaling speedup -- measured, not
+    modelled (each GPU of a node at its own clocks and HBM)."""
+    out = {}
+    params = P.make(L.KMG_SPECTRUM, k=8)
+    for g in (2, 4, 8):
+        mode = share_mode(n, g)
+        if mode == "cols":
+            r = run_colshare(ctx, dist, "spectrum_k8", params, L.KMG_I32, n, seed, steps, warmup,
+                             spectrum_row, world=g, rank=0)
+            width = r["cols_this_rank"]
+        else:
+            block = (-(-n // g) + 7) // 8 * 8
+            r = run_slab(ctx, params, L.KMG_I32, n, seed, 0, block, steps, warmup, (0, block - 1),
+                         spectrum_row, timing=2)
+            width = block
+        out[str(g)] = {"share": mode, "rows_or_cols": width, "ms": r["ms_per_step"],
+                       "gram_ms": r["stages_ms"].get("gram"), "speedup": full_ms / r["ms_per_step"],
+                       "spot_check": r["spot_check"]}
+    return out
+
+
+def sp_kernel_name(plan):
+    """The gram_sp_kernel instance a spectrum build at this plan launches (int32 K, L=101:
+    packed 16-bit accumulators; plain stores for one column chunk; two rows a workgroup at
+    chunks <= 16384 columns, launch_gram_spectrum)."""
+    ch, nch = plan.get("chunk") or 0, plan.get("nchunks") or 1
+    return "kmg::gram_sp_kernel<true,1,%s,%d>" % ("false" if nch == 1 else "true",
+                                                  2 if 0 < ch <= 16384 else 1)
+
+
+def spectrum_row(codes, lens, r):
+    import cref
+    return cref.spectrum(codes, lens, 8, rows=(r, r + 1))[0].astype(np.int64)
 
 
 def run_colblock_assembly(ctx, dist, params, out_dtype, n, seed, steps, warmup, oracle_row,
@@ -1142,6 +1262,9 @@ def main():
                     help="G > 1 assembly: 2 upper-triangle slabs + mirror, 1 full rows")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-mismatch", action="store_true")
+    ap.add_argument("--no-weak", action="store_true",
+                    help="skip the weak-scaled G > 1 build (N = n sqrt(G)): for rehearsals with "
+                         "several ranks on one GPU, whose HBM the G weak shares would overfill")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the config 4 / 5, host-path, run.py and downstream lines")
@@ -1218,21 +1341,35 @@ def main():
                 ctx.comm_destroy()
             rccl = False
             rccl_error = rccl_error or "another rank's ncclCommInitRank failed"
-    # headline at every G: the named N = n1 (strong scaling), rows sharded over the ranks
-    # with no data-path collective (the rows of K are independent: SURVEY §8e); at G > 1
-    # the north-star's final RCCL all-gather (K assembled on every GPU) is `assembled` and
-    # the weak-scaled build (N = n1 sqrt(G)) `weak_scaled`
+    # headline at every G: the named N = n1 (strong scaling), K sharded over the ranks with
+    # no data-path collective (the rows of K are independent, and K is symmetric: SURVEY
+    # §8e) -- a rank's 1/G of the rows, or at G >= 4 its 1/G of the columns as one column
+    # chunk (share_mode: the faster shape there); the other shape is `other_share`.  At
+    # G > 1 the north-star's final RCCL all-gather (K assembled on every GPU) is `assembled`
+    # and the weak-scaled build (N = n1 sqrt(G)) `weak_scaled`
     n = n1
-    sp = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
-                   sp_seed, args.steps, args.warmup, check_spectrum, gather=0)
-    sp["rows_per_rank"] = dist.gather(sp["rows_this_rank"])
+    mode = share_mode(n, dist.world)
+    sp_rows = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n,
+                        sp_seed, args.steps, args.warmup, check_spectrum, gather=0)
+    sp_rows["share"] = "rows"
+    sp_rows["rows_per_rank"] = dist.gather(sp_rows["rows_this_rank"])
+    sp_cols = None
+    if dist.world > 1:
+        sp_cols = run_colshare(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32,
+                               n, sp_seed, args.steps, args.warmup, spectrum_row)
+        sp_cols["cols_per_rank"] = dist.gather(sp_cols["cols_this_rank"])
+    sp, sp_other = (sp_cols, sp_rows) if mode == "cols" else (sp_rows, sp_cols)
     sp["devices_per_rank"] = dist.gather(ctx.device)
+    shares = None
+    if dist.world == 1 and not args.no_extra:
+        shares = measured_shares(ctx, dist, n, sp_seed, max(10, args.steps), args.warmup,
+                                 sp["ms_per_step"])
     asm = None
     if rccl:
         asm = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, n1,
                         sp_seed, args.steps, args.warmup, check_spectrum)
     weak = None
-    if dist.world > 1:
+    if dist.world > 1 and not args.no_weak:
         nw = weak_scaled_n(n1, dist.world)
         weak = run_build(ctx, dist, "spectrum_k8", P.make(L.KMG_SPECTRUM, k=8), L.KMG_I32, nw,
                          2, args.steps, args.warmup, check_spectrum, gather=0)
@@ -1271,14 +1408,16 @@ def main():
 
     # roofline of the dominant kernel: gram_sp_kernel, one launch per round
     st = sp["stages_ms"]
-    rows_per_launch = sp["rows_this_rank"] / max(1, st.get("gram_launches", 1) /
-                                                  max(1, args.steps))
-    alg_bytes = 4.0 * rows_per_launch * n + 52.0 * n  # int32 K write + packed input read
+    launches = max(1, st.get("gram_launches", 1) / max(1, args.steps))
+    # K entries a launch writes: rows x all N (row share) or all N rows x the rank's columns
+    out_per_launch = (sp["rows_this_rank"] * n if mode == "rows" else n * sp["cols_this_rank"]) / launches
+    alg_bytes = 4.0 * out_per_launch + 52.0 * n  # int32 K write + packed input read
     kern_s = st["gram"] / 1e3
     achieved = alg_bytes / kern_s
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK, "traffic": load_traffic("spectrum_k8", n),
-            "kernel": "kmg::gram_sp_kernel<true,1,%s>" % ("true" if n > 24576 else "false"),
+            "frac": achieved / HBM_PEAK,
+            "traffic": load_traffic("spectrum_k8", n) if dist.world == 1 else None,
+            "kernel": sp_kernel_name(sp.get("plan") or {}),
             "kernel_ms": st["gram"],
             "alg_bytes_per_launch": alg_bytes,
             # hipMemsetAsync over the same K buffer in the same run: a reference rate, not a
@@ -1298,18 +1437,33 @@ def main():
         "vs_baseline": None, "dtype": "int32",
         "data": "synthetic i.i.d. uniform ACGT, L=101, numpy default_rng(%d)" % (4 if n == 100000 else 2),
         "config": {"workload": "spectrum k=8 full-K build, N=%d x L=101 (BASELINE configs[3], the "
-                               "north_star's target config; G>1: each GPU its 1/G of the rows x "
-                               "all N columns, no data-path collective, K assembled over RCCL "
-                               "measured as `assembled`)" % n,
-                   "N": n, "L": 101, "k": 8,
-                   "rows_this_rank": sp["rows_this_rank"],
-                   "rows_per_rank": sp["rows_per_rank"],
+                               "north_star's target config; G>1: each GPU its 1/G share of K -- "
+                               "rows K[R_g, :] at G=2, columns K[:, C_g] as one column chunk at "
+                               "G>=4 -- no data-path collective, K assembled over RCCL measured "
+                               "as `assembled`)" % n,
+                   "N": n, "L": 101, "k": 8, "share": mode,
+                   **({"rows_this_rank": sp["rows_this_rank"],
+                       "rows_per_rank": sp["rows_per_rank"], "block_rows": sp["block_rows"]}
+                      if mode == "rows" else
+                      {"cols_this_rank": sp["cols_this_rank"],
+                       "cols_per_rank": sp["cols_per_rank"]}),
                    "devices_per_rank": sp["devices_per_rank"],
                    "rccl": rccl, "rccl_error": rccl_error,
-                   "block_rows": sp["block_rows"], "parallelism": f"row-blocks x{dist.world}",
+                   "parallelism": f"{'row' if mode == 'rows' else 'column'}-blocks x{dist.world}",
                    "out_dtype": "int32", "full_k_build_ms": sp["ms_per_step"]},
         "stages_ms": sp["stages_ms"], "roofline": roof, "spot_check": sp["spot_check"],
     }
+    if shares:
+        # the G-rank headline's per-rank share, timed here (collective-free: its time is the
+        # job's); speedup = the one-GPU full build / the share
+        line["shares_measured"] = {g: {"share": v["share"], "ms": _r(v["ms"]),
+                                       "speedup": _r(v["speedup"], 3), "spot_check": v["spot_check"]}
+                                   for g, v in shares.items()}
+    if sp_other:
+        line["other_share"] = {"share": sp_other["share"], "ms_per_step": sp_other["ms_per_step"],
+                               "pairs_per_s": sp_other["pairs_per_s"],
+                               "gram_ms": sp_other["stages_ms"].get("gram"),
+                               "spot_check": sp_other["spot_check"]}
     if asm:
         # the north-star's assembly: N = n1, block-cyclic rows, upper-triangle uint8 round
         # slabs (escape list) all-gathered in place over RCCL + local unpack / mirror, so

@@ -147,9 +147,11 @@ struct Tuning {
   int sp_order = 1;         // KMG_SP_ORDER: spectrum grid, 0 row-major, 1 chunk-major (N=100000:
                             // Gram 6.66 -> 5.85 ms, interleaved A/B profiles/r02aq_sp_order_ab.jsonl)
   int sp_rows = 0;          // KMG_SP_ROWS: spectrum rows per workgroup, 1, 2 or 4 (full-width
-                            // dtypes), 0 auto: 2 for a single-chunk launch (column block 12500
-                            // wide: Gram 1.18 -> 0.88 ms; full K and row shares neutral,
-                            // profiles/r06j_rows*_ab.jsonl), else 1
+                            // dtypes), 0 auto: 2 for chunks <= 16384 columns (the 12500-column
+                            // block: Gram 1.18 -> 0.88 ms; at 20000- and 25000-column chunks
+                            // neutral or slower, profiles/r06j_rows*_ab.jsonl, r06k_*), else 1
+  int sp_cb_chunk = 32768;  // KMG_SP_CB_CHUNK: spectrum column blocks this wide or narrower
+                            // are one column chunk (kmg_gram_device_cols)
   int dense_sb = 0;         // KMG_DENSE_SB: dense Gram super-block edge in tiles (0: by F panel size)
   int dense_bk = 128;       // KMG_DENSE_BK: dense Gram k-stage bytes, 64 or 128 (128: half the
                             // barriers; MM k=7 N=20000 3.38 -> 3.13 ms, k=6 0.92 -> 0.87,
@@ -197,6 +199,7 @@ void read_tuning(Tuning &t) {
   t.sp_store = env_or("KMG_SP_STORE", d.sp_store);
   t.sp_order = env_or("KMG_SP_ORDER", d.sp_order);
   t.sp_rows = env_or("KMG_SP_ROWS", d.sp_rows);
+  t.sp_cb_chunk = env_or("KMG_SP_CB_CHUNK", d.sp_cb_chunk);
   t.dense_sb = env_or("KMG_DENSE_SB", d.dense_sb);
   t.dense_bk = env_or("KMG_DENSE_BK", d.dense_bk);
   t.dense_half = env_or("KMG_DENSE_HALF", d.dense_half);
@@ -1250,7 +1253,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         g.nkeys = (uint32_t)pow4(k);
         gi = g;
         gi.n = ncols;
-        choose_chunks(gi, std::min(65536, c->tune.sp_chunk));
+        // a column block of up to KMG_SP_CB_CHUNK columns is ONE chunk: N=100000, the G=4
+        // block (25000 columns) 2.06 -> 1.73 ms against two chunks of 12504
+        // (profiles/r06k_colblock_rows_g24.jsonl); wider blocks and full rows keep
+        // KMG_SP_CHUNK (a 25000-column chunk's index slice outgrows the XCD's L2: full K
+        // 6.3 -> 7.4 ms, profiles/r06k_colblock_chunk_g2.jsonl)
+        const int maxc = colblk && ncols <= c->tune.sp_cb_chunk ? c->tune.sp_cb_chunk : c->tune.sp_chunk;
+        choose_chunks(gi, std::min(65536, maxc));
         g.chunk = gi.chunk;
         g.nchunks = gi.nchunks;
       } else {

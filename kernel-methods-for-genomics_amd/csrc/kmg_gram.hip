@@ -1265,7 +1265,7 @@ hipError_t launch_gram_spectrum(const IndexGeom &g, const Packed &pk, const uint
   const bool pack = g.pmax <= 255;
   const int words = pack ? (((g.chunk + 7) >> 3) << 2) : (((g.chunk + 3) >> 2) << 2);
   // rows a workgroup (KMG_SP_ROWS 0 auto, 2 or 4): full-width dtypes, all accumulators in LDS
-  if (rows_per == 0) rows_per = g.nchunks == 1 ? 2 : 1;  // auto (kmg_api.cpp Tuning::sp_rows)
+  if (rows_per == 0) rows_per = g.chunk <= 16384 ? 2 : 1;  // auto (kmg_api.cpp Tuning::sp_rows)
   int rpw = (rows_per == 2 || rows_per == 4) && o.dtype != KMG_U16 && o.dtype != KMG_U8 ? rows_per : 1;
   while (rpw > 1 && (size_t)rpw * words * 4 > 160 * 1024) rpw >>= 1;
   const size_t lds = (size_t)words * 4 * rpw;

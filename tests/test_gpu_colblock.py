@@ -172,18 +172,34 @@ def test_column_block_packed_float64_n20000(ctx, tune):
     assert np.array_equal(Kn, ref)
 
 
+# (KMG_SP_CB_CHUNK, KMG_SP_ROWS): blocks as one chunk (the default) or as 64-column chunks,
+# one / two / four rows a workgroup (0: by chunk width)
+SP_CB_TUNES = [("32768", "0"), ("64", "0"), ("64", "1"), ("32768", "2"), ("64", "4")]
+
+
 @pytest.mark.parametrize("k", [6, 8, 12])
-def test_spectrum_column_blocks_vs_full(ctx, k):
+@pytest.mark.parametrize("cb_chunk,rows", SP_CB_TUNES)
+def test_spectrum_column_blocks_vs_full(ctx, tune, k, cb_chunk, rows):
     """Spectrum column blocks (get_spectrum_K, kernels.py:28-47): the posting index over the
     block's sequences only, every row; int32 raw and float64 normalised blocks equal the
-    columns of the single-call K bit for bit (ragged rows: lengths 60..101)."""
-    codes, lens = E.synthetic(900, 101, seed=300 + k)
+    columns of the single-call K bit for bit (ragged rows: lengths 60..101), whether a block
+    is one column chunk or several and whatever the rows a workgroup (odd row counts leave
+    a workgroup one row short)."""
+    codes, lens = E.synthetic(901, 101, seed=300 + k)
     lens[::7] = 60 + (np.arange(len(lens[::7])) % 41)
     full = ctx.gram(P.make(L.KMG_SPECTRUM, k=k), codes, lens, L.KMG_I32)
     fulln = ctx.gram(P.make(L.KMG_SPECTRUM, k=k, normalize=1), codes, lens, L.KMG_F64)
-    for col0, col1 in ((0, 900), (0, 113), (400, 777), (899, 900)):
+    # (a block wider than KMG_SP_CB_CHUNK is chunked by KMG_SP_CHUNK)
+    tune(KMG_SP_CB_CHUNK=cb_chunk, KMG_SP_CHUNK="64" if cb_chunk == "64" else "24576",
+         KMG_SP_ROWS=rows)
+    for col0, col1 in ((0, 901), (0, 113), (400, 777), (900, 901)):
         K = _col_block(ctx, P.make(L.KMG_SPECTRUM, k=k), codes, lens, col0, col1, L.KMG_I32)
-        assert ctx.last_plan()["formulation"] == "posting"
+        plan = ctx.last_plan()
+        assert plan["formulation"] == "posting"
+        if cb_chunk == "64" and col1 - col0 > 64:
+            assert plan["nchunks"] > 1
+        else:
+            assert plan["nchunks"] == 1
         assert np.array_equal(K, full[:, col0:col1]), (col0, col1)
         Kn = _col_block(ctx, P.make(L.KMG_SPECTRUM, k=k, normalize=1), codes, lens, col0, col1,
                         L.KMG_F64)

@@ -568,6 +568,42 @@ def test_rccl_allgather_single_rank(ctx):
             ctx.dfree(p_)
 
 
+@pytest.mark.parametrize("rows", ["1", "2", "4"])
+@pytest.mark.parametrize("chunk", ["304", "24576"])
+def test_spectrum_rows_per_workgroup(ctx, tune, rows, chunk):
+    """gram_sp_kernel with 1, 2 or 4 rows a workgroup (KMG_SP_ROWS), over several column
+    chunks and over one: the full K (int32, float64 normalised) and a row range of odd
+    length (the last workgroup one row short) equal the oracle (get_spectrum_K,
+    kernels.py:28-47; normalize_K, kernels.py:398-415); ragged rows."""
+    codes, lens = E.synthetic(1001, 101, seed=78)
+    lens[::6] = 30 + (np.arange(len(lens[::6])) % 72)
+    tune(KMG_SP_CHUNK=chunk, KMG_SP_ROWS=rows)
+    ref = cref.spectrum(codes, lens, 8)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=8), codes, lens, L.KMG_I32)
+    assert (ctx.last_plan()["nchunks"] > 1) == (chunk == "304")
+    assert np.array_equal(K.astype(np.int64), ref)
+    Kn = ctx.gram(P.make(L.KMG_SPECTRUM, k=8, normalize=1), codes, lens, L.KMG_F64)
+    d = np.sqrt(np.diag(ref).astype(np.float64))
+    refn = ref.astype(np.float64) / (d[:, None] * d[None, :])
+    np.fill_diagonal(refn, 1.0)
+    assert np.array_equal(Kn, refn)
+    n, ldc = codes.shape
+    r0, r1 = 17, 520
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc((r1 - r0) * n * 4)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device(P.make(L.KMG_SPECTRUM, k=8), d_codes, d_lens, n, ldc, r0, r1, L.KMG_I32,
+                        d_out, n)
+        Kr = np.empty((r1 - r0, n), dtype=np.int32)
+        ctx.d2h(Kr, d_out)
+        assert np.array_equal(Kr.astype(np.int64), ref[r0:r1])
+    finally:
+        for p_ in (d_codes, d_lens, d_out):
+            ctx.dfree(p_)
+
+
 def test_spectrum_column_chunks(ctx, tune):
     """Spectrum over several column chunks (the config-4 layout at a small N): full K (int32
     and float64 normalised), a row slab and block-cyclic rows of three ranks (several ranges

@@ -74,3 +74,23 @@ def test_bench_headline_projection_is_strong_at_named_n():
         assert p[g]["N"] == 100000
         assert abs(p[g]["ms_model"] - (0.13 + 6.3 / int(g))) < 1e-9
     assert p["8"]["speedup_model"] > 6.0
+
+
+def test_bench_headline_share_shapes():
+    """The G-rank headline's per-rank share (bench.share_mode): rows at G = 1 and 2; at G >= 4
+    a column block, which the library makes ONE column chunk (KMG_SP_CB_CHUNK = 32768), so
+    every rank's columns fit it; sp_kernel_name names the gram_sp_kernel instance the plan
+    launches (int32 K: plain stores for one chunk; two rows a workgroup at chunks <= 16384)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    import bench
+    from kmgram.shard import rank_rows
+    assert bench.share_mode(100000, 1) == "rows"
+    assert bench.share_mode(100000, 2) == "rows"
+    assert bench.share_mode(100000, 3) == "rows"  # 33334 columns: past one chunk
+    for g in (4, 5, 8, 16):
+        assert bench.share_mode(100000, g) == "cols"
+        widths = [b - a for a, b in (rank_rows(100000, g, r) for r in range(g))]
+        assert sum(widths) == 100000 and max(widths) <= bench.SP_COLSHARE_MAX
+    assert bench.sp_kernel_name({"chunk": 20000, "nchunks": 5}) == "kmg::gram_sp_kernel<true,1,true,1>"
+    assert bench.sp_kernel_name({"chunk": 25000, "nchunks": 1}) == "kmg::gram_sp_kernel<true,1,false,1>"
+    assert bench.sp_kernel_name({"chunk": 12504, "nchunks": 1}) == "kmg::gram_sp_kernel<true,1,false,2>"

@@ -43,6 +43,8 @@ def main():
         ctx.h2d(dc, codes)
         ctx.h2d(dl, lens)
         steps = case.get("steps", 5)
+        # pre_mb: device memory held while the output is allocated (shifts where it lands)
+        pre = ctx.dmalloc(case["pre_mb"] << 20) if case.get("pre_mb") else None
         cols = case.get("cols")  # [c0, c1]: the column block K[:, c0:c1] (kmg_gram_device_cols)
         if cols:
             c0, c1 = cols
@@ -93,9 +95,11 @@ def main():
             if cols:
                 ref = ref[cols[0]:cols[1]]
             ok = bool(np.array_equal(row.astype(ref.dtype), ref))
-        for p in (do, dc, dl):
+        addr = do.value
+        for p in (do, dc, dl) + ((pre,) if pre else ()):
             ctx.dfree(p)
-        print(json.dumps({"case": case, "ms": wall * 1e3, "stages": st, "check": ok}), flush=True)
+        print(json.dumps({"case": case, "ms": wall * 1e3, "stages": st, "check": ok,
+                          "out_addr": hex(addr)}), flush=True)
     ctx.close()
 
 
