@@ -110,7 +110,13 @@ struct Tuning {
                             // 4 neighbourhood lists (kmg_nbhd.hip); (3, round 3's pair lines,
                             // was removed in round 5: measured slower than the lists at k = 9)
   int nb_threads = 0;       // KMG_NB_THREADS: neighbourhood-list Gram workgroup, 512 / 1024
-                            // (0 auto)
+                            // (0 auto: 512 for a column block -- three workgroups a CU over its
+                            // narrower chunks: config-5 1/8 share raw 19.0 -> 18.0 ms, float64
+                            // 25.3 -> 24.9, N=20000 7000 columns 1.62 -> 1.51; 1024 otherwise,
+                            // two a CU at 20000 columns; profiles/r06n_colblock_threads2.jsonl)
+  int nb_lds512 = 0;        // KMG_NB_LDS512: KB of LDS a 512-thread NB Gram workgroup may take
+                            // when sizing chunks (0 auto: 53, three a CU, for a column block;
+                            // 40, four a CU, otherwise)
   int nb_unroll = 0;        // KMG_NB_UNROLL: 16-byte pieces in flight a lane, NB Gram (4 / 8;
                             // 0 auto: 8, or 4 for an upper-block-triangle build or packed
                             // lists -- profiles/r04x2_nb_unroll_ab.jsonl; column block N=200000
@@ -190,6 +196,8 @@ void read_tuning(Tuning &t) {
   t.wd_form = env_or("KMG_WD_FORM", d.wd_form);
   t.ss_lpp = env_or("KMG_SS_LPP", d.ss_lpp);
   t.nb_threads = env_or("KMG_NB_THREADS", d.nb_threads);
+  t.nb_lds512 = env_or("KMG_NB_LDS512", d.nb_lds512);
+  if (t.nb_lds512 != 0) t.nb_lds512 = std::max(16, std::min(80, t.nb_lds512));
   t.nb_fill = env_or("KMG_NB_FILL", d.nb_fill);
   t.nb_pack_reads = env_or("KMG_NB_PACK_READS", d.nb_pack_reads);
   t.nb_fill_threads = env_or("KMG_NB_FILL_THREADS", d.nb_fill_threads);
@@ -587,13 +595,14 @@ int slot_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz) {
 // 2 esz (nch - 1) / (2 nch) n^2 bytes.  Priced at 6 TB/s for the Gram and 5 TB/s for the
 // mirror.  Largest chunk: the int32 LDS accumulator beside the row tables, and where
 // segment 2 packs, the sorted fill's LDS buffer (nb_sorted_max_chunk: ~24900 at k = 9).
-int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted) {
+int nb_chunk(int64_t n, int pmax, int k, int ldp, int cap, int tri_esz, int threads, bool sorted,
+             int lds512_kb = 40) {
   // two workgroups a CU (their table builds, epilogues and streams overlap; one a CU measured
   // 22 % slower at N=20000, profiles/r05g_*): the accumulator, 16 dummy columns and the row
   // table in 80 KB (1024 threads) or 40 KB (512)
   // (sizing for one workgroup a CU, chunks up to ~40000, measured slower for the config-5
   // slab too: Gram 26.0 -> 30.5 ms, profiles/r05v.jsonl)
-  const int64_t lds_words = (threads == 512 ? 40 : 80) * 1024 / 4;
+  const int64_t lds_words = (threads == 512 ? lds512_kb : 80) * 1024 / 4;
   int64_t max_chunk = (lds_words - 16 - 4 * (int64_t)pmax - 2 - ldp) & ~7LL;
   max_chunk = std::min<int64_t>(max_chunk, 65536 - 128);
   const int smax = sorted ? nb_sorted_max_chunk(k, pmax) : 0;
@@ -1141,7 +1150,8 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
         // gc: the column sequences the lists are built over (all n, or a column block's)
         IndexGeom gc = g;
         gc.n = ncols;
-        const int nbt = c->tune.nb_threads ? c->tune.nb_threads : 1024;
+        const int nbt = c->tune.nb_threads ? c->tune.nb_threads : colblk ? 512 : 1024;
+        const int lds512 = c->tune.nb_lds512 ? c->tune.nb_lds512 : colblk ? 53 : 40;
         // the sorted fill (packed segment 2) where each list is read often enough to repay its
         // sort: reads a list = rows read x windows a row / 4^k (x (nch + 1) / (2 nch) for a
         // square by its block triangle); else 16-bit lists
@@ -1150,13 +1160,13 @@ int gram_device(kmg_ctx *c, const kmg_params *p, const uint8_t *d_codes, const i
           int64_t rows_read = 0;
           for (const RowRange &r : ranges) rows_read += r.row1 - r.row0;
           const int ch = nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
-                                  true);
+                                  true, lds512);
           const int64_t nch = (ncols + ch - 1) / ch;
           const double f = (tri_esz > 0 && nch > 1) ? (double)(nch + 1) / (2.0 * nch) : 1.0;
           sorted = (double)rows_read * g.pmax / (double)pow4(k) * f >= (double)c->tune.nb_pack_reads;
         }
         choose_chunks(gc, nb_chunk(ncols, g.pmax, k, (int)pkd.ldp, c->tune.mm_chunk, tri_esz, nbt,
-                                   sorted));
+                                   sorted, lds512));
         g.chunk = gc.chunk;
         g.nchunks = gc.nchunks;
         o.tri = tri_esz > 0 && g.nchunks > 1;

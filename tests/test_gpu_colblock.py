@@ -38,12 +38,14 @@ def _col_block(ctx, params, codes, lens, col0, col1, dt):
 
 @pytest.mark.parametrize("k", [8, 9, 10])
 @pytest.mark.parametrize("fill", ["0", "1", "4"])
-def test_column_blocks_vs_oracle(ctx, tune, k, fill):
+@pytest.mark.parametrize("threads", ["0", "1024"])
+def test_column_blocks_vs_oracle(ctx, tune, k, fill, threads):
     """Blocks at the start, inside, at the end and of one column; 30 poly-A rows make lists
-    past the fills' LDS buffers (lane-per-run fallbacks)."""
+    past the fills' LDS buffers (lane-per-run fallbacks).  Gram workgroups of 512 threads
+    (the column blocks' default) and of 1024."""
     codes, lens = E.synthetic(700, 101, seed=200 + k)
     codes[:30] = 0
-    tune(KMG_NB_FILL=fill)
+    tune(KMG_NB_FILL=fill, KMG_NB_THREADS=None if threads == "0" else threads)
     raw_p = P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=0)
     if fill == "1" and k == 10:  # segment 2 too sparse to pack: the forced sorted fill refuses
         with pytest.raises(L.KmgUnsupported, match="sorted fill"):
@@ -53,6 +55,7 @@ def test_column_blocks_vs_oracle(ctx, tune, k, fill):
     for col0, col1 in ((0, 700), (0, 123), (250, 611), (699, 700)):
         K = _col_block(ctx, raw_p, codes, lens, col0, col1, L.KMG_I32)
         assert ctx.last_plan()["formulation"] == "neighbourhood"
+        assert ctx.last_plan()["threads"] == (512 if threads == "0" else 1024)
         assert np.array_equal(K.astype(np.int64), ref[:, col0:col1]), (col0, col1)
     Kn = _col_block(ctx, P.make(L.KMG_MISMATCH, k=k, m=1, window=101, normalize=1), codes, lens,
                     250, 611, L.KMG_F64)
@@ -125,7 +128,7 @@ def test_config5_column_block_n200000_full(ctx, c0):
         ctx.synchronize()
         plan = ctx.last_plan()
         assert plan["formulation"] == "neighbourhood" and plan["packed"], plan
-        assert plan["nchunks"] == 2 and not plan["triangle"], plan
+        assert plan["nchunks"] == 2 and not plan["triangle"] and plan["threads"] == 512, plan
         ch = plan["chunk"]
         sums = I.mismatch1_row_sums(codes, k, cols=(c0, c1))
         buf = np.empty((piece, w), dtype=np.int32)
