@@ -604,6 +604,35 @@ def test_spectrum_rows_per_workgroup(ctx, tune, rows, chunk):
             ctx.dfree(p_)
 
 
+@pytest.mark.parametrize("rows", ["1", "2", "4"])
+def test_spectrum_rows_per_workgroup_long_sequences(ctx, tune, rows):
+    """Sequences of 300..700 symbols (more than 255 windows: 32-bit accumulators, so two or
+    four rows a workgroup take 2-4x the LDS and fall back to fewer rows past 160 KB): full K
+    and a column block equal the oracle (get_spectrum_K, kernels.py:28-47)."""
+    codes, lens = E.synthetic(300, 700, seed=79)
+    lens[:] = 300 + (np.arange(300) * 7) % 401
+    tune(KMG_SP_ROWS=rows, KMG_SP_CHUNK="128")
+    ref = cref.spectrum(codes, lens, 7)
+    K = ctx.gram(P.make(L.KMG_SPECTRUM, k=7), codes, lens, L.KMG_I32)
+    assert ctx.last_plan()["nchunks"] > 1
+    assert np.array_equal(K.astype(np.int64), ref)
+    n, ldc = codes.shape
+    c0, c1 = 37, 290
+    d_codes, d_lens = ctx.dmalloc(codes.nbytes), ctx.dmalloc(lens.nbytes)
+    d_out = ctx.dmalloc(n * (c1 - c0) * 4)
+    try:
+        ctx.h2d(d_codes, codes)
+        ctx.h2d(d_lens, lens)
+        ctx.gram_device_cols(P.make(L.KMG_SPECTRUM, k=7), d_codes, d_lens, n, ldc, c0, c1,
+                             L.KMG_I32, d_out, c1 - c0)
+        Kc = np.empty((n, c1 - c0), dtype=np.int32)
+        ctx.d2h(Kc, d_out)
+        assert np.array_equal(Kc.astype(np.int64), ref[:, c0:c1])
+    finally:
+        for p_ in (d_codes, d_lens, d_out):
+            ctx.dfree(p_)
+
+
 def test_spectrum_column_chunks(ctx, tune):
     """Spectrum over several column chunks (the config-4 layout at a small N): full K (int32
     and float64 normalised), a row slab and block-cyclic rows of three ranks (several ranges
